@@ -1,0 +1,152 @@
+/*
+ * imsame_dev.h -- C-ABI drop-in boundary of the MI355X seed-and-extend path.
+ *
+ * Plain C types only (no HIP / torch types).  The reference has no plugin
+ * API: its seam for this path is the pthread worker
+ *     void *computeAlignmentsByThread(void *HashTableArgs)
+ *         /root/reference/src/alignmentFunctions.h:51 (decl), .c:43-208 (body)
+ * fed by the index built inline in main()
+ *         /root/reference/src/IMSAME.c:194-289 (DB load + 12-mer insert)
+ * and the stand-alone tool
+ *         /root/reference/src/reverseComplement.c:21-118.
+ * Each entry point below names the reference code it replaces.
+ *
+ * Ownership: the caller owns every host buffer (borrowed for the call);
+ * the context owns device copies, the index and scratch.  One host thread
+ * per context; contexts on different devices may run concurrently.
+ * Errors are returned as negative IMSAME_E_* codes -- the library never
+ * calls exit() (the reference's terror() does, commonFunctions.c:10-13);
+ * the CLI maps codes back onto the reference's fatal messages.
+ */
+#ifndef IMSAME_DEV_H
+#define IMSAME_DEV_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IMSAME_OK                 0
+#define IMSAME_E_HIP             -1   /* HIP runtime error / no device              */
+#define IMSAME_E_OOM             -2   /* device or host allocation failed           */
+#define IMSAME_E_READ_TOO_LONG   -3   /* xlen or ylen > max_read_size on an e-value
+                                         passing hit: the reference's terror(
+                                         "Read size reached for gapped alignment.")
+                                         alignmentFunctions.c:155                   */
+#define IMSAME_E_ARG             -4   /* bad argument                                */
+#define IMSAME_E_RANGE           -5   /* gap parameters could overflow int32 scores  */
+#define IMSAME_E_PATHS           -6   /* path arena too small (retry with more)      */
+#define IMSAME_E_STATE           -7   /* index / query not loaded                    */
+
+/* Reference constants restated (structs.h:13-19). */
+#define IMSAME_FIXED_K        12
+#define IMSAME_POINT           4
+#define IMSAME_MAX_READ_SIZE 3000
+#define IMSAME_ALIGN_LEN      60
+
+/* Alignment parameters, same meaning and defaults as IMSAME.c:44-49 /
+ * init_args (IMSAME.c:520-578).  igap/egap are the NEGATIVE values the
+ * reference uses internally (CLI "-igap 5" => igap = -5). */
+typedef struct imsame_params {
+    long double min_e;          /* e-value threshold: pass iff e <  min_e   */
+    long double min_coverage;   /* accept iff len/ylen    >= min_coverage  */
+    long double min_identity;   /* accept iff ident/len   >= min_identity  */
+    int64_t     igap;
+    int64_t     egap;
+    uint64_t    max_read_size;  /* IMSAME_MAX_READ_SIZE unless raised (C5)  */
+    uint32_t    want_paths;     /* 1: return alignment paths of accepted reads */
+    uint32_t    reserved;
+} imsame_params;
+
+/* Fill the reference defaults: min_e = 1/powl(10,20), cov = id = 0.5,
+ * igap = -5, egap = -2, max_read_size = 3000, want_paths = 0. */
+void imsame_params_default(imsame_params *p);
+
+/* Per-read outcome, 64 bytes.  For an accepted read the fields describe the
+ * FIRST accepted (read, db record) pair in the reference's visiting order
+ * (alignmentFunctions.c:91-195); for other reads only ylen is set. */
+typedef struct imsame_read_result {
+    uint64_t db_seq;        /* accepted database record (global 0-based index) */
+    int64_t  score;         /* best cell score  (NW bc.score)                   */
+    uint32_t bx, by;        /* best cell        (bc.xpos, bc.ypos)              */
+    uint32_t length;        /* BasicAlignment.length                            */
+    uint32_t identities;    /* BasicAlignment.identities                        */
+    uint32_t igaps, egaps;  /* BasicAlignment.igaps / egaps                     */
+    uint32_t head_x, head_y;/* backtrackingNW ret_head_x / ret_head_y           */
+    uint32_t ylen;          /* read length                                      */
+    uint32_t status;        /* 0 = not found, 1 = accepted                      */
+    uint32_t path_off;      /* first entry of this read's path in the arena     */
+    uint32_t path_len;      /* number of path entries (0 if none)               */
+} imsame_read_result;
+
+/* A path is the backtrack of the accepted alignment, walked from the best
+ * cell towards the origin (backtrackingNW order), as u32 runs:
+ *   bits 31..30 = move (IMSAME_MOVE_*), bits 29..0 = run length / jump size. */
+#define IMSAME_MOVE_DIAG 0u   /* n diagonal steps: X[px],Y[py] pairs           */
+#define IMSAME_MOVE_UP   1u   /* one jump of n rows: X[px..px-n+1] vs '-'      */
+#define IMSAME_MOVE_LEFT 2u   /* one jump of n cols: '-' vs Y[py..py-n+1]      */
+
+typedef struct imsame_stats {
+    uint64_t n_reads;       /* reads processed                       */
+    uint64_t n_accepted;    /* reads accepted                        */
+    uint64_t n_nw;          /* gapped alignments computed            */
+    uint64_t nw_cells;      /* sum xlen*ylen over computed NW         */
+    uint64_t n_hits;        /* ungapped extensions evaluated          */
+    uint64_t rounds;        /* seed->NW rounds                        */
+    uint64_t err_read;      /* IMSAME_E_READ_TOO_LONG: offending read */
+    uint64_t err_dbseq;     /* ... and database record                */
+    double   ms_seed;       /* device time in seed/ungapped kernels   */
+    double   ms_nw;         /* device time in NW kernels              */
+    double   ms_total;      /* wall time of imsame_dev_align          */
+    double   nw_launch_ms;  /* average NW kernel launch duration      */
+    uint64_t nw_launches;
+    uint64_t nw_bytes;      /* algorithmic bytes moved by NW launches */
+} imsame_stats;
+
+typedef struct imsame_ctx imsame_ctx;
+
+/* Open device `device` (HIP ordinal).  Fails with IMSAME_E_HIP if no GPU. */
+int  imsame_dev_open(int device, imsame_ctx **out);
+void imsame_dev_close(imsame_ctx *ctx);
+const char *imsame_strerror(int code);
+
+/* Replaces the 12-mer insert loop IMSAME.c:232-281 (Container + llpos pools,
+ * alignmentFunctions.h:4-6, structs.h:26-30): builds the direct-address
+ * 4^12 bucket index in HBM (CSR; hits visited in the reference's LIFO order).
+ *   db_seq   : ACGT-filtered concatenation (IMSAME.c:216-221), db_len bases
+ *   db_start : n_db record starts (IMSAME.c:200)
+ *   db_brk   : optional bitmap, bit p (LSB-first) = k-mer reset before base p
+ *              (non-ACGT, non-'\n' byte: IMSAME.c:229-231); record starts are
+ *              resets implicitly.  NULL = none besides record starts. */
+int imsame_dev_index(imsame_ctx *ctx, const uint8_t *db_seq, uint64_t db_len,
+                     const uint64_t *db_start, uint64_t n_db, const uint8_t *db_brk);
+
+/* Upload the query (IMSAME.c:320-371 output): ACGT-filtered concatenation
+ * and n_q read starts. */
+int imsame_dev_set_query(imsame_ctx *ctx, const uint8_t *q_seq, uint64_t q_len,
+                         const uint64_t *q_start, uint64_t n_q);
+
+/* Replaces T x computeAlignmentsByThread (alignmentFunctions.c:43-208) over
+ * reads [read_from, read_to) of the loaded query.  n_threads_semantic is the
+ * reference's -n_threads: it fixes the chunk heads {i*floor(n/T)}
+ * (IMSAME.c:414,430-452) whose first k-mer does not borrow the previous
+ * read's last base, so results equal the reference's
+ * for that -n_threads.  res[k] describes read read_from+k.  paths/paths_cap:
+ * u32 arena for want_paths (may be NULL when want_paths == 0). */
+int imsame_dev_align(imsame_ctx *ctx, uint64_t read_from, uint64_t read_to,
+                     uint64_t n_threads_semantic, const imsame_params *prm,
+                     imsame_read_result *res, uint32_t *paths, uint64_t paths_cap,
+                     uint64_t *paths_used, imsame_stats *stats);
+
+/* Replaces reverseComplement.c:21-118: FASTA image -> records in reverse
+ * order, header line kept, letters reversed and complemented (A<->T, C<->G,
+ * U->A, case kept), one sequence line per record.  If out_cap is too small
+ * the call returns IMSAME_E_ARG with *out_len = the size required
+ * (in_len + records + 1 suffices unless headers contain '>'). */
+int imsame_dev_revcomp(imsame_ctx *ctx, const uint8_t *in, uint64_t in_len,
+                       uint8_t *out, uint64_t out_cap, uint64_t *out_len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

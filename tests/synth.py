@@ -1,0 +1,106 @@
+"""Canonical synthetic inputs.
+
+numpy PCG64, iid uniform ACGT reference cut into fixed-length records;
+"Illumina-like" reads: 90 % sampled uniformly from the reference
+concatenation (record boundaries may be crossed) with 1 % substitutions (to a
+different base), 0.05 % insertions, 0.05 % deletions; 10 % iid random reads.
+
+Array forms return (seq: uint8[ACGT bytes], starts: uint64[n]) -- the exact
+shape of the reference loaders' output (IMSAME.c:194-371) -- so large
+workloads never go through Python strings.
+"""
+import numpy as np
+
+ACGT = np.frombuffer(b"ACGT", dtype=np.uint8)
+
+
+def make_reference_arr(total, rec_len, seed):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    seq = ACGT[rng.integers(0, 4, total, dtype=np.uint8)]
+    starts = np.arange(0, total, rec_len, dtype=np.uint64)
+    return seq, starts
+
+
+def make_reference(total, rec_len, seed):
+    seq, starts = make_reference_arr(total, rec_len, seed)
+    b = seq.tobytes().decode()
+    return [b[s:s + rec_len] for s in starts.tolist()]
+
+
+def _mutate_rows(rng, src, L, sub, ins, dele):
+    """src: (n, L+pad) uint8 windows -> (n, L) reads with substitutions and
+    (rare) indels; indel reads are re-built individually."""
+    n = src.shape[0]
+    out = src[:, :L].copy()
+    # substitutions to a different base
+    m = rng.random((n, L)) < sub
+    if m.any():
+        codes = np.searchsorted(ACGT, out[m])
+        shift = rng.integers(1, 4, codes.shape[0])
+        out[m] = ACGT[(codes + shift) % 4]
+    # indels
+    ev = rng.random((n, src.shape[1]))
+    has = ((ev < ins + dele).any(axis=1)).nonzero()[0]
+    for r in has.tolist():
+        row = []
+        for k in range(src.shape[1]):
+            e = ev[r, k]
+            c = int(src[r, k])
+            if e < dele:
+                continue
+            if e < dele + ins:
+                row.append(int(ACGT[rng.integers(0, 4)]))
+            if rng.random() < sub:
+                c = int(ACGT[(np.searchsorted(ACGT, c) + rng.integers(1, 4)) % 4])
+            row.append(c)
+            if len(row) >= L:
+                break
+        while len(row) < L:
+            row.append(int(ACGT[rng.integers(0, 4)]))
+        out[r] = np.array(row[:L], dtype=np.uint8)
+    return out
+
+
+def make_reads_arr(ref_seq, n, L, seed, sub=0.01, ins=0.0005, dele=0.0005, frac_true=0.9):
+    """ref_seq: uint8 concatenation.  Returns (seq uint8[n*L], starts uint64[n])."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    pad = 8
+    is_true = rng.random(n) < frac_true
+    reads = np.empty((n, L), dtype=np.uint8)
+    nt = int(is_true.sum())
+    if nt:
+        off = rng.integers(0, len(ref_seq) - (L + pad), nt)
+        idx = off[:, None] + np.arange(L + pad)[None, :]
+        reads[is_true] = _mutate_rows(rng, ref_seq[idx], L, sub, ins, dele)
+    nr = n - nt
+    if nr:
+        reads[~is_true] = ACGT[rng.integers(0, 4, (nr, L), dtype=np.uint8)]
+    starts = np.arange(0, n * L, L, dtype=np.uint64)
+    return reads.reshape(-1), starts
+
+
+def make_reads(ref_records, n, L, seed, sub=0.01, ins=0.0005, dele=0.0005, frac_true=0.9):
+    cat = np.frombuffer("".join(ref_records).encode(), dtype=np.uint8)
+    seq, starts = make_reads_arr(cat, n, L, seed, sub, ins, dele, frac_true)
+    b = seq.tobytes().decode()
+    return [b[s:s + L] for s in starts.tolist()]
+
+
+def to_fasta(seq, starts, prefix, width=80):
+    """Array form -> FASTA bytes (LF, `>prefix_<i>` headers)."""
+    b = seq.tobytes()
+    ends = list(starts[1:].tolist()) + [len(b)]
+    out = []
+    for i, (s, e) in enumerate(zip(starts.tolist(), ends)):
+        out.append(f">{prefix}_{i}\n".encode())
+        if width:
+            for k in range(s, e, width):
+                out.append(b[k:min(e, k + width)] + b"\n")
+        else:
+            out.append(b[s:e] + b"\n")
+    return b"".join(out)
+
+
+def write_fasta(path, seq, starts, prefix, width=80):
+    with open(path, "wb") as f:
+        f.write(to_fasta(seq, starts, prefix, width))

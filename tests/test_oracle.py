@@ -1,0 +1,70 @@
+"""Pin the CPU restatement (oracle/) against the reference's golden vectors.
+
+These are the oracle's credentials: every later parity claim of the HIP path
+is a comparison against this oracle (on the GPU box, where /root/reference
+does not exist) or against the same golden vectors.
+"""
+import os
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+from tests import golden_io as G
+from tests.oracle_bind import Oracle
+
+
+def test_nw_pairs_match_reference(oracle):
+    rows = G.nw_pairs()
+    assert len(rows) > 300
+    import hashlib
+    for r in rows:
+        o = oracle.nw(r["X"], r["Y"], r["igap"], r["egap"])
+        for k in ("score", "bx", "by", "length", "identities", "igaps", "egaps", "head_x", "head_y"):
+            assert o[k] == r[k], (k, o[k], r[k], len(r["X"]), len(r["Y"]))
+        assert len(o["text"]) == r["text_len"]
+        assert hashlib.sha1(o["text"]).hexdigest() == r["text_sha1"]
+        if "text" in r:
+            assert o["text"].decode() == r["text"]
+
+
+def test_ungapped_match_reference(oracle):
+    import ctypes
+    from tests.oracle_bind import UgOut
+    fmt = oracle.lib.or_fmt_ld
+    off = UgOut.e_value.offset
+    rows, cases = G.ungapped_rows()
+    assert len(rows) > 1000
+    arrs = {c: (G.seqs_arrays(v["db"]), G.seqs_arrays(v["reads"])) for c, v in cases.items()}
+    for r in rows:
+        (db, dbs), (q, qs) = arrs[r["case"]]
+        o = oracle.ungapped(db, dbs, q, qs, r["pos_db"], r["pos_q"], r["read"], r["dbseq"])
+        assert (o.x_start, o.y_start, o.t_len) == (r["x_start"], r["y_start"], r["t_len"])
+        buf = ctypes.create_string_buffer(64)
+        # compare the full 80-bit value through the same printf as the reference driver
+        fmt(ctypes.c_void_p(ctypes.addressof(o) + off), buf, 64)
+        assert buf.value.decode() == r["e_hex"], (buf.value, r["e_hex"])
+
+
+@pytest.mark.parametrize("name", G.e2e_cases())
+def test_cli_e2e_match_reference(oracle, name):
+    case = G.e2e_case(name)
+    extra = case["meta"]["extra"]
+    for T in case["meta"]["runs"]:
+        with tempfile.TemporaryDirectory() as td:
+            outp = os.path.join(td, "o.align")
+            p = Oracle.run_cli(["-query", case["query"], "-db", case["db"], "-out", outp,
+                                "-n_threads", T, *extra])
+            blob = open(outp, "rb").read() if os.path.exists(outp) else b""
+            G.check_cli_against_golden(case, int(T), p.returncode, p.stdout, blob)
+
+
+def test_revcomp_match_reference(oracle):
+    d = os.path.join(G.GOLDEN, "revcomp")
+    names = sorted(f[:-3] for f in os.listdir(d) if f.endswith(".in"))
+    assert len(names) >= 6
+    for n in names:
+        data = open(os.path.join(d, n + ".in"), "rb").read()
+        exp = open(os.path.join(d, n + ".out"), "rb").read()
+        assert oracle.revcomp(data) == exp, n
