@@ -1,0 +1,181 @@
+#!/usr/bin/env python3
+"""Benchmark of the IMSAME seed-and-extend hot path on MI355X.
+
+Metric (BASELINE.json): reads aligned/sec (node), 1M x 150 bp synthetic
+Illumina-like reads vs a 50 Mbp synthetic reference (configs[1]).
+
+One step = one imsame_dev_align pass over the rank's 1M-read shard (seed
+scan + ungapped/e-value + NW wavefront + backtrack + acceptance + D2H of the
+per-read results), inputs resident in HBM.  N GPUs: one process per GPU
+(torchrun), each aligns its OWN 1M-read shard against its replica of the
+index (weak scaling, no data-path collective); the accepted-read counters are
+all-reduced over RCCL at the end.  value = N * 1M * steps / max-over-ranks
+wall time of the timed region.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "reads aligned/sec (node), 1M×150bp vs 50Mbp ref, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md, chip-level parameters
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--reads", type=int, default=1_000_000, help="reads per GPU")
+    ap.add_argument("--read-len", type=int, default=150)
+    ap.add_argument("--ref-bp", type=int, default=50_000_000)
+    ap.add_argument("--record-bp", type=int, default=2_000)
+    ap.add_argument("--n-threads", type=int, default=16, help="reference -n_threads semantics")
+    ap.add_argument("--cpu-sample", type=int, default=40_000, help="reads in the CPU baseline sample (0: skip)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "nw_traffic.json"))
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import imsame_amd
+    from tests import synth
+
+    # synthetic C2 inputs: the reference is replicated, each rank has its own reads
+    ref, rst = synth.make_reference_arr(a.ref_bp, a.record_bp, seed=42)
+    q, qs = synth.make_reads_arr(ref, a.reads, a.read_len, seed=43 + 1000 * rank)
+    dev = imsame_amd.Device(local)
+    t0 = time.time()
+    dev.index(ref, rst)
+    t_index = time.time() - t0
+    dev.set_query(q, qs)                               # H2D once: inputs resident in HBM
+    params = dev.params()
+
+    def step():
+        return dev.align(0, a.reads, n_threads=a.n_threads, params=params)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(a.warmup):
+        step()
+    barrier()
+    stats = []
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        res, _, st = step()
+        stats.append(st.as_dict())
+    barrier()
+    elapsed = time.perf_counter() - t0
+    accepted = int((res["status"] == 1).sum())
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed, float(accepted)], dtype=torch.float64, device=f"cuda:{local}")
+        tmax = t[:1].clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tsum = t[1:].clone()
+        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+        elapsed = float(tmax.item())
+        accepted_all = int(tsum.item())
+    else:
+        accepted_all = accepted
+    total_reads = world * a.reads * a.steps
+    value = total_reads / elapsed
+
+    # dominant kernel: nw_kernel.  Algorithmic bytes per NW candidate (SURVEY
+    # 8(d)): record + read + 2 B/cell traceback floor; HIP events on the
+    # library's own stream bracket every NW launch.
+    nw_ms = sum(s["ms_nw"] for s in stats)
+    nw_launches = sum(s["nw_launches"] for s in stats)
+    cells = sum(s["nw_cells"] for s in stats)
+    n_nw = sum(s["n_nw"] for s in stats)
+    seq_bytes = n_nw * (a.record_bp + a.read_len)
+    alg_bytes = 2 * cells + seq_bytes
+    achieved = alg_bytes / (nw_ms / 1e3) / 1e9 if nw_ms else 0.0
+    traffic = None
+    if os.path.exists(a.traffic_json):
+        try:
+            tj = json.load(open(a.traffic_json))
+            traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "kernel": "nw_kernel", "launches": nw_launches,
+                "avg_launch_ms": round(nw_ms / max(nw_launches, 1), 4),
+                "alg_bytes_per_launch": int(alg_bytes / max(nw_launches, 1)),
+                "cells_per_s": round(cells / (nw_ms / 1e3), 1) if nw_ms else 0.0}
+
+    cpu = None
+    if rank == 0 and world == 1 and a.cpu_sample > 0:
+        cpu = cpu_baseline(dev, ref, rst, q, qs, a)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "reads/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "int32", "data": "synthetic",
+            "config": {"workload": "C2: 1M x 150 bp Illumina-like reads per GPU vs 50 Mbp synthetic reference "
+                                   "(2 kbp records), BASELINE.json configs[1]",
+                       "reads_per_gpu": a.reads, "read_len": a.read_len, "ref_bp": a.ref_bp,
+                       "record_bp": a.record_bp, "n_threads_semantic": a.n_threads,
+                       "parallelism": f"dp{world} (read shards, replicated index)"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "detail": {"accepted_reads": accepted_all, "index_build_s": round(t_index, 3),
+                       "rounds": stats[-1]["rounds"], "nw_per_read": round(stats[-1]["n_nw"] / a.reads, 4),
+                       "hits_per_read": round(stats[-1]["n_hits"] / a.reads, 2),
+                       "ms_seed": round(stats[-1]["ms_seed"], 3), "ms_nw": round(stats[-1]["ms_nw"], 3),
+                       "ms_align_call": round(stats[-1]["ms_total"], 3)},
+        }
+        print(json.dumps(line), flush=True)
+    dev.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(dev, ref, rst, q, qs, a):
+    """The oracle (clean-room CPU restatement, 'port') on the host cores, on a
+    bounded sample: the first cpu_sample reads of the rank-0 shard taken as a
+    query of their own, -n_threads cpu_threads, alignment phase only (index
+    build excluded, as for the GPU).  The GPU then aligns the same sample view
+    with the same -n_threads and every per-read result is compared."""
+    from tests.oracle_bind import Oracle
+    from imsame_amd import PARITY_FIELDS
+    o = Oracle.load()
+    n = min(a.cpu_sample, len(qs))
+    qv = q[:int(qs[n])] if n < len(qs) else q
+    rc, exp, _ = o.align(ref, rst, qv, qs[:n], None, a.cpu_threads)
+    o.lib.or_last_align_seconds.restype = C.c_double
+    secs = o.lib.or_last_align_seconds()
+    dev.set_query(qv, qs[:n])
+    got, _, _ = dev.align(0, n, n_threads=a.cpu_threads)
+    same = int(np.all([exp[f] == got[f] for f in PARITY_FIELDS], axis=0).sum())
+    return {"value": round(n / secs, 1), "unit": "reads/s", "cores": a.cpu_threads, "kind": "port",
+            "sample": f"first {n} reads of the rank-0 shard as their own query, oracle/imsame_oracle.c "
+                      f"-n_threads {a.cpu_threads}, alignment-phase wall {secs:.2f} s",
+            "sample_reads_identical_to_gpu": same, "sample_reads_compared": n}
+
+
+if __name__ == "__main__":
+    main()

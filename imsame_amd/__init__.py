@@ -1,0 +1,220 @@
+"""imsame_amd -- MI355X-native IMSAME seed-and-extend path.
+
+Python mirror of the C-ABI boundary (include/imsame_dev.h).  The reference
+(Bitlab-UMA/IMSAME) is a C program; its seam for this path is the pthread
+worker computeAlignmentsByThread (alignmentFunctions.c:43) fed by the 12-mer
+index built in main (IMSAME.c:194-289).  Here:
+
+    dev = Device(0)                         # imsame_dev_open
+    dev.index(db_seq, db_starts, db_brk)    # replaces IMSAME.c:232-281
+    dev.set_query(q_seq, q_starts)
+    res, paths, stats = dev.align(n_threads=T, params=dev.params())
+                                            # replaces T x computeAlignmentsByThread
+
+Every call runs on the GPU through libimsame_dev.so; there is no CPU
+fallback -- a missing library or device raises ImsameError.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import abi
+from .abi import Params, Stats, RESULT_DTYPE, PARITY_FIELDS  # noqa: F401
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_DEV = os.path.join(HERE, "lib", "libimsame_dev.so")
+LIB_HOST = os.path.join(HERE, "lib", "libimsame_host.so")
+CLI = os.path.join(HERE, "bin", "imsame")
+
+_lib = None
+_host = None
+
+
+class ImsameError(RuntimeError):
+    def __init__(self, code, what=""):
+        self.code = code
+        msg = _strerror(code) if _lib is not None else str(code)
+        super().__init__(f"{what}: {msg} ({code})" if what else f"{msg} ({code})")
+
+
+def _strerror(code):
+    return _lib.imsame_strerror(code).decode()
+
+
+def lib():
+    """Load libimsame_dev.so (built by __graft_entry__.build / csrc/Makefile)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_DEV):
+            raise ImsameError(abi.IMSAME_E_STATE, f"{LIB_DEV} missing: run __graft_entry__.build()")
+        L = C.CDLL(LIB_DEV)
+        vp, u64 = C.c_void_p, C.c_uint64
+        L.imsame_strerror.restype = C.c_char_p
+        L.imsame_strerror.argtypes = [C.c_int]
+        L.imsame_params_default.argtypes = [C.POINTER(Params)]
+        L.imsame_dev_open.argtypes = [C.c_int, C.POINTER(vp)]
+        L.imsame_dev_close.argtypes = [vp]
+        L.imsame_dev_index.argtypes = [vp, vp, u64, vp, u64, vp]
+        L.imsame_dev_set_query.argtypes = [vp, vp, u64, vp, u64]
+        L.imsame_dev_align.argtypes = [vp, u64, u64, u64, C.POINTER(Params), vp, vp, u64, C.POINTER(u64),
+                                       C.POINTER(Stats)]
+        L.imsame_dev_nw_pairs.argtypes = [vp, vp, vp, vp, vp, u64, C.POINTER(Params), vp, vp, u64,
+                                          C.POINTER(u64), C.POINTER(C.c_double)]
+        L.imsame_dev_revcomp.argtypes = [vp, vp, u64, vp, u64, C.POINTER(u64)]
+        _lib = L
+    return _lib
+
+
+def host_lib():
+    global _host
+    if _host is None:
+        H = C.CDLL(LIB_HOST)
+        H.host_render.restype = C.c_uint64
+        H.host_render.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.POINTER(abi.ReadResult),
+                                  C.c_void_p, C.c_void_p]
+        _host = H
+    return _host
+
+
+class _Text(C.Structure):
+    _fields_ = [("buf", C.c_void_p), ("len", C.c_size_t), ("cap", C.c_size_t)]
+
+
+def render(X, Y, result_row, path):
+    """.align body text of one accepted read (build_alignment text,
+    alignmentFunctions.c:230-271) from a device path."""
+    H = host_lib()
+    rr = abi.ReadResult()
+    for k in RESULT_DTYPE.names:
+        setattr(rr, k, int(result_row[k]))
+    X = np.frombuffer(X, dtype=np.uint8) if isinstance(X, (bytes, bytearray)) else X
+    Y = np.frombuffer(Y, dtype=np.uint8) if isinstance(Y, (bytes, bytearray)) else Y
+    path = np.ascontiguousarray(path, dtype=np.uint32)
+    t = _Text()
+    ident = H.host_render(X.ctypes.data, len(X), Y.ctypes.data, len(Y), C.byref(rr),
+                          path.ctypes.data if len(path) else None, C.byref(t))
+    out = C.string_at(t.buf, t.len)
+    C.CDLL(None).free(C.c_void_p(t.buf))
+    return out, int(ident)
+
+
+def _arr(a, dt):
+    return np.ascontiguousarray(a, dtype=dt)
+
+
+class Device:
+    """One HIP device context (imsame_ctx)."""
+
+    def __init__(self, device=0):
+        L = lib()
+        h = C.c_void_p()
+        rc = L.imsame_dev_open(device, C.byref(h))
+        if rc:
+            raise ImsameError(rc, f"imsame_dev_open({device})")
+        self._h = h
+        self._keep = []
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().imsame_dev_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @staticmethod
+    def params(**kw):
+        """Reference defaults (IMSAME.c:44-49) updated with kw; igap/egap are
+        the negative internal values (CLI "-igap 5" -> igap=-5)."""
+        p = Params()
+        lib().imsame_params_default(C.byref(p))
+        for k, v in kw.items():
+            setattr(p, k, v)
+        return p
+
+    def index(self, db_seq, db_starts, db_brk=None):
+        db_seq, db_starts = _arr(db_seq, np.uint8), _arr(db_starts, np.uint64)
+        brk = None if db_brk is None else _arr(db_brk, np.uint8)
+        rc = lib().imsame_dev_index(self._h, db_seq.ctypes.data, len(db_seq), db_starts.ctypes.data,
+                                    len(db_starts), None if brk is None else brk.ctypes.data)
+        if rc:
+            raise ImsameError(rc, "imsame_dev_index")
+
+    def set_query(self, q_seq, q_starts):
+        q_seq, q_starts = _arr(q_seq, np.uint8), _arr(q_starts, np.uint64)
+        rc = lib().imsame_dev_set_query(self._h, q_seq.ctypes.data, len(q_seq), q_starts.ctypes.data,
+                                        len(q_starts))
+        if rc:
+            raise ImsameError(rc, "imsame_dev_set_query")
+        self.n_q = len(q_starts)
+
+    def align(self, read_from=0, read_to=None, n_threads=4, params=None, want_paths=False, paths_cap=None,
+              allow_too_long=False):
+        """Per-read results (numpy RESULT_DTYPE) for reads [read_from, read_to)."""
+        read_to = self.n_q if read_to is None else read_to
+        p = params if params is not None else self.params()
+        p.want_paths = 1 if want_paths else 0
+        n = read_to - read_from
+        res = np.zeros(n, dtype=RESULT_DTYPE)
+        cap = (paths_cap if paths_cap is not None else 8 * n + 1024) if want_paths else 0
+        st = Stats()
+        used = C.c_uint64()
+        while True:
+            paths = np.zeros(max(cap, 1), dtype=np.uint32)
+            rc = lib().imsame_dev_align(self._h, read_from, read_to, n_threads, C.byref(p), res.ctypes.data,
+                                        paths.ctypes.data if want_paths else None, cap, C.byref(used),
+                                        C.byref(st))
+            if rc == abi.IMSAME_E_PATHS:
+                cap = int(used.value * 1.25) + 1024
+                continue
+            break
+        if rc and not (rc == abi.IMSAME_E_READ_TOO_LONG and allow_too_long):
+            raise ImsameError(rc, "imsame_dev_align")
+        return res, paths[:used.value], st
+
+    def nw_pairs(self, X, Y, params=None, want_paths=False):
+        """Unit-level NW + backtrack + acceptance of explicit pairs
+        (build_alignment, alignmentFunctions.c:210-274)."""
+        p = params if params is not None else self.params()
+        p.want_paths = 1 if want_paths else 0
+        xs = np.frombuffer(b"".join(X), dtype=np.uint8).copy()
+        ys = np.frombuffer(b"".join(Y), dtype=np.uint8).copy()
+        xst = np.cumsum([0] + [len(x) for x in X]).astype(np.uint64)
+        yst = np.cumsum([0] + [len(y) for y in Y]).astype(np.uint64)
+        res = np.zeros(len(X), dtype=RESULT_DTYPE)
+        cap = (sum(len(x) + len(y) for x, y in zip(X, Y)) + 16) if want_paths else 0
+        paths = np.zeros(max(cap, 1), dtype=np.uint32)
+        used = C.c_uint64()
+        ms = C.c_double()
+        rc = lib().imsame_dev_nw_pairs(self._h, xs.ctypes.data, xst.ctypes.data, ys.ctypes.data, yst.ctypes.data,
+                                       len(X), C.byref(p), res.ctypes.data, paths.ctypes.data, cap,
+                                       C.byref(used), C.byref(ms))
+        if rc:
+            raise ImsameError(rc, "imsame_dev_nw_pairs")
+        return res, paths[:used.value], ms.value
+
+    def revcomp(self, data):
+        """reverseComplement.c on the device: FASTA bytes -> FASTA bytes."""
+        src = np.frombuffer(data, dtype=np.uint8)
+        cap = len(data) + data.count(b">") + 2
+        while True:
+            out = np.zeros(max(cap, 1), dtype=np.uint8)
+            ol = C.c_uint64()
+            rc = lib().imsame_dev_revcomp(self._h, src.ctypes.data if len(src) else None, len(src),
+                                          out.ctypes.data, cap, C.byref(ol))
+            if rc == abi.IMSAME_E_ARG and ol.value > cap:
+                cap = ol.value
+                continue
+            if rc:
+                raise ImsameError(rc, "imsame_dev_revcomp")
+            return out[:ol.value].tobytes()

@@ -1,0 +1,29 @@
+/* imsame_host.h -- host-side helpers of the CLI: FASTA loading with the
+ * reference's rules and .align text rendering from device paths. */
+#ifndef IMSAME_HOST_H
+#define IMSAME_HOST_H
+#include <stdint.h>
+#include <stddef.h>
+#include "../../../include/imsame_dev.h"
+
+typedef struct {
+    uint8_t  *seq;     /* ACGT-filtered concatenation           */
+    uint64_t *start;   /* n + 1 entries (start[n] = len)        */
+    uint64_t  n, len;
+    uint8_t  *brk;     /* database: k-mer reset bitmap, else NULL */
+} host_seqs;
+
+typedef struct { char *buf; size_t len, cap; } host_text;
+
+/* IMSAME.c:194-289 (want_brk = 1, database) / :320-371 (query) */
+int  host_parse_fasta(const uint8_t *b, uint64_t nb, int want_brk, host_seqs *s);
+int  host_load_fasta(const char *path, int want_brk, host_seqs *s);
+void host_free_seqs(host_seqs *s);
+
+/* backtrackingNW's strings (alignmentFunctions.c:493-560) rebuilt from a
+ * device path, then build_alignment's 60-column text (:230-271).
+ * Returns the identities counted by the text loop. */
+uint64_t host_render(const uint8_t *X, uint64_t xlen, const uint8_t *Y, uint64_t ylen,
+                     const imsame_read_result *r, const uint32_t *path, host_text *t);
+
+#endif

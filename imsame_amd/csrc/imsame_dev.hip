@@ -1,0 +1,702 @@
+// imsame_dev.hip -- MI355X (gfx950) implementation of include/imsame_dev.h.
+//
+// Device pipeline for one imsame_dev_align call:
+//   index  : kmer_code -> count -> scan -> scatter -> segsort   (CSR in HBM)
+//   rounds : seed_kernel   first e-value-passing, not-yet-rejected hit per
+//                          active read, in the reference's visiting order
+//            nw_kernel     gapped alignment + backtrack + accept (wavefront)
+//            update_kernel accepted -> result; rejected -> memo + next round
+// The reference visits (window, hit) pairs in order and stops at the first
+// accepted one (alignmentFunctions.c:91-195).  NW is a pure function of
+// (record, read), so a rejected record is skipped
+// on later hits instead of being recomputed; results are unchanged.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <math.h>
+#include <limits.h>
+#include <time.h>
+#include <vector>
+#include <algorithm>
+#include "../../include/imsame_dev.h"
+
+#include "tables.h"
+#include "nw_kernel.hip"
+#include "seed_kernel.hip"
+
+
+#define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+    fprintf(stderr, "[imsame] HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+    return IMSAME_E_HIP; } } while (0)
+
+// ---------------------------------------------------------------------------
+// device helpers
+// ---------------------------------------------------------------------------
+
+// ---------------------------------------------------------------------------
+// index build (replaces IMSAME.c:232-281)
+// ---------------------------------------------------------------------------
+__global__ void mark_record_starts(const uint64_t *st, uint64_t n, uint64_t L, uint32_t *brk) {
+    uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (k < n && st[k] < L) atomicOr(&brk[st[k] >> 5], 1u << (st[k] & 31));
+}
+
+// code of the 12-mer ending at base p, or ~0 when a reset lies in (p-11, p]
+__global__ void kmer_code_kernel(const uint8_t *seq, uint64_t L, const uint32_t *brk, uint32_t *codes,
+                                 uint32_t *cnt) {
+    uint64_t p = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (p >= L) return;
+    uint32_t code = 0xFFFFFFFFu;
+    if (p >= IMSAME_FIXED_K - 1) {
+        const uint64_t b0 = p - (IMSAME_FIXED_K - 2);           // bits p-10 .. p
+        const uint64_t w = b0 >> 5;
+        const uint64_t win = ((uint64_t)brk[w] | ((uint64_t)brk[w + 1] << 32)) >> (b0 & 31);
+        if ((win & ((1u << (IMSAME_FIXED_K - 1)) - 1)) == 0) {
+            code = 0;
+#pragma unroll
+            for (int k = IMSAME_FIXED_K - 1; k >= 0; --k) code = (code << 2) | base2(seq[p - k]);
+            atomicAdd(&cnt[code], 1u);
+        }
+    }
+    codes[p] = code;
+}
+
+__global__ void kmer_scatter(const uint32_t *codes, uint64_t L, const uint32_t *off, uint32_t *fill,
+                             const uint64_t *st, uint64_t n_db, uint2 *ent) {
+    uint64_t p = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (p >= L) return;
+    const uint32_t c = codes[p];
+    if (c == 0xFFFFFFFFu) return;
+    uint64_t lo = 0, hi = n_db;                 // last record with start <= p
+    while (hi - lo > 1) { uint64_t m = (lo + hi) >> 1; if (st[m] <= p) lo = m; else hi = m; }
+    const uint32_t slot = off[c] + atomicAdd(&fill[c], 1u);
+    ent[slot] = make_uint2((uint32_t)(p + 1), (uint32_t)lo);   // pos = last base + 1 (IMSAME.c:247)
+}
+
+// buckets in DESCENDING pos = the reference's LIFO chain order (IMSAME.c:255-276)
+__global__ void segsort_small(const uint32_t *off, uint2 *ent, uint32_t *big, uint32_t *nbig) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= NBUCKETS) return;
+    const uint32_t lo = off[b], n = off[b + 1] - lo;
+    if (n < 2) return;
+    if (n > 32) { big[atomicAdd(nbig, 1u)] = b; return; }
+    uint2 *e = ent + lo;
+    for (uint32_t i = 1; i < n; ++i) {
+        uint2 v = e[i];
+        uint32_t j = i;
+        while (j > 0 && e[j - 1].x < v.x) { e[j] = e[j - 1]; --j; }
+        e[j] = v;
+    }
+}
+
+// one block per large bucket (n > 32): bitonic sort, descending pos, in LDS
+// when the padded bucket fits, else in a padded global scratch area.
+__device__ void bitonic_desc(uint2 *s, uint32_t np) {
+    for (uint32_t k = 2; k <= np; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) {
+                const uint32_t l = i ^ j;
+                if (l > i) {
+                    const bool desc = (i & k) == 0;
+                    if ((s[i].x < s[l].x) == desc) { uint2 t = s[i]; s[i] = s[l]; s[l] = t; }
+                }
+            }
+            __syncthreads();
+        }
+}
+
+__global__ void segsort_big(const uint32_t *off, uint2 *ent, const uint32_t *big) {
+    __shared__ uint2 s[4096];
+    const uint32_t b = big[blockIdx.x];
+    const uint32_t lo = off[b], n = off[b + 1] - lo;
+    uint32_t np = 1;
+    while (np < n) np <<= 1;
+    if (np > 4096) return;                      // handled by segsort_huge
+    uint2 *e = ent + lo;
+    for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) s[i] = i < n ? e[i] : make_uint2(0u, 0u);
+    __syncthreads();
+    bitonic_desc(s, np);
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) e[i] = s[i];
+}
+
+__global__ void segsort_huge(uint2 *e, uint32_t n, uint2 *scratch, uint32_t np) {
+    for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) scratch[i] = i < n ? e[i] : make_uint2(0u, 0u);
+    __syncthreads();
+    bitonic_desc(scratch, np);                  // __syncthreads orders global accesses of the block
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) e[i] = scratch[i];
+}
+
+// exclusive scan of n u32 (1024 elements per block; recursive over block sums)
+__global__ void scan_blocks(const uint32_t *in, uint32_t *out, uint32_t *bsum, uint64_t n) {
+    __shared__ uint32_t s[1024];
+    const uint64_t i = blockIdx.x * 1024ull + threadIdx.x;
+    const uint32_t v = i < n ? in[i] : 0;
+    s[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        const uint32_t t = threadIdx.x >= (uint32_t)o ? s[threadIdx.x - o] : 0;
+        __syncthreads();
+        s[threadIdx.x] += t;
+        __syncthreads();
+    }
+    if (i < n) out[i] = s[threadIdx.x] - v;
+    if (threadIdx.x == 1023) bsum[blockIdx.x] = s[1023];
+}
+__global__ void scan_add(uint32_t *out, const uint32_t *bpre, uint64_t n) {
+    const uint64_t i = blockIdx.x * 1024ull + threadIdx.x;
+    if (i < n) out[i] += bpre[blockIdx.x];
+}
+
+// ---------------------------------------------------------------------------
+// reverse complement (replaces reverseComplement.c:21-118)
+// ---------------------------------------------------------------------------
+#include "revcomp_kernel.hip"
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+struct DBuf {
+    void *p = nullptr; size_t cap = 0;
+    int ensure(size_t n) {
+        if (n <= cap) return 0;
+        if (p) (void)hipFree(p);
+        p = nullptr; cap = 0;
+        size_t want = n + n / 8 + 4096;
+        if (hipMalloc(&p, want) != hipSuccess) { p = nullptr; return IMSAME_E_OOM; }
+        cap = want;
+        return 0;
+    }
+    void release() { if (p) (void)hipFree(p); p = nullptr; cap = 0; }
+    template <class T> T *as() const { return (T *)p; }
+};
+
+struct imsame_ctx {
+    int device = 0, ncu = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // database + index
+    DBuf db, db_start, off, ent, brk, codes, fill, big;
+    uint64_t n_db = 0, db_len = 0, n_ent = 0;
+    uint32_t max_rec = 0;
+    std::vector<uint64_t> h_db_start;
+    bool have_index = false;
+    // query
+    DBuf q, q_start;
+    uint64_t n_q = 0, q_len = 0;
+    std::vector<uint64_t> h_q_start;
+    bool have_query = false;
+    // per-read state
+    DBuf res, cur_p, cur_h, memo, nmemo, rstat, act0, act1;
+    // candidates
+    DBuf cread, csid, cread2, csid2, cout, cout2;
+    // scalars (one block of u64 counters)
+    DBuf ctr;
+    // tables
+    DBuf minraw, minlen, minident;
+    // NW scratch
+    DBuf tb, bnd, paths;
+    // revcomp
+    DBuf rc_in, rc_out, rc_a, rc_b, rc_c;
+};
+
+// counters block layout (u64 slots)
+enum { C_NCAND = 0, C_NCAND2, C_NNEXT, C_WORK, C_WORK2, C_PATHS, C_FLAGS, C_ERR, C_HITS, C_CELLS, C_NACC, C_NSLOTS };
+
+static double now_ms() {
+    struct timespec ts; clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+}
+
+extern "C" void imsame_params_default(imsame_params *p) {
+    memset(p, 0, sizeof *p);
+    p->min_e = 1 / powl(10, 20);                         // IMSAME.c:44
+    p->min_coverage = 0.5; p->min_identity = 0.5;        // :46
+    p->igap = -5; p->egap = -2;                          // :47
+    p->max_read_size = IMSAME_MAX_READ_SIZE;
+    p->want_paths = 0;
+}
+
+extern "C" const char *imsame_strerror(int code) {
+    switch (code) {
+    case IMSAME_OK: return "ok";
+    case IMSAME_E_HIP: return "HIP runtime error";
+    case IMSAME_E_OOM: return "out of memory";
+    case IMSAME_E_READ_TOO_LONG: return "Read size reached for gapped alignment.";
+    case IMSAME_E_ARG: return "bad argument";
+    case IMSAME_E_RANGE: return "gap parameters out of int32 range";
+    case IMSAME_E_PATHS: return "path arena too small";
+    case IMSAME_E_STATE: return "index or query not loaded";
+    }
+    return "unknown error";
+}
+
+extern "C" int imsame_dev_open(int device, imsame_ctx **out) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) return IMSAME_E_HIP;
+    HIPCHK(hipSetDevice(device));
+    imsame_ctx *c = new imsame_ctx();
+    c->device = device;
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, device));
+    c->ncu = prop.multiProcessorCount;
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreate(&c->ev0));
+    HIPCHK(hipEventCreate(&c->ev1));
+    if (c->ctr.ensure(C_NSLOTS * 8)) { delete c; return IMSAME_E_OOM; }
+    *out = c;
+    return IMSAME_OK;
+}
+
+extern "C" void imsame_dev_close(imsame_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    DBuf *bufs[] = {&c->db, &c->db_start, &c->off, &c->ent, &c->brk, &c->codes, &c->fill, &c->big, &c->q,
+                    &c->q_start, &c->res, &c->cur_p, &c->cur_h, &c->memo, &c->nmemo, &c->rstat, &c->act0,
+                    &c->act1, &c->cread, &c->csid, &c->cread2, &c->csid2, &c->cout, &c->cout2, &c->ctr,
+                    &c->minraw, &c->minlen, &c->minident, &c->tb, &c->bnd, &c->paths, &c->rc_in, &c->rc_out,
+                    &c->rc_a, &c->rc_b, &c->rc_c};
+    for (DBuf *b : bufs) b->release();
+    (void)hipEventDestroy(c->ev0);
+    (void)hipEventDestroy(c->ev1);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+static unsigned nblk(uint64_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
+
+// exclusive scan out[0..n) of in[0..n) (u32, wraps past 2^32: callers size for it)
+static int dev_scan(hipStream_t s, const uint32_t *in, uint32_t *out, uint64_t n) {
+    if (n == 0) return 0;
+    const uint64_t nb = (n + 1023) / 1024;
+    DBuf bs, bp;
+    if (bs.ensure(nb * 4 + 16) || bp.ensure(nb * 4 + 16)) return IMSAME_E_OOM;
+    scan_blocks<<<(unsigned)nb, 1024, 0, s>>>(in, out, bs.as<uint32_t>(), n);
+    if (nb > 1) {
+        int rc = dev_scan(s, bs.as<uint32_t>(), bp.as<uint32_t>(), nb);
+        if (rc) return rc;
+        scan_add<<<(unsigned)nb, 1024, 0, s>>>(out, bp.as<uint32_t>(), n);
+    }
+    HIPCHK(hipStreamSynchronize(s));     // the level buffers are freed on return
+    return 0;
+}
+
+extern "C" int imsame_dev_index(imsame_ctx *c, const uint8_t *db_seq, uint64_t db_len, const uint64_t *db_start,
+                                uint64_t n_db, const uint8_t *db_brk) {
+    if (!c || (db_len && !db_seq) || (n_db && !db_start)) return IMSAME_E_ARG;
+    if (db_len >= 0xFFFFFFF0ull || n_db >= 0xFFFFFFF0ull) return IMSAME_E_ARG;   // u32 positions
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    c->have_index = false;
+    c->n_db = n_db; c->db_len = db_len;
+    c->h_db_start.assign(db_start, db_start + n_db);
+    c->h_db_start.push_back(db_len);
+    c->max_rec = 0;
+    for (uint64_t k = 0; k < n_db; ++k)
+        c->max_rec = (uint32_t)std::max<uint64_t>(c->max_rec, c->h_db_start[k + 1] - c->h_db_start[k]);
+    const uint64_t nw = db_len / 32 + 2;
+    if (c->db.ensure(db_len + 64) || c->db_start.ensure((n_db + 1) * 8) || c->brk.ensure(nw * 4) ||
+        c->codes.ensure((db_len + 1) * 4) || c->off.ensure(((uint64_t)NBUCKETS + 1) * 4) ||
+        c->fill.ensure((uint64_t)NBUCKETS * 4) || c->big.ensure((uint64_t)NBUCKETS * 4))
+        return IMSAME_E_OOM;
+    if (db_len) HIPCHK(hipMemcpyAsync(c->db.p, db_seq, db_len, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->db_start.p, c->h_db_start.data(), (n_db + 1) * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemsetAsync(c->brk.p, 0, nw * 4, s));
+    if (db_brk && db_len) HIPCHK(hipMemcpyAsync(c->brk.p, db_brk, (db_len + 7) / 8, hipMemcpyHostToDevice, s));
+    if (n_db) mark_record_starts<<<nblk(n_db, 256), 256, 0, s>>>(c->db_start.as<uint64_t>(), n_db, db_len,
+                                                                   c->brk.as<uint32_t>());
+    HIPCHK(hipMemsetAsync(c->fill.p, 0, (uint64_t)NBUCKETS * 4, s));
+    if (db_len) kmer_code_kernel<<<nblk(db_len, 256), 256, 0, s>>>(c->db.as<uint8_t>(), db_len, c->brk.as<uint32_t>(),
+                                                                  c->codes.as<uint32_t>(), c->fill.as<uint32_t>());
+    // exclusive scan of the counts -> off[0..NB], off[NB] = total
+    uint32_t total = 0;
+    {
+        DBuf cnt;
+        if (cnt.ensure(((uint64_t)NBUCKETS + 1) * 4)) return IMSAME_E_OOM;
+        HIPCHK(hipMemsetAsync(cnt.p, 0, ((uint64_t)NBUCKETS + 1) * 4, s));
+        HIPCHK(hipMemcpyAsync(cnt.p, c->fill.p, (uint64_t)NBUCKETS * 4, hipMemcpyDeviceToDevice, s));
+        int rc = dev_scan(s, cnt.as<uint32_t>(), c->off.as<uint32_t>(), (uint64_t)NBUCKETS + 1);
+        if (rc) return rc;
+        HIPCHK(hipMemcpyAsync(&total, c->off.as<uint32_t>() + NBUCKETS, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        cnt.release();
+    }
+    c->n_ent = total;
+    if (c->ent.ensure(((uint64_t)total + 1) * 8)) return IMSAME_E_OOM;
+    HIPCHK(hipMemsetAsync(c->fill.p, 0, (uint64_t)NBUCKETS * 4, s));
+    if (db_len) kmer_scatter<<<nblk(db_len, 256), 256, 0, s>>>(c->codes.as<uint32_t>(), db_len, c->off.as<uint32_t>(),
+                                                              c->fill.as<uint32_t>(), c->db_start.as<uint64_t>(), n_db,
+                                                              c->ent.as<uint2>());
+    uint32_t *nbig = c->fill.as<uint32_t>();       // fill is free again: reuse as a counter
+    HIPCHK(hipMemsetAsync(nbig, 0, 4, s));
+    segsort_small<<<nblk(NBUCKETS, 256), 256, 0, s>>>(c->off.as<uint32_t>(), c->ent.as<uint2>(),
+                                                      c->big.as<uint32_t>(), nbig);
+    uint32_t hbig = 0;
+    HIPCHK(hipMemcpyAsync(&hbig, nbig, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (hbig) {
+        segsort_big<<<hbig, 256, 0, s>>>(c->off.as<uint32_t>(), c->ent.as<uint2>(), c->big.as<uint32_t>());
+        // buckets beyond 4096 entries (repeats): one block each, padded global scratch
+        std::vector<uint32_t> bigs(hbig), offs(NBUCKETS + 1);
+        HIPCHK(hipMemcpyAsync(bigs.data(), c->big.p, (uint64_t)hbig * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(offs.data(), c->off.p, ((uint64_t)NBUCKETS + 1) * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        DBuf scr;
+        for (uint32_t b : bigs) {
+            const uint32_t nb = offs[b + 1] - offs[b];
+            uint32_t np = 1;
+            while (np < nb) np <<= 1;
+            if (np <= 4096) continue;
+            if (scr.ensure((uint64_t)np * 8)) return IMSAME_E_OOM;
+            segsort_huge<<<1, 1024, 0, s>>>(c->ent.as<uint2>() + offs[b], nb, scr.as<uint2>(), np);
+        }
+        HIPCHK(hipStreamSynchronize(s));
+        scr.release();
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipGetLastError());
+    c->codes.release();
+    c->have_index = true;
+    return IMSAME_OK;
+}
+
+extern "C" int imsame_dev_set_query(imsame_ctx *c, const uint8_t *q_seq, uint64_t q_len, const uint64_t *q_start,
+                                    uint64_t n_q) {
+    if (!c || (q_len && !q_seq) || (n_q && !q_start)) return IMSAME_E_ARG;
+    if (n_q >= 0xFFFFFFF0ull) return IMSAME_E_ARG;
+    HIPCHK(hipSetDevice(c->device));
+    c->have_query = false;
+    c->n_q = n_q; c->q_len = q_len;
+    c->h_q_start.assign(q_start, q_start + n_q);
+    c->h_q_start.push_back(q_len);
+    if (c->q.ensure(q_len + 64) || c->q_start.ensure((n_q + 1) * 8)) return IMSAME_E_OOM;
+    if (q_len) HIPCHK(hipMemcpyAsync(c->q.p, q_seq, q_len, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->q_start.p, c->h_q_start.data(), (n_q + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->have_query = true;
+    return IMSAME_OK;
+}
+
+static int build_tables(imsame_ctx *c, const imsame_params *p, uint32_t ymax, uint32_t xmax) {
+    std::vector<uint64_t> mr;
+    std::vector<uint32_t> ml, mi;
+    imsame_build_tables(p, c->db_len, ymax, xmax, mr, ml, mi);
+    if (c->minraw.ensure(mr.size() * 8) || c->minlen.ensure(ml.size() * 4) || c->minident.ensure(mi.size() * 4))
+        return IMSAME_E_OOM;
+    HIPCHK(hipMemcpyAsync(c->minraw.p, mr.data(), mr.size() * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->minlen.p, ml.data(), ml.size() * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->minident.p, mi.data(), mi.size() * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));   // host vectors die here
+    return 0;
+}
+
+struct NwPlan { int G, GPW, xcap, xstride, steps, nstr; size_t lds; unsigned blocks; };
+
+static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, NwPlan *pl) {
+    const int wpb = 4;
+    const NwShape sh = nw_shape(ymax, xcap);
+    pl->G = sh.G; pl->GPW = sh.GPW; pl->nstr = sh.nstr; pl->xcap = sh.xcap; pl->xstride = sh.xstride;
+    pl->steps = sh.steps;
+    pl->lds = (size_t)wpb * nw_wave_lds(pl->GPW, pl->xstride);
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw_kernel, wpb * 64, pl->lds) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+    per_cu = std::min(per_cu, 8);
+    const uint64_t waves_needed = (ncand + pl->GPW - 1) / pl->GPW;
+    pl->blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)c->ncu * per_cu, (waves_needed + wpb - 1) / wpb));
+    return 0;
+}
+
+static int launch_nw(imsame_ctx *c, const NwPlan &pl, const uint32_t *cread, const uint32_t *csid, uint32_t n,
+                     imsame_read_result *outp, int64_t ig, int64_t eg, const imsame_params *p, uint32_t ymax,
+                     uint32_t xmax, uint32_t *work, const uint8_t *dbp, const uint64_t *dbs, const uint8_t *qp,
+                     const uint64_t *qs, uint32_t paths_cap, double *ms) {
+    hipStream_t s = c->stream;
+    const unsigned slots = pl.blocks * 4;
+    const uint64_t tb_dw = (uint64_t)pl.nstr * pl.steps * 64 * NW_KW;
+    if (c->tb.ensure(slots * tb_dw * 4) || c->bnd.ensure((uint64_t)slots * 3 * pl.xcap * 4 + 64)) return IMSAME_E_OOM;
+    NwLaunch P;
+    memset(&P, 0, sizeof P);
+    P.db = dbp; P.db_start = dbs; P.q = qp; P.q_start = qs;
+    P.cand_read = cread; P.cand_sid = csid; P.n_cand = n;
+    P.igap = (int32_t)ig; P.egap = (int32_t)eg;
+    P.G = pl.G; P.GPW = pl.GPW; P.xcap = pl.xcap; P.xstride = pl.xstride; P.steps = pl.steps;
+    P.tb = c->tb.as<uint32_t>(); P.tb_wave_dw = tb_dw;
+    P.bnd = c->bnd.as<int32_t>(); P.bnd_wave = (uint64_t)3 * pl.xcap;
+    P.minlen = c->minlen.as<uint32_t>(); P.n_minlen = ymax + 1;
+    P.minident = c->minident.as<uint32_t>(); P.n_minident = xmax + ymax + 2;
+    P.counter = work;
+    P.out = outp;
+    uint64_t *ctr = c->ctr.as<uint64_t>();
+    P.paths = c->paths.as<uint32_t>(); P.paths_cap = paths_cap;
+    P.paths_used = (uint32_t *)(ctr + C_PATHS); P.want_paths = p->want_paths;
+    P.flags = (uint32_t *)(ctr + C_FLAGS);
+    HIPCHK(hipMemsetAsync(work, 0, 4, s));
+    HIPCHK(hipEventRecord(c->ev0, s));
+    nw_kernel<<<pl.blocks, 256, pl.lds, s>>>(P);
+    HIPCHK(hipEventRecord(c->ev1, s));
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventSynchronize(c->ev1));
+    float f = 0;
+    HIPCHK(hipEventElapsedTime(&f, c->ev0, c->ev1));
+    *ms = f;
+    return 0;
+}
+
+static int paths_setup(imsame_ctx *c, const imsame_params *p, uint64_t paths_cap, uint32_t *cap32) {
+    *cap32 = 0;
+    if (p->want_paths) {
+        *cap32 = (uint32_t)std::min<uint64_t>(paths_cap, 0xFFFFFFF0u);
+        if (c->paths.ensure((uint64_t)*cap32 * 4 + 16)) return IMSAME_E_OOM;
+    }
+    return 0;
+}
+
+extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64_t n_threads_semantic,
+                                const imsame_params *p, imsame_read_result *res, uint32_t *paths, uint64_t paths_cap,
+                                uint64_t *paths_used, imsame_stats *stats) {
+    const double t_start = now_ms();
+    if (!c || !p || (!res && read_to > read_from)) return IMSAME_E_ARG;
+    if (!c->have_index || !c->have_query) return IMSAME_E_STATE;
+    if (read_to > c->n_q || read_from > read_to) return IMSAME_E_ARG;
+    if (p->want_paths && !paths) return IMSAME_E_ARG;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const uint32_t n = (uint32_t)(read_to - read_from);
+    imsame_stats st;
+    memset(&st, 0, sizeof st);
+    st.n_reads = n;
+    st.err_read = ~0ull;
+    if (paths_used) *paths_used = 0;
+    // shapes
+    uint32_t ymax = 0;
+    for (uint64_t r = read_from; r < read_to; ++r)
+        ymax = (uint32_t)std::max<uint64_t>(ymax, c->h_q_start[r + 1] - c->h_q_start[r]);
+    const uint32_t xcap = (uint32_t)std::min<uint64_t>(c->max_rec, p->max_read_size);
+    const uint32_t ycap = (uint32_t)std::min<uint64_t>(ymax, p->max_read_size);
+    if (!imsame_gaps_in_range(p->igap, p->egap, xcap, ycap)) return IMSAME_E_RANGE;
+    if (std::max(xcap, ycap) > 0x3FFF) return IMSAME_E_ARG;       // 14-bit traceback coordinates
+    int rc = build_tables(c, p, ymax, xcap);
+    if (rc) return rc;
+    uint32_t pcap = 0;
+    if ((rc = paths_setup(c, p, paths_cap, &pcap))) return rc;
+    if (n == 0) { if (stats) *stats = st; return IMSAME_OK; }
+    if (c->res.ensure((uint64_t)n * 64) || c->cur_p.ensure((uint64_t)n * 8) || c->cur_h.ensure((uint64_t)n * 4) ||
+        c->memo.ensure((uint64_t)n * 4 * MEMO) || c->nmemo.ensure(n) || c->rstat.ensure(n) ||
+        c->act0.ensure((uint64_t)n * 4) || c->act1.ensure((uint64_t)n * 4) || c->cread.ensure((uint64_t)n * 4) ||
+        c->csid.ensure((uint64_t)n * 4) || c->cread2.ensure((uint64_t)n * 4) || c->csid2.ensure((uint64_t)n * 4) ||
+        c->cout.ensure((uint64_t)n * 64) || c->cout2.ensure((uint64_t)n * 64))
+        return IMSAME_E_OOM;
+    uint64_t *ctr = c->ctr.as<uint64_t>();
+    HIPCHK(hipMemsetAsync(ctr, 0, C_NSLOTS * 8, s));
+    const unsigned long long errinit = ~0ull;
+    HIPCHK(hipMemcpyAsync(ctr + C_ERR, &errinit, 8, hipMemcpyHostToDevice, s));
+    InitLaunch I = {c->q_start.as<uint64_t>(), read_from, n, c->res.as<imsame_read_result>(), c->cur_p.as<uint64_t>(),
+                    c->cur_h.as<uint32_t>(), c->nmemo.as<uint8_t>(), c->rstat.as<uint8_t>(), c->act0.as<uint32_t>()};
+    init_kernel<<<nblk(n, 256), 256, 0, s>>>(I);
+    HIPCHK(hipGetLastError());
+
+    const uint32_t short_y = std::min<uint32_t>(ycap, NW_W / 2);
+    uint32_t nact = n;
+    uint32_t *act = c->act0.as<uint32_t>(), *nxt = c->act1.as<uint32_t>();
+    uint64_t nw_ms_launch_sum = 0;
+    (void)nw_ms_launch_sum;
+    while (nact) {
+        st.rounds++;
+        HIPCHK(hipMemsetAsync(ctr + C_NCAND, 0, 3 * 8, s));     // NCAND, NCAND2, NNEXT
+        SeedLaunch S;
+        S.db = c->db.as<uint8_t>(); S.db_start = c->db_start.as<uint64_t>(); S.n_db = c->n_db; S.db_len = c->db_len;
+        S.q = c->q.as<uint8_t>(); S.q_start = c->q_start.as<uint64_t>(); S.n_q = c->n_q; S.q_len = c->q_len;
+        S.off = c->off.as<uint32_t>(); S.ent = c->ent.as<uint2>();
+        S.active = act; S.n_active = nact;
+        S.read_from = read_from;
+        S.T = n_threads_semantic ? n_threads_semantic : 1;
+        S.rpt = (uint64_t)floorl((long double)c->n_q / (long double)S.T);     // IMSAME.c:414
+        S.cur_p = c->cur_p.as<uint64_t>(); S.cur_h = c->cur_h.as<uint32_t>(); S.memo = c->memo.as<uint32_t>();
+        S.nmemo = c->nmemo.as<uint8_t>(); S.rstat = c->rstat.as<uint8_t>();
+        S.minraw = c->minraw.as<uint64_t>(); S.n_minraw = ymax + 1;
+        S.max_rs = p->max_read_size; S.short_ylen = short_y;
+        S.cread = c->cread.as<uint32_t>(); S.csid = c->csid.as<uint32_t>(); S.ncand = (uint32_t *)(ctr + C_NCAND);
+        S.cread2 = c->cread2.as<uint32_t>(); S.csid2 = c->csid2.as<uint32_t>(); S.ncand2 = (uint32_t *)(ctr + C_NCAND2);
+        S.err = (unsigned long long *)(ctr + C_ERR); S.nhits = (unsigned long long *)(ctr + C_HITS);
+        HIPCHK(hipEventRecord(c->ev0, s));
+        seed_kernel<<<nblk(nact, 256), 256, 0, s>>>(S);
+        HIPCHK(hipEventRecord(c->ev1, s));
+        HIPCHK(hipGetLastError());
+        uint64_t hc[2];
+        HIPCHK(hipMemcpyAsync(hc, ctr + C_NCAND, 16, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        float fs = 0;
+        HIPCHK(hipEventElapsedTime(&fs, c->ev0, c->ev1));
+        st.ms_seed += fs;
+        const uint32_t n1 = (uint32_t)hc[0], n2 = (uint32_t)hc[1];
+        if (n1 + n2 == 0) break;
+        struct Cls { uint32_t n; uint32_t *cr, *cs; imsame_read_result *o; uint32_t ylim; int work; };
+        Cls cls[2] = {{n1, c->cread.as<uint32_t>(), c->csid.as<uint32_t>(), c->cout.as<imsame_read_result>(), short_y, C_WORK},
+                      {n2, c->cread2.as<uint32_t>(), c->csid2.as<uint32_t>(), c->cout2.as<imsame_read_result>(), ycap, C_WORK2}};
+        for (int k = 0; k < 2; ++k) {
+            if (!cls[k].n) continue;
+            NwPlan pl;
+            plan_nw(c, cls[k].ylim, xcap, cls[k].n, &pl);
+            double ms = 0;
+            rc = launch_nw(c, pl, cls[k].cr, cls[k].cs, cls[k].n, cls[k].o, p->igap, p->egap, p, ymax, xcap,
+                           (uint32_t *)(ctr + cls[k].work), c->db.as<uint8_t>(), c->db_start.as<uint64_t>(),
+                           c->q.as<uint8_t>(), c->q_start.as<uint64_t>(), pcap, &ms);
+            if (rc) return rc;
+            st.ms_nw += ms; st.nw_launches++; st.n_nw += cls[k].n;
+            UpdLaunch U = {cls[k].cr, cls[k].cs, cls[k].n, cls[k].o, read_from, c->res.as<imsame_read_result>(),
+                           c->rstat.as<uint8_t>(), c->memo.as<uint32_t>(), c->nmemo.as<uint8_t>(), nxt,
+                           (uint32_t *)(ctr + C_NNEXT), (unsigned long long *)(ctr + C_CELLS),
+                           (unsigned long long *)(ctr + C_NACC), c->db_start.as<uint64_t>()};
+            update_kernel<<<nblk(cls[k].n, 256), 256, 0, s>>>(U);
+            HIPCHK(hipGetLastError());
+        }
+        uint64_t nn = 0;
+        HIPCHK(hipMemcpyAsync(&nn, ctr + C_NNEXT, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        nact = (uint32_t)nn;
+        std::swap(act, nxt);
+    }
+    uint64_t hc[C_NSLOTS];
+    HIPCHK(hipMemcpyAsync(hc, ctr, C_NSLOTS * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(res, c->res.p, (uint64_t)n * 64, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    st.n_hits = hc[C_HITS];
+    st.nw_cells = hc[C_CELLS];
+    st.n_accepted = hc[C_NACC];
+    st.nw_launch_ms = st.nw_launches ? st.ms_nw / st.nw_launches : 0;
+    st.nw_bytes = 2 * st.nw_cells;       // traceback floor; sequences added below
+    st.nw_bytes += 0;
+    int ret = IMSAME_OK;
+    if (hc[C_ERR] != ~0ull) {
+        st.err_read = hc[C_ERR] >> 32; st.err_dbseq = hc[C_ERR] & 0xFFFFFFFFull;
+        ret = IMSAME_E_READ_TOO_LONG;
+    }
+    if (p->want_paths) {
+        const uint64_t used = (uint32_t)hc[C_PATHS];
+        if (paths_used) *paths_used = used;
+        if (hc[C_FLAGS] & 1) { if (ret == IMSAME_OK) ret = IMSAME_E_PATHS; }
+        else if (used) {
+            HIPCHK(hipMemcpyAsync(paths, c->paths.p, used * 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+        }
+    }
+    st.ms_total = now_ms() - t_start;
+    if (stats) *stats = st;
+    return ret;
+}
+
+// Unit-level entry: NW + backtrack + acceptance for explicit (X_k, Y_k) pairs
+// (build_alignment, alignmentFunctions.c:210-274), default-or-given params.
+extern "C" int imsame_dev_nw_pairs(imsame_ctx *c, const uint8_t *xs, const uint64_t *x_start, const uint8_t *ys,
+                                   const uint64_t *y_start, uint64_t npairs, const imsame_params *p,
+                                   imsame_read_result *res, uint32_t *paths, uint64_t paths_cap, uint64_t *paths_used,
+                                   double *kernel_ms) {
+    if (!c || !p || !res || npairs == 0) return IMSAME_E_ARG;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const uint64_t xl = x_start[npairs], yl = y_start[npairs];
+    uint32_t xmax = 0, ymax = 0;
+    for (uint64_t k = 0; k < npairs; ++k) {
+        xmax = (uint32_t)std::max<uint64_t>(xmax, x_start[k + 1] - x_start[k]);
+        ymax = (uint32_t)std::max<uint64_t>(ymax, y_start[k + 1] - y_start[k]);
+        if (x_start[k + 1] - x_start[k] < 2 || y_start[k + 1] - y_start[k] < 2) return IMSAME_E_ARG;
+    }
+    if (!imsame_gaps_in_range(p->igap, p->egap, xmax, ymax)) return IMSAME_E_RANGE;
+    if (std::max(xmax, ymax) > 0x3FFF) return IMSAME_E_ARG;
+    DBuf dx, dxs, dy, dys, dc, dout;
+    if (dx.ensure(xl + 64) || dxs.ensure((npairs + 1) * 8) || dy.ensure(yl + 64) || dys.ensure((npairs + 1) * 8) ||
+        dc.ensure(npairs * 8) || dout.ensure(npairs * 64))
+        return IMSAME_E_OOM;
+    std::vector<uint32_t> idx(npairs);
+    for (uint64_t k = 0; k < npairs; ++k) idx[k] = (uint32_t)k;
+    HIPCHK(hipMemcpyAsync(dx.p, xs, xl, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(dxs.p, x_start, (npairs + 1) * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(dy.p, ys, yl, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(dys.p, y_start, (npairs + 1) * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(dc.p, idx.data(), npairs * 4, hipMemcpyHostToDevice, s));
+    uint64_t saved = c->db_len;
+    c->db_len = 1;     // e-value table unused here
+    int rc = build_tables(c, p, ymax, xmax);
+    c->db_len = saved;
+    if (rc) return rc;
+    uint32_t pcap = 0;
+    if ((rc = paths_setup(c, p, paths_cap, &pcap))) return rc;
+    uint64_t *ctr = c->ctr.as<uint64_t>();
+    HIPCHK(hipMemsetAsync(ctr, 0, C_NSLOTS * 8, s));
+    NwPlan pl;
+    plan_nw(c, ymax, xmax, (uint32_t)npairs, &pl);
+    double ms = 0;
+    rc = launch_nw(c, pl, dc.as<uint32_t>(), dc.as<uint32_t>(), (uint32_t)npairs, dout.as<imsame_read_result>(),
+                   p->igap, p->egap, p, ymax, xmax, (uint32_t *)(ctr + C_WORK), dx.as<uint8_t>(), dxs.as<uint64_t>(),
+                   dy.as<uint8_t>(), dys.as<uint64_t>(), pcap, &ms);
+    if (rc) return rc;
+    if (kernel_ms) *kernel_ms = ms;
+    HIPCHK(hipMemcpyAsync(res, dout.p, npairs * 64, hipMemcpyDeviceToHost, s));
+    uint64_t hc[C_NSLOTS];
+    HIPCHK(hipMemcpyAsync(hc, ctr, C_NSLOTS * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    int ret = IMSAME_OK;
+    if (p->want_paths) {
+        if (paths_used) *paths_used = (uint32_t)hc[C_PATHS];
+        if (hc[C_FLAGS] & 1) ret = IMSAME_E_PATHS;
+        else if (hc[C_PATHS]) {
+            HIPCHK(hipMemcpyAsync(paths, c->paths.p, (uint32_t)hc[C_PATHS] * 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+        }
+    }
+    dx.release(); dxs.release(); dy.release(); dys.release(); dc.release(); dout.release();
+    return ret;
+}
+
+// reverseComplement.c:21-118 on the device (see revcomp_kernel.hip)
+extern "C" int imsame_dev_revcomp(imsame_ctx *c, const uint8_t *in, uint64_t n, uint8_t *out, uint64_t out_cap,
+                                  uint64_t *out_len) {
+    if (!c || !out_len || (n && !in)) return IMSAME_E_ARG;
+    if (n >= 0xFFFFFFF0ull) return IMSAME_E_ARG;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    *out_len = 0;
+    if (n == 0) return IMSAME_OK;
+    if (c->rc_in.ensure(n + 16) || c->rc_a.ensure((n + 1) * 4 * 2 + 64) || c->rc_b.ensure((n + 1) * 4 * 2 + 64))
+        return IMSAME_E_OOM;
+    uint32_t *fgt = c->rc_a.as<uint32_t>(), *flet = fgt + (n + 1);
+    uint32_t *gpos = c->rc_b.as<uint32_t>(), *let = gpos + (n + 1);
+    HIPCHK(hipMemcpyAsync(c->rc_in.p, in, n, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemsetAsync(fgt, 0, (n + 1) * 4 * 2, s));
+    rc_flags<<<nblk(n, 256), 256, 0, s>>>(c->rc_in.as<uint8_t>(), n, fgt, flet);
+    int rc = dev_scan(s, fgt, gpos, n + 1);
+    if (!rc) rc = dev_scan(s, flet, let, n + 1);
+    if (rc) return rc;
+    uint32_t nr = 0;
+    HIPCHK(hipMemcpyAsync(&nr, gpos + n, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (nr == 0) return IMSAME_OK;
+    if (c->rc_c.ensure((uint64_t)nr * 4 * 5 + 64)) return IMSAME_E_OOM;
+    uint32_t *off = c->rc_c.as<uint32_t>(), *hend = off + nr, *bend = hend + nr, *szr = bend + nr, *oo = szr + nr;
+    rc_offsets<<<nblk(n, 256), 256, 0, s>>>(c->rc_in.as<uint8_t>(), n, gpos, off);
+    rc_records<<<nblk(nr, 256), 256, 0, s>>>(c->rc_in.as<uint8_t>(), n, off, nr, let, hend, bend, szr);
+    // sizes can exceed 2^32 only for > 4 GB outputs (rejected above for inputs)
+    DBuf oo1;
+    if (oo1.ensure(((uint64_t)nr + 1) * 4)) return IMSAME_E_OOM;
+    HIPCHK(hipMemsetAsync(oo1.p, 0, ((uint64_t)nr + 1) * 4, s));
+    HIPCHK(hipMemcpyAsync(oo1.p, szr, (uint64_t)nr * 4, hipMemcpyDeviceToDevice, s));
+    if ((rc = dev_scan(s, oo1.as<uint32_t>(), oo, nr))) return rc;
+    uint32_t last_o = 0, last_sz = 0;
+    HIPCHK(hipMemcpyAsync(&last_o, oo + nr - 1, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&last_sz, szr + nr - 1, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    const uint64_t total = (uint64_t)last_o + last_sz;
+    *out_len = total;
+    if (total > out_cap || !out) return IMSAME_E_ARG;
+    if (c->rc_out.ensure(total + 16)) return IMSAME_E_OOM;
+    rc_headers<<<nblk(nr, 256), 256, 0, s>>>(c->rc_in.as<uint8_t>(), off, nr, hend, bend, let, oo, c->rc_out.as<uint8_t>());
+    rc_bodies<<<nblk(n, 256), 256, 0, s>>>(c->rc_in.as<uint8_t>(), n, off, nr, hend, bend, let, oo, c->rc_out.as<uint8_t>());
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(out, c->rc_out.p, total, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    oo1.release();
+    return IMSAME_OK;
+}

@@ -1,0 +1,192 @@
+// seed_kernel.hip -- per-read seed scan + ungapped extension + e-value test,
+// and the per-round bookkeeping kernels.  Included by imsame_dev.hip (and by
+// tests/emu/wave_emu.cpp under IMSAME_WAVE_EMU).
+//
+// Reference: computeAlignmentsByThread  alignmentFunctions.c:43-208
+//            alignmentFromQuickHits     alignmentFunctions.c:276-387
+// One thread per active read resumes the reference's visiting order
+// (window-major, hits of a bucket in LIFO = descending-pos order) from the
+// read's cursor and stops at the first hit whose e-value passes and whose
+// record is not already known to be rejected for this read.
+#include "wave_ops.h"
+
+#define MEMO 4
+#define NBUCKETS (1u << 24)
+enum { RS_ACTIVE = 0, RS_DONE = 1, RS_ACCEPTED = 2, RS_ERROR = 3 };
+
+__device__ __forceinline__ uint32_t base2(uint32_t c) { return ((c >> 1) ^ (c >> 2)) & 3u; }  // A0 C1 G2 T3
+
+struct SeedLaunch {
+    const uint8_t *db; const uint64_t *db_start; uint64_t n_db, db_len;
+    const uint8_t *q;  const uint64_t *q_start;  uint64_t n_q, q_len;
+    const uint32_t *off; const uint2 *ent;        // CSR, each bucket in descending pos
+    const uint32_t *active; uint32_t n_active;
+    uint64_t read_from, rpt, T;
+    uint64_t *cur_p; uint32_t *cur_h; uint32_t *memo; uint8_t *nmemo; uint8_t *rstat;
+    const uint64_t *minraw; uint32_t n_minraw;
+    uint64_t max_rs; uint32_t short_ylen;
+    uint32_t *cread, *csid, *ncand;        // class 0: ylen <= short_ylen
+    uint32_t *cread2, *csid2, *ncand2;     // class 1: longer reads
+    unsigned long long *err;               // min (read << 32 | record)
+    unsigned long long *nhits;
+};
+
+// alignmentFromQuickHits (alignmentFunctions.c:276-387): the raw score in the
+// reference's u64 wrap arithmetic (:373).  Loop bounds fold the reference's
+// per-step tests (:321-322, :344-345) into one limit per direction.
+__device__ __forceinline__ uint64_t ungapped_raw(const uint8_t *__restrict__ db, const uint8_t *__restrict__ q,
+                                                 int64_t pd0, int64_t pq0, int64_t xs, int64_t xe, int64_t ys,
+                                                 int64_t ye, int64_t dbl, int64_t ql) {
+    int64_t end_x = pd0 - 1, beg_x = end_x - IMSAME_FIXED_K + 1;
+    int sc = IMSAME_FIXED_K * IMSAME_POINT, best_r = sc, best_l = sc;
+    uint64_t idents = IMSAME_FIXED_K;
+    const int64_t fx = min(min(dbl - 1, xe), pd0 + (min(ql - 1, ye) - pq0));
+    for (int64_t x = pd0, y = pq0; sc > 0 && x <= fx; ++x, ++y) {
+        if (db[x] == q[y]) { sc += IMSAME_POINT; ++idents; } else sc -= IMSAME_POINT;
+        if (best_r <= sc) { best_r = sc; end_x = x; }
+    }
+    sc = best_r;                        // left pass restarts from the right max, best_l stays 48 (:339)
+    const int64_t bx0 = pd0 - IMSAME_FIXED_K - 1, by0 = pq0 - IMSAME_FIXED_K - 1;
+    const int64_t lx = max(max((int64_t)0, xs), bx0 - (by0 - max((int64_t)0, ys)));
+    for (int64_t x = bx0, y = by0; sc > 0 && x >= lx; --x, --y) {
+        if (db[x] == q[y]) { sc += IMSAME_POINT; ++idents; } else sc -= IMSAME_POINT;
+        if (best_l <= sc) { best_l = sc; beg_x = x; }
+    }
+    const uint64_t t_len = (uint64_t)(end_x - beg_x);
+    return idents * IMSAME_POINT - (t_len - idents) * IMSAME_POINT;
+}
+
+__device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint64_t &hits) {
+    const uint64_t r = S.active[idx], k = r - S.read_from;
+    const uint64_t rs = S.q_start[r], re = S.q_start[r + 1];
+    const uint64_t ylen = re - rs;
+    // chunk heads (IMSAME.c:414,430-452): a read borrows
+    // the previous read's last base (the skip at :96-105 does not advance
+    // curr_pos) unless it opens its chunk; an empty chunk-opening read (UB in
+    // the reference) hands that role to the next read.
+    const uint64_t from_c = (S.rpt == 0) ? 0 : min(r / S.rpt, S.T - 1) * S.rpt;
+    const bool head = S.q_start[from_c] == rs;
+    const uint64_t p0 = rs - (head ? 0 : 1);
+    const uint64_t up_to = (r + 1 < S.n_q) ? (re ? re - 1 : 0) : S.q_len;    // :93
+    uint64_t p = S.cur_p[k];
+    uint32_t h = S.cur_h[k];
+    if (p == ~0ull) { p = p0 + IMSAME_FIXED_K - 1; h = 0; }
+    const uint32_t nm = S.nmemo[k];
+    uint32_t memo[MEMO];
+#pragma unroll
+    for (int m = 0; m < MEMO; ++m) memo[m] = (m < (int)nm) ? S.memo[k * MEMO + m] : 0xFFFFFFFFu;
+    const uint64_t mraw = ylen < S.n_minraw ? S.minraw[ylen] : ~0ull;
+    const int64_t ys = (int64_t)rs, ye = (r == S.n_q - 1) ? (int64_t)S.q_len : (int64_t)re - 1;
+    uint32_t code = 0;
+    bool have = false, found = false;
+    for (; p < up_to; ++p, h = 0) {
+        if (!have) {
+            code = 0;
+            for (int t = IMSAME_FIXED_K - 1; t >= 0; --t) code = (code << 2) | base2(S.q[p - t]);
+            have = true;
+        } else {
+            code = ((code << 2) | base2(S.q[p])) & (NBUCKETS - 1);
+        }
+        const uint32_t lo = S.off[code], hi = S.off[code + 1];
+        for (uint32_t e = lo + h; e < hi; ++e, ++h) {
+            const uint2 ent = S.ent[e];
+            const uint32_t sid = ent.y;
+            bool skip = false;
+#pragma unroll
+            for (int m = 0; m < MEMO; ++m) skip |= memo[m] == sid;
+            if (skip) continue;                 // NW(sid, r) already rejected (Q18)
+            const int64_t xs = (int64_t)S.db_start[sid];
+            const int64_t xe = (sid == S.n_db - 1) ? (int64_t)S.db_len : (int64_t)S.db_start[sid + 1] - 1;
+            ++hits;
+            const uint64_t raw = ungapped_raw(S.db, S.q, ent.x, (int64_t)p + 1, xs, xe, ys, ye,
+                                              (int64_t)S.db_len, (int64_t)S.q_len);
+            if (mraw != ~0ull && raw >= mraw) {                      // e < min_e (:139)
+                const uint64_t xlen = S.db_start[sid + 1] - S.db_start[sid];
+                if (xlen > S.max_rs || ylen > S.max_rs) {            // terror (:155)
+                    S.rstat[k] = RS_ERROR;
+                    wv_atomic_min64(S.err, (unsigned long long)((r << 32) | sid));
+                } else {
+                    S.cur_p[k] = p; S.cur_h[k] = h + 1;
+                    if (ylen <= S.short_ylen) {
+                        const uint32_t o = wv_atomic_add(S.ncand, 1u);
+                        S.cread[o] = (uint32_t)r; S.csid[o] = sid;
+                    } else {
+                        const uint32_t o = wv_atomic_add(S.ncand2, 1u);
+                        S.cread2[o] = (uint32_t)r; S.csid2[o] = sid;
+                    }
+                }
+                found = true;
+                break;
+            }
+        }
+        if (found) break;
+    }
+    if (!found) S.rstat[k] = RS_DONE;
+}
+
+struct UpdLaunch {
+    const uint32_t *cread, *csid; uint32_t n;
+    const imsame_read_result *out;
+    uint64_t read_from;
+    imsame_read_result *res;
+    uint8_t *rstat; uint32_t *memo; uint8_t *nmemo;
+    uint32_t *next; uint32_t *nnext;
+    unsigned long long *cells; unsigned long long *nacc;
+    const uint64_t *db_start;
+};
+
+// accepted -> the read's result (NWaligned = 1, :172); rejected -> remember
+// the record and keep scanning from the cursor next round
+__device__ __forceinline__ void update_one(const UpdLaunch &U, uint32_t c, uint64_t &cells, uint64_t &acc) {
+    const uint32_t r = U.cread[c];
+    const uint64_t k = r - U.read_from;
+    const imsame_read_result o = U.out[c];
+    cells += (uint64_t)(U.db_start[o.db_seq + 1] - U.db_start[o.db_seq]) * o.ylen;
+    if (o.status == 1) {
+        U.res[k] = o;
+        U.rstat[k] = RS_ACCEPTED;
+        acc += 1;
+    } else {
+        const uint32_t nm = U.nmemo[k];
+        if (nm < MEMO) { U.memo[k * MEMO + nm] = (uint32_t)o.db_seq; U.nmemo[k] = (uint8_t)(nm + 1); }
+        U.next[wv_atomic_add(U.nnext, 1u)] = r;
+    }
+}
+
+struct InitLaunch {
+    const uint64_t *q_start; uint64_t read_from; uint32_t n;
+    imsame_read_result *res; uint64_t *cur_p; uint32_t *cur_h; uint8_t *nmemo; uint8_t *rstat;
+    uint32_t *active;
+};
+
+__device__ __forceinline__ void init_one(const InitLaunch &I, uint32_t k) {
+    const uint64_t r = I.read_from + k;
+    imsame_read_result z;
+    memset(&z, 0, sizeof z);
+    z.ylen = (uint32_t)(I.q_start[r + 1] - I.q_start[r]);
+    I.res[k] = z;
+    I.cur_p[k] = ~0ull; I.cur_h[k] = 0; I.nmemo[k] = 0; I.rstat[k] = RS_ACTIVE;
+    I.active[k] = (uint32_t)r;
+}
+
+#ifndef IMSAME_WAVE_EMU
+__global__ __launch_bounds__(256) void seed_kernel(SeedLaunch S) {
+    const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t hits = 0;
+    if (idx < S.n_active) seed_one(S, idx, hits);
+    if (hits) atomicAdd(S.nhits, (unsigned long long)hits);
+}
+
+__global__ void update_kernel(UpdLaunch U) {
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t cells = 0, acc = 0;
+    if (c < U.n) update_one(U, c, cells, acc);
+    if (cells) atomicAdd(U.cells, (unsigned long long)cells);
+    if (acc) atomicAdd(U.nacc, (unsigned long long)acc);
+}
+
+__global__ void init_kernel(InitLaunch I) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < I.n) init_one(I, k);
+}
+#endif

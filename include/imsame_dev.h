@@ -138,6 +138,16 @@ int imsame_dev_align(imsame_ctx *ctx, uint64_t read_from, uint64_t read_to,
                      imsame_read_result *res, uint32_t *paths, uint64_t paths_cap,
                      uint64_t *paths_used, imsame_stats *stats);
 
+/* Unit-level entry replacing build_alignment (alignmentFunctions.c:210-274:
+ * NW + backtrackingNW + identities) plus the acceptance test (:163) for
+ * explicit pairs: X_k = xs[x_start[k] .. x_start[k+1]) (database record,
+ * rows), Y_k likewise (read, columns); x_start/y_start have npairs+1 entries.
+ * res[k].status = 1 accepted / 2 rejected.  kernel_ms: device time. */
+int imsame_dev_nw_pairs(imsame_ctx *ctx, const uint8_t *xs, const uint64_t *x_start,
+                        const uint8_t *ys, const uint64_t *y_start, uint64_t npairs,
+                        const imsame_params *prm, imsame_read_result *res, uint32_t *paths,
+                        uint64_t paths_cap, uint64_t *paths_used, double *kernel_ms);
+
 /* Replaces reverseComplement.c:21-118: FASTA image -> records in reverse
  * order, header line kept, letters reversed and complemented (A<->T, C<->G,
  * U->A, case kept), one sequence line per record.  If out_cap is too small

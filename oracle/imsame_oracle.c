@@ -413,6 +413,10 @@ static void *scan_chunk(void *arg) {
     return NULL;
 }
 
+/* wall time of the last alignment phase (threads only, no loading/index) */
+static double g_align_seconds;
+double or_last_align_seconds(void) { return g_align_seconds; }
+
 /* Partition, IMSAME.c:414,430-452: rpt = floor(n/T); chunk i = [i*rpt,(i+1)*rpt),
  * the last chunk runs to n. */
 static int run_chunks(const or_seqs *db, const or_seqs *q, const or_index *ix, const imsame_params *prm,
@@ -433,8 +437,12 @@ static int run_chunks(const or_seqs *db, const or_seqs *q, const or_index *ix, c
         if (print_going) printf("Going from %" PRIu64 " to %" PRIu64 "\n", ch[t].from, ch[t].to);
     }
     if (print_going) fflush(stdout);
+    struct timespec a0, a1;
+    clock_gettime(CLOCK_MONOTONIC, &a0);
     for (uint64_t t = 0; t < T; t++) pthread_create(&th[t], NULL, scan_chunk, &ch[t]);
     for (uint64_t t = 0; t < T; t++) pthread_join(th[t], NULL);
+    clock_gettime(CLOCK_MONOTONIC, &a1);
+    g_align_seconds = (a1.tv_sec - a0.tv_sec) + (a1.tv_nsec - a0.tv_nsec) * 1e-9;
     int st = 0;
     uint64_t nn = 0;
     for (uint64_t t = 0; t < T; t++) {
@@ -619,5 +627,28 @@ int or_main(int argc, char **argv) {
 int main(int argc, char **argv) { return or_main(argc, argv); }
 #endif
 
+/* test helper: run the loader on a byte image; caller buffers: seq n+1,
+ * starts n+2 entries, brk n/8+2 bytes */
+int or_parse(const uint8_t *buf, uint64_t n, int want_brk, uint8_t *seq, uint64_t *len, uint64_t *starts,
+             uint64_t *nrec, uint8_t *brk) {
+    or_seqs s;
+    or_parse_fasta(buf, n, &s, want_brk);
+    memcpy(seq, s.seq, s.len);
+    memcpy(starts, s.start, (s.n + 1) * sizeof(uint64_t));
+    if (want_brk && brk) memcpy(brk, s.brk, n / 8 + 2);
+    *len = s.len; *nrec = s.n;
+    or_free_seqs(&s);
+    return 0;
+}
+
 /* test helper: glibc "%La" rendering of a long double held in memory */
 int or_fmt_ld(const long double *x, char *buf, int cap) { return snprintf(buf, (size_t)cap, "%La", *x); }
+
+/* test helpers: the reference's e-value and identity tests on given integers */
+int or_epass(uint64_t raw, uint64_t ylen, uint64_t Ldb, const imsame_params *p) {
+    long double e = (long double)0.333 * (long double)ylen * Ldb * expl(-0.275 * (long double)raw);
+    return e < p->min_e;
+}
+int or_ident_ok(uint64_t ident, uint64_t len, const imsame_params *p) {
+    return (long double)ident / len >= p->min_identity;
+}

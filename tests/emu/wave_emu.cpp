@@ -1,0 +1,202 @@
+// wave_emu.cpp -- TEST INFRASTRUCTURE: runs the device kernel source
+// (imsame_amd/csrc/{nw,seed}_kernel.hip) on the CPU.  Each wave is 64 host
+// threads; DPP / ballot / shuffle are lock-step exchanges (wave_ops.h,
+// IMSAME_WAVE_EMU).  The round orchestration below mirrors
+// imsame_dev.hip:imsame_dev_align with host memory in place of HBM.
+// Built by tests/emu/Makefile into tests/emu/build/libwave_emu.so.
+#define IMSAME_WAVE_EMU 1
+#include <barrier>
+#include <functional>
+#include <thread>
+#include <vector>
+#include <stdio.h>
+#include <string.h>
+#include <math.h>
+#include "../../imsame_amd/csrc/wave_ops.h"
+
+namespace wvemu {
+struct Wave {
+    std::barrier<> bar{64};
+    uint64_t xch[64];
+};
+thread_local Wave *t_wave;
+thread_local int t_lane;
+thread_local uint64_t *t_xch;
+void sync() { t_wave->bar.arrive_and_wait(); }
+}  // namespace wvemu
+
+#include "../../include/imsame_dev.h"
+#include "../../imsame_amd/csrc/tables.h"
+#include "../../imsame_amd/csrc/nw_kernel.hip"
+#include "../../imsame_amd/csrc/seed_kernel.hip"
+
+static void run_wave(const std::function<void(int)> &f) {
+    wvemu::Wave w;
+    std::vector<std::thread> th;
+    th.reserve(64);
+    for (int l = 0; l < 64; ++l)
+        th.emplace_back([&w, &f, l] {
+            wvemu::t_wave = &w; wvemu::t_lane = l; wvemu::t_xch = w.xch;
+            f(l);
+        });
+    for (auto &t : th) t.join();
+}
+
+static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, const uint64_t *qs,
+                  const uint32_t *cread, const uint32_t *csid, uint32_t n, const imsame_params *p, uint32_t ymax,
+                  uint32_t xmax, const std::vector<uint32_t> &ml, const std::vector<uint32_t> &mi,
+                  imsame_read_result *out, uint32_t *paths, uint32_t pcap, uint32_t *pused, uint32_t *flags) {
+    const NwShape sh = nw_shape(ymax, xmax);
+    std::vector<uint32_t> tb((size_t)sh.nstr * sh.steps * 64 * NW_KW + 64, 0xABABABABu);
+    std::vector<int32_t> bnd((size_t)3 * sh.xcap + 64);
+    std::vector<uint8_t> lds(nw_wave_lds(sh.GPW, sh.xstride) + 64);
+    uint32_t counter = 0;
+    NwLaunch P;
+    memset(&P, 0, sizeof P);
+    P.db = db; P.db_start = dbs; P.q = q; P.q_start = qs;
+    P.cand_read = cread; P.cand_sid = csid; P.n_cand = n;
+    P.igap = (int32_t)p->igap; P.egap = (int32_t)p->egap;
+    P.G = sh.G; P.GPW = sh.GPW; P.xcap = sh.xcap; P.xstride = sh.xstride; P.steps = sh.steps;
+    P.tb = tb.data(); P.tb_wave_dw = tb.size();
+    P.bnd = bnd.data(); P.bnd_wave = bnd.size();
+    P.minlen = ml.data(); P.n_minlen = ymax + 1;
+    P.minident = mi.data(); P.n_minident = xmax + ymax + 2;
+    P.counter = &counter; P.out = out;
+    P.paths = paths; P.paths_cap = pcap; P.paths_used = pused; P.want_paths = p->want_paths;
+    P.flags = flags;
+    run_wave([&](int lane) { nw_wave(P, lds.data(), lane, 0); });
+    return 0;
+}
+
+extern "C" int emu_nw_pairs(const uint8_t *xs, const uint64_t *x_start, const uint8_t *ys, const uint64_t *y_start,
+                            uint64_t npairs, const imsame_params *p, imsame_read_result *res, uint32_t *paths,
+                            uint64_t paths_cap, uint64_t *paths_used, uint32_t *flags_out) {
+    uint32_t xmax = 0, ymax = 0;
+    for (uint64_t k = 0; k < npairs; ++k) {
+        xmax = std::max<uint32_t>(xmax, (uint32_t)(x_start[k + 1] - x_start[k]));
+        ymax = std::max<uint32_t>(ymax, (uint32_t)(y_start[k + 1] - y_start[k]));
+    }
+    if (!imsame_gaps_in_range(p->igap, p->egap, xmax, ymax)) return IMSAME_E_RANGE;
+    std::vector<uint64_t> mr;
+    std::vector<uint32_t> ml, mi, idx(npairs);
+    imsame_build_tables(p, 1, ymax, xmax, mr, ml, mi);
+    for (uint64_t k = 0; k < npairs; ++k) idx[k] = (uint32_t)k;
+    uint32_t pused = 0, flags = 0;
+    run_nw(xs, x_start, ys, y_start, idx.data(), idx.data(), (uint32_t)npairs, p, ymax, xmax, ml, mi, res, paths,
+           (uint32_t)paths_cap, &pused, &flags);
+    if (paths_used) *paths_used = pused;
+    if (flags_out) *flags_out = flags;
+    return (flags & 1) ? IMSAME_E_PATHS : 0;
+}
+
+// host CSR with the device index's semantics (imsame_dev.hip: kmer_code_kernel,
+// kmer_scatter, segsort): buckets in descending pos
+static void build_csr(const uint8_t *db, uint64_t L, const uint64_t *dbs, uint64_t n_db, const uint8_t *brk_in,
+                      std::vector<uint32_t> &off, std::vector<uint2> &ent) {
+    std::vector<uint32_t> brk(L / 32 + 2, 0);
+    if (brk_in) for (uint64_t b = 0; b < (L + 7) / 8; ++b) brk[b / 4] |= (uint32_t)brk_in[b] << (8 * (b % 4));
+    for (uint64_t s = 0; s < n_db; ++s) if (dbs[s] < L) brk[dbs[s] >> 5] |= 1u << (dbs[s] & 31);
+    std::vector<uint32_t> code(L, 0xFFFFFFFFu);
+    off.assign(NBUCKETS + 1, 0);
+    for (uint64_t p = IMSAME_FIXED_K - 1; p < L; ++p) {
+        const uint64_t b0 = p - (IMSAME_FIXED_K - 2);
+        const uint64_t win = ((uint64_t)brk[b0 >> 5] | ((uint64_t)brk[(b0 >> 5) + 1] << 32)) >> (b0 & 31);
+        if (win & ((1u << (IMSAME_FIXED_K - 1)) - 1)) continue;
+        uint32_t c = 0;
+        for (int k = IMSAME_FIXED_K - 1; k >= 0; --k) c = (c << 2) | base2(db[p - k]);
+        code[p] = c;
+        off[c + 1]++;
+    }
+    for (uint32_t b = 0; b < NBUCKETS; ++b) off[b + 1] += off[b];
+    ent.assign(off[NBUCKETS] + 1, uint2{0, 0});
+    std::vector<uint32_t> fill(off.begin(), off.end() - 1);
+    for (uint64_t p = L; p-- > 0;) {          // descending positions
+        if (code[p] == 0xFFFFFFFFu) continue;
+        uint64_t lo = 0, hi = n_db;
+        while (hi - lo > 1) { uint64_t m = (lo + hi) / 2; if (dbs[m] <= p) lo = m; else hi = m; }
+        ent[fill[code[p]]++] = uint2{(uint32_t)(p + 1), (uint32_t)lo};
+    }
+}
+
+extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_start, uint64_t n_db,
+                         const uint8_t *db_brk, const uint8_t *q, uint64_t q_len, const uint64_t *q_start,
+                         uint64_t n_q, uint64_t read_from, uint64_t read_to, uint64_t T, const imsame_params *p,
+                         imsame_read_result *res, uint32_t *paths, uint64_t paths_cap, uint64_t *paths_used,
+                         imsame_stats *stats) {
+    std::vector<uint64_t> dbs(db_start, db_start + n_db), qs(q_start, q_start + n_q);
+    dbs.push_back(db_len); qs.push_back(q_len);
+    std::vector<uint32_t> off;
+    std::vector<uint2> ent;
+    build_csr(db, db_len, dbs.data(), n_db, db_brk, off, ent);
+    uint32_t max_rec = 0, ymax = 0;
+    for (uint64_t s = 0; s < n_db; ++s) max_rec = std::max<uint32_t>(max_rec, (uint32_t)(dbs[s + 1] - dbs[s]));
+    for (uint64_t r = read_from; r < read_to; ++r) ymax = std::max<uint32_t>(ymax, (uint32_t)(qs[r + 1] - qs[r]));
+    const uint32_t xcap = (uint32_t)std::min<uint64_t>(max_rec, p->max_read_size);
+    const uint32_t ycap = (uint32_t)std::min<uint64_t>(ymax, p->max_read_size);
+    if (!imsame_gaps_in_range(p->igap, p->egap, xcap, ycap)) return IMSAME_E_RANGE;
+    std::vector<uint64_t> mr;
+    std::vector<uint32_t> ml, mi;
+    imsame_build_tables(p, db_len, ymax, xcap, mr, ml, mi);
+    const uint32_t n = (uint32_t)(read_to - read_from);
+    std::vector<uint64_t> cur_p(n);
+    std::vector<uint32_t> cur_h(n), memo((size_t)n * MEMO), act(n), nxt(n), cr(n), cs(n), cr2(n), cs2(n);
+    std::vector<uint8_t> nmemo(n), rstat(n);
+    std::vector<imsame_read_result> o1(n), o2(n);
+    InitLaunch I = {qs.data(), read_from, n, res, cur_p.data(), cur_h.data(), nmemo.data(), rstat.data(), act.data()};
+    for (uint32_t k = 0; k < n; ++k) init_one(I, k);
+    uint32_t nc[3] = {0, 0, 0}, pused = 0, flags = 0;
+    unsigned long long err = ~0ull, nhits = 0, cells = 0, nacc = 0;
+    const uint32_t short_y = std::min<uint32_t>(ycap, NW_W / 2);
+    uint32_t nact = n;
+    imsame_stats st;
+    memset(&st, 0, sizeof st);
+    while (nact) {
+        st.rounds++;
+        nc[0] = nc[1] = nc[2] = 0;
+        SeedLaunch S;
+        S.db = db; S.db_start = dbs.data(); S.n_db = n_db; S.db_len = db_len;
+        S.q = q; S.q_start = qs.data(); S.n_q = n_q; S.q_len = q_len;
+        S.off = off.data(); S.ent = ent.data();
+        S.active = act.data(); S.n_active = nact;
+        S.read_from = read_from; S.T = T ? T : 1;
+        S.rpt = (uint64_t)floorl((long double)n_q / (long double)S.T);
+        S.cur_p = cur_p.data(); S.cur_h = cur_h.data(); S.memo = memo.data(); S.nmemo = nmemo.data();
+        S.rstat = rstat.data();
+        S.minraw = mr.data(); S.n_minraw = ymax + 1;
+        S.max_rs = p->max_read_size; S.short_ylen = short_y;
+        S.cread = cr.data(); S.csid = cs.data(); S.ncand = &nc[0];
+        S.cread2 = cr2.data(); S.csid2 = cs2.data(); S.ncand2 = &nc[1];
+        S.err = &err; S.nhits = &nhits;
+        for (uint32_t i = 0; i < nact; ++i) { uint64_t h = 0; seed_one(S, i, h); nhits += h; }
+        if (nc[0] + nc[1] == 0) break;
+        struct { uint32_t n; uint32_t *r, *s; imsame_read_result *o; uint32_t y; } cls[2] = {
+            {nc[0], cr.data(), cs.data(), o1.data(), short_y}, {nc[1], cr2.data(), cs2.data(), o2.data(), ycap}};
+        for (auto &c : cls) {
+            if (!c.n) continue;
+            run_nw(db, dbs.data(), q, qs.data(), c.r, c.s, c.n, p, c.y, xcap, ml, mi, c.o, paths,
+                   (uint32_t)paths_cap, &pused, &flags);
+            st.n_nw += c.n;
+            UpdLaunch U = {c.r, c.s, c.n, c.o, read_from, res, rstat.data(), memo.data(), nmemo.data(),
+                           nxt.data(), &nc[2], &cells, &nacc, dbs.data()};
+            for (uint32_t k = 0; k < c.n; ++k) { uint64_t ce = 0, ac = 0; update_one(U, k, ce, ac); cells += ce; nacc += ac; }
+        }
+        nact = nc[2];
+        std::swap(act, nxt);
+    }
+    st.n_reads = n; st.n_hits = nhits; st.nw_cells = cells; st.n_accepted = nacc;
+    st.err_read = ~0ull;
+    int ret = 0;
+    if (err != ~0ull) { st.err_read = err >> 32; st.err_dbseq = err & 0xFFFFFFFFull; ret = IMSAME_E_READ_TOO_LONG; }
+    if (paths_used) *paths_used = pused;
+    if ((flags & 1) && !ret) ret = IMSAME_E_PATHS;
+    if (stats) *stats = st;
+    return ret;
+}
+
+// table entry points for tests/test_host.py
+extern "C" uint64_t emu_minraw(uint64_t ylen, uint64_t Ldb, const imsame_params *p) {
+    return imsame_minraw(ylen, Ldb, p->min_e);
+}
+extern "C" uint32_t emu_minnum(uint64_t den, uint64_t cap, const imsame_params *p, int identity) {
+    return imsame_minnum(den, identity ? p->min_identity : p->min_coverage, cap);
+}

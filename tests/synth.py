@@ -30,34 +30,28 @@ def make_reference(total, rec_len, seed):
 def _mutate_rows(rng, src, L, sub, ins, dele):
     """src: (n, L+pad) uint8 windows -> (n, L) reads with substitutions and
     (rare) indels; indel reads are re-built individually."""
-    n = src.shape[0]
-    out = src[:, :L].copy()
+    n, W = src.shape
+    src = src.copy()
     # substitutions to a different base
-    m = rng.random((n, L)) < sub
+    m = rng.random((n, W)) < sub
     if m.any():
-        codes = np.searchsorted(ACGT, out[m])
-        shift = rng.integers(1, 4, codes.shape[0])
-        out[m] = ACGT[(codes + shift) % 4]
-    # indels
-    ev = rng.random((n, src.shape[1]))
-    has = ((ev < ins + dele).any(axis=1)).nonzero()[0]
-    for r in has.tolist():
-        row = []
-        for k in range(src.shape[1]):
-            e = ev[r, k]
-            c = int(src[r, k])
-            if e < dele:
-                continue
-            if e < dele + ins:
-                row.append(int(ACGT[rng.integers(0, 4)]))
-            if rng.random() < sub:
-                c = int(ACGT[(np.searchsorted(ACGT, c) + rng.integers(1, 4)) % 4])
-            row.append(c)
-            if len(row) >= L:
-                break
-        while len(row) < L:
-            row.append(int(ACGT[rng.integers(0, 4)]))
-        out[r] = np.array(row[:L], dtype=np.uint8)
+        codes = np.searchsorted(ACGT, src[m])
+        src[m] = ACGT[(codes + rng.integers(1, 4, codes.shape[0])) % 4]
+    out = src[:, :L].copy()
+    # indels: a deleted source base emits nothing, an insertion emits a random
+    # base before its source base; rows are then cut to L (padded if short)
+    ev = rng.random((n, W))
+    rows = np.flatnonzero((ev < ins + dele).any(axis=1))
+    if len(rows):
+        e = ev[rows]
+        keep = e >= dele
+        insb = keep & (e < dele + ins)
+        emit = keep.astype(np.int64) + insb
+        pos = np.cumsum(emit, axis=1)                          # one past this base's slot
+        buf = ACGT[rng.integers(0, 4, (len(rows), 2 * W + 1), dtype=np.uint8)]
+        rr = np.broadcast_to(np.arange(len(rows))[:, None], e.shape)
+        buf[rr[keep], (pos - 1)[keep]] = src[rows][keep]
+        out[rows] = buf[:, :L]
     return out
 
 

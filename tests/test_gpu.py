@@ -1,0 +1,181 @@
+"""GPU parity tests: the compiled HIP path (through the C-ABI) against the
+oracle and the reference's golden vectors.  Run with `pytest -m gpu`."""
+import collections
+import hashlib
+import os
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+from imsame_amd import Device, render, fasta, CLI, PARITY_FIELDS
+from imsame_amd import abi
+from tests import golden_io as G
+from tests import synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    d = Device(0)
+    yield d
+    d.close()
+
+
+def _cmp(r_dev, r_ref, limit=None):
+    n = len(r_ref) if limit is None else limit
+    bad = []
+    for f in PARITY_FIELDS:
+        idx = np.flatnonzero(r_dev[f][:n] != r_ref[f][:n])
+        bad += [(int(i), f, int(r_dev[f][i]), int(r_ref[f][i])) for i in idx[:5]]
+    return bad
+
+
+def test_nw_pairs_match_reference_golden(dev, oracle):
+    rows = G.nw_pairs()
+    groups = collections.defaultdict(list)
+    for r in rows:
+        groups[(r["igap"], r["egap"])].append(r)
+    checked_text = 0
+    for (ig, eg), rs in groups.items():
+        p = dev.params(igap=ig, egap=eg, min_coverage=1e-9, min_identity=1e-9)
+        X = [r["X"].encode() for r in rs]
+        Y = [r["Y"].encode() for r in rs]
+        res, paths, _ = dev.nw_pairs(X, Y, p, want_paths=True)
+        for k, r in enumerate(rs):
+            for f in ("score", "bx", "by", "length", "identities", "igaps", "egaps", "head_x", "head_y"):
+                assert int(res[k][f]) == r[f], (f, k, ig, eg, len(r["X"]), len(r["Y"]))
+            if res[k]["status"] == 1:
+                txt, ident = render(X[k], Y[k], res[k], paths[res[k]["path_off"]:res[k]["path_off"] + res[k]["path_len"]])
+                assert hashlib.sha1(txt).hexdigest() == r["text_sha1"]
+                assert ident == r["identities"]
+                checked_text += 1
+    assert checked_text > 250
+
+
+def _params_for(dev, case):
+    ex = case["meta"]["extra"]
+    if not ex:
+        return dev.params()
+    a = dict(zip(ex[::2], ex[1::2]))
+    return dev.params(min_e=float(a["-evalue"]), min_coverage=float(a["-coverage"]),
+                      min_identity=float(a["-identity"]), igap=-int(a["-igap"]), egap=-int(a["-egap"]))
+
+
+@pytest.mark.parametrize("name", G.e2e_cases())
+def test_align_matches_oracle_e2e(dev, oracle, name):
+    case = G.e2e_case(name)
+    db, dbs, brk = fasta.load(case["db"], True)
+    q, qs, _ = fasta.load(case["query"])
+    dev.index(db, dbs, brk)
+    dev.set_query(q, qs)
+    for T in [int(t) for t in case["meta"]["runs"]]:
+        p = _params_for(dev, case)
+        res, _, st = dev.align(n_threads=T, params=p, allow_too_long=True)
+        po = _params_for(oracle, case)        # exact long double defaults on both sides
+        rc, ref, er = oracle.align(db, dbs, q, qs, po, T, brk)
+        lim = er if rc else None
+        assert not _cmp(res, ref, lim), _cmp(res, ref, lim)
+        if rc:
+            assert st.err_read == er
+
+
+@pytest.mark.parametrize("name", G.e2e_cases())
+def test_cli_matches_reference_golden(name):
+    case = G.e2e_case(name)
+    for T in case["meta"]["runs"]:
+        with tempfile.TemporaryDirectory() as td:
+            outp = os.path.join(td, "o.align")
+            p = subprocess.run([CLI, "-query", case["query"], "-db", case["db"], "-out", outp, "-n_threads", T,
+                                *case["meta"]["extra"]], stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=300)
+            blob = open(outp, "rb").read() if os.path.exists(outp) else b""
+            G.check_cli_against_golden(case, int(T), p.returncode, p.stdout, blob)
+
+
+def test_revcomp_matches_reference_golden(dev, oracle):
+    d = os.path.join(G.GOLDEN, "revcomp")
+    names = sorted(f[:-3] for f in os.listdir(d) if f.endswith(".in"))
+    for n in names:
+        data = open(os.path.join(d, n + ".in"), "rb").read()
+        assert dev.revcomp(data) == open(os.path.join(d, n + ".out"), "rb").read(), n
+    rng = np.random.default_rng(5)
+    alphabet = np.frombuffer(b"ACGTacgtNnUuRY*-\r\n\n\n>", dtype=np.uint8)
+    for _ in range(20):
+        blob = b">h\n" + alphabet[rng.integers(0, len(alphabet), int(rng.integers(0, 5000)))].tobytes()
+        assert dev.revcomp(blob) == oracle.revcomp(blob)
+    big = synth.to_fasta(*synth.make_reference_arr(3_000_000, 150, seed=3), "m", width=70)
+    assert dev.revcomp(big) == oracle.revcomp(big)
+
+
+def test_synthetic_c2_shape_vs_oracle_all_T(dev, oracle):
+    """C2 shape scaled down: 2 Mbp in 2 kbp records, 12k x 150 bp reads."""
+    ref, rst = synth.make_reference_arr(2_000_000, 2_000, seed=42)
+    q, qs = synth.make_reads_arr(ref, 12_000, 150, seed=43)
+    dev.index(ref, rst)
+    dev.set_query(q, qs)
+    for T in (1, 8, 16):
+        res, _, st = dev.align(n_threads=T)
+        rc, exp, _ = oracle.align(ref, rst, q, qs, None, T)
+        assert rc == 0
+        assert not _cmp(res, exp), _cmp(res, exp)
+        assert (res["status"] == 1).sum() > 10_000
+    # shards with the global chunk-head semantics equal the full run
+    full, _, _ = dev.align(n_threads=8)
+    parts = [dev.align(a, b, n_threads=8)[0] for a, b in ((0, 3001), (3001, 7777), (7777, 12_000))]
+    assert not _cmp(np.concatenate(parts), full)
+
+
+def test_c1_shape_vs_oracle(dev, oracle):
+    """C1: 10k x 100 bp vs 1 Mbp (500 records), T = 1 (BASELINE configs[0])."""
+    ref, rst = synth.make_reference_arr(1_000_000, 2_000, seed=1)
+    q, qs = synth.make_reads_arr(ref, 10_000, 100, seed=2)
+    dev.index(ref, rst)
+    dev.set_query(q, qs)
+    res, _, _ = dev.align(n_threads=1)
+    rc, exp, _ = oracle.align(ref, rst, q, qs, None, 1)
+    assert not _cmp(res, exp), _cmp(res, exp)
+
+
+def test_long_reads_multi_strip(dev, oracle):
+    """Reads longer than one strip (320 columns): 600-2500 bp vs 3 kbp records."""
+    ref, rst = synth.make_reference_arr(300_000, 3_000, seed=9)
+    rng = np.random.default_rng(10)
+    reads = []
+    for k in range(60):
+        L = int(rng.integers(600, 2500))
+        o = int(rng.integers(0, len(ref) - L))
+        reads.append(ref[o:o + L].copy())
+    q = np.concatenate(reads)
+    qs = np.cumsum([0] + [len(r) for r in reads[:-1]]).astype(np.uint64)
+    dev.index(ref, rst)
+    dev.set_query(q, qs)
+    res, _, _ = dev.align(n_threads=1)
+    rc, exp, _ = oracle.align(ref, rst, q, qs, None, 1)
+    assert not _cmp(res, exp), _cmp(res, exp)
+
+
+def test_full_c2_reference_properties(dev, oracle):
+    """BASELINE configs[1] reference (50 Mbp, 25k records) with 100k reads:
+    parity on a prefix sample vs the oracle + self-consistency on all."""
+    ref, rst = synth.make_reference_arr(50_000_000, 2_000, seed=42)
+    q, qs = synth.make_reads_arr(ref, 100_000, 150, seed=43)
+    dev.index(ref, rst)
+    dev.set_query(q, qs)
+    res, paths, st = dev.align(n_threads=1, want_paths=True)
+    acc = res["status"] == 1
+    assert acc.mean() > 0.85
+    # every accepted path re-renders to the device's own identity count
+    for k in np.flatnonzero(acc)[:2000]:
+        r = res[k]
+        s = int(r["db_seq"])
+        X = ref[int(rst[s]):int(rst[s + 1]) if s + 1 < len(rst) else len(ref)]
+        Y = q[int(qs[k]):int(qs[k]) + int(r["ylen"])]
+        _, ident = render(X.tobytes(), Y.tobytes(), r, paths[r["path_off"]:r["path_off"] + r["path_len"]])
+        assert ident == r["identities"]
+    # oracle on the first 1500 reads (T = 1: only the sample's last read sees a
+    # different end-of-query bound, so it is excluded)
+    n = 1500
+    rc, exp, _ = oracle.align(ref, rst, q[:int(qs[n])], qs[:n], None, 1)
+    assert not _cmp(res[:n - 1], exp[:n - 1]), _cmp(res[:n - 1], exp[:n - 1])

@@ -1,0 +1,143 @@
+"""CPU tests of the product's host side and of the kernel SOURCE via the
+wave emulator (tests/emu): no GPU needed."""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from imsame_amd import abi, fasta
+from imsame_amd import PARITY_FIELDS
+from tests import golden_io as G
+from tests.emu_bind import Emu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "imsame_dev.h")
+LIBDEV = os.path.join(REPO, "imsame_amd", "lib", "libimsame_dev.so")
+
+
+@pytest.fixture(scope="module")
+def emu():
+    return Emu.load()
+
+
+def _declared_symbols():
+    import re
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char \*)\s*(imsame_\w+)\(", txt, re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    if not os.path.exists(LIBDEV):
+        subprocess.run(["make", "-s", "-C", os.path.join(REPO, "imsame_amd", "csrc")], check=True)
+    lib = C.CDLL(LIBDEV)
+    syms = _declared_symbols()
+    assert len(syms) >= 9, syms
+    for s in syms:
+        assert hasattr(lib, s), s
+
+
+def test_abi_struct_layout():
+    assert C.sizeof(abi.ReadResult) == 64
+    assert abi.ReadResult.path_len.offset == 60
+    assert C.sizeof(abi.Params) == 80
+    assert abi.Params.igap.offset == 48
+
+
+def test_open_without_gpu_fails_loudly():
+    import torch
+    if torch.cuda.device_count() > 0:
+        pytest.skip("a GPU is present")
+    import imsame_amd
+    with pytest.raises(imsame_amd.ImsameError):
+        imsame_amd.Device(0)
+
+
+def test_fasta_loader_matches_oracle_loader(oracle):
+    files = []
+    for c in G.e2e_cases():
+        d = G.e2e_case(c)
+        files += [d["db"], d["query"]]
+    rcd = os.path.join(G.GOLDEN, "revcomp")
+    files += [os.path.join(rcd, f) for f in sorted(os.listdir(rcd))]
+    blobs = [open(f, "rb").read() for f in files] + [
+        b"", b">", b">x", b">x\n", b"AC>x\nAC\n>", b">a\nAC\r\nGT\n>b>c\nTT\n",
+        b">a\nACGTNACGT\n>b\n\n>c\nacgtx-ACGT\n>"]
+    for data in blobs:
+        n = len(data)
+        src = np.frombuffer(data, np.uint8)
+        seq = np.zeros(n + 1, np.uint8)
+        st = np.zeros(n + 2, np.uint64)
+        bk = np.zeros(n // 8 + 2, np.uint8)
+        L, N = C.c_uint64(), C.c_uint64()
+        oracle.lib.or_parse(C.c_void_p(src.ctypes.data), C.c_uint64(n), C.c_int(1), C.c_void_p(seq.ctypes.data),
+                            C.byref(L), C.c_void_p(st.ctypes.data), C.byref(N), C.c_void_p(bk.ctypes.data))
+        s2, st2, b2 = fasta.parse(data, True)
+        nb = (L.value + 7) // 8
+        assert seq[:L.value].tobytes() == s2.tobytes()
+        assert np.array_equal(st[:N.value], st2)
+        assert bk[:nb].tobytes() == b2[:nb].tobytes()
+
+
+def test_emulated_nw_kernel_matches_reference_golden(emu, oracle):
+    """The NW kernel source, run lane by lane, against the reference's NW."""
+    rows = [r for r in G.nw_pairs() if len(r["X"]) * len(r["Y"]) <= 80_000]
+    assert len(rows) > 200
+    groups = {}
+    for r in rows:
+        groups.setdefault((r["igap"], r["egap"]), []).append(r)
+    for (ig, eg), rs in groups.items():
+        p = oracle.params(igap=ig, egap=eg)
+        rc, res, _, flags = emu.nw_pairs([r["X"].encode() for r in rs], [r["Y"].encode() for r in rs], p)
+        assert rc == 0 and flags == 0
+        for k, r in enumerate(rs):
+            for f in ("score", "bx", "by", "length", "identities", "igaps", "egaps", "head_x", "head_y"):
+                assert int(res[k][f]) == r[f], (f, ig, eg, len(r["X"]), len(r["Y"]))
+
+
+@pytest.mark.parametrize("name", ["borrowed", "edges", "reads_vs_reads", "toolong"])
+def test_emulated_pipeline_matches_oracle(emu, oracle, name):
+    """Seed scan + rounds + NW (kernel source, emulated) vs the oracle."""
+    case = G.e2e_case(name)
+    db, dbs, brk = fasta.load(case["db"], True)
+    q, qs, _ = fasta.load(case["query"])
+    for T in [int(t) for t in case["meta"]["runs"]]:
+        p = oracle.params()
+        rc1, r1, er = oracle.align(db, dbs, q, qs, p, T, brk)
+        rc2, r2, _, st = emu.align(db, dbs, q, qs, p, T, db_brk=brk)
+        assert rc1 == rc2
+        n = er if rc1 else len(r1)
+        for f in PARITY_FIELDS:
+            assert np.array_equal(r1[f][:n], r2[f][:n]), (name, T, f)
+        if rc1:
+            assert st.err_read == er
+
+
+def test_thresholds_match_long_double_tests(emu, oracle):
+    """Integer tables (csrc/tables.h) == the reference's long double tests."""
+    lib = emu.lib
+    lib.emu_minraw.restype = C.c_uint64
+    lib.emu_minraw.argtypes = [C.c_uint64, C.c_uint64, C.POINTER(abi.Params)]
+    lib.emu_minnum.restype = C.c_uint32
+    lib.emu_minnum.argtypes = [C.c_uint64, C.c_uint64, C.POINTER(abi.Params), C.c_int]
+    oracle.lib.or_epass.restype = C.c_int
+    oracle.lib.or_epass.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.POINTER(abi.Params)]
+    for p in (oracle.params(), oracle.params(min_e=1e-10), oracle.params(min_e=1e-30),
+              oracle.params(min_e=0.0)):
+        for L in (1_000_000, 50_000_000, 500_000_000):
+            for y in list(range(0, 40)) + [99, 100, 101, 149, 150, 151, 1000, 2999, 3000]:
+                m = lib.emu_minraw(y, L, C.byref(p))
+                for raw in list(range(0, 8 * y + 80, 4)) + [m - 1, m, m + 1, 2**63, 2**64 - 1]:
+                    if raw < 0 or raw >= 2**64:
+                        continue
+                    exp = oracle.lib.or_epass(raw, y, L, C.byref(p))
+                    assert (m != 2**64 - 1 and raw >= m) == bool(exp), (y, L, raw, m)
+    p = oracle.params(min_coverage=0.5, min_identity=0.9)
+    for den in range(1, 400):
+        mc = lib.emu_minnum(den, 2 * den + 8, C.byref(p), 0)
+        mi = lib.emu_minnum(den, den, C.byref(p), 1)
+        for num in range(0, 2 * den + 8):
+            assert (num >= mc) == (num / den >= 0.5)
+            if num <= den:
+                assert (num >= mi) == bool(oracle.lib.or_ident_ok(num, den, C.byref(p)))
