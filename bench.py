@@ -89,14 +89,9 @@ def main():
     elapsed = time.perf_counter() - t0
     accepted = int((res["status"] == 1).sum())
     if dist is not None:
-        import torch
-        t = torch.tensor([elapsed, float(accepted)], dtype=torch.float64, device=f"cuda:{local}")
-        tmax = t[:1].clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        tsum = t[1:].clone()
-        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
-        elapsed = float(tmax.item())
-        accepted_all = int(tsum.item())
+        from imsame_amd.dist import all_reduce     # RCCL: max of the clocks, sum of the counters
+        elapsed = all_reduce([elapsed], op="max")[0]
+        accepted_all = int(all_reduce([accepted])[0])
     else:
         accepted_all = accepted
     total_reads = world * a.reads * a.steps

@@ -556,6 +556,20 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
         uint64_t nn = 0;
         HIPCHK(hipMemcpyAsync(&nn, ctr + C_NNEXT, 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
+        if (getenv("IMSAME_DEBUG_ROUNDS")) {      // diagnostics: per-round shape + a few candidates
+            std::vector<imsame_read_result> o(std::min<uint32_t>(n1, 6));
+            std::vector<uint32_t> cr(o.size());
+            if (!o.empty()) {
+                HIPCHK(hipMemcpy(o.data(), c->cout.p, o.size() * 64, hipMemcpyDeviceToHost));
+                HIPCHK(hipMemcpy(cr.data(), c->cread.p, o.size() * 4, hipMemcpyDeviceToHost));
+            }
+            fprintf(stderr, "[round %llu] active=%u cand=%u+%u next=%llu seed_ms=%.3f |", (unsigned long long)st.rounds,
+                    nact, n1, n2, (unsigned long long)nn, fs);
+            for (size_t k = 0; k < o.size(); ++k)
+                fprintf(stderr, " r%u/s%llu st%u len%u id%u y%u", cr[k], (unsigned long long)o[k].db_seq, o[k].status,
+                        o[k].length, o[k].identities, o[k].ylen);
+            fprintf(stderr, "\n");
+        }
         nact = (uint32_t)nn;
         std::swap(act, nxt);
     }
