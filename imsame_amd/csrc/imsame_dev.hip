@@ -188,7 +188,7 @@ struct imsame_ctx {
     std::vector<uint64_t> h_q_start;
     bool have_query = false;
     // per-read state
-    DBuf res, cur_p, cur_h, memo, nmemo, rstat, act0, act1;
+    DBuf res, cur_p, cur_h, memo, nmemo, rstat, act0, act1, cbase, ccnt, perr;
     // candidates
     DBuf cread, csid, cread2, csid2, cout, cout2;
     // scalars (one block of u64 counters)
@@ -257,7 +257,7 @@ extern "C" void imsame_dev_close(imsame_ctx *c) {
                     &c->q_start, &c->res, &c->cur_p, &c->cur_h, &c->memo, &c->nmemo, &c->rstat, &c->act0,
                     &c->act1, &c->cread, &c->csid, &c->cread2, &c->csid2, &c->cout, &c->cout2, &c->ctr,
                     &c->minraw, &c->minlen, &c->minident, &c->tb, &c->bnd, &c->paths, &c->rc_in, &c->rc_out,
-                    &c->rc_a, &c->rc_b, &c->rc_c};
+                    &c->rc_a, &c->rc_b, &c->rc_c, &c->cbase, &c->ccnt, &c->perr};
     for (DBuf *b : bufs) b->release();
     (void)hipEventDestroy(c->ev0);
     (void)hipEventDestroy(c->ev1);
@@ -401,8 +401,10 @@ static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, 
     pl->steps = sh.steps;
     pl->lds = (size_t)wpb * nw_wave_lds(pl->GPW, pl->xstride);
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw_kernel, wpb * 64, pl->lds) != hipSuccess || per_cu < 1)
-        per_cu = 1;
+    hipError_t oe = (pl->nstr > 1)
+        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw_kernel<true>, wpb * 64, pl->lds)
+        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw_kernel<false>, wpb * 64, pl->lds);
+    if (oe != hipSuccess || per_cu < 1) per_cu = 1;
     per_cu = std::min(per_cu, 8);
     const uint64_t waves_needed = (ncand + pl->GPW - 1) / pl->GPW;
     pl->blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)c->ncu * per_cu, (waves_needed + wpb - 1) / wpb));
@@ -415,7 +417,7 @@ static int launch_nw(imsame_ctx *c, const NwPlan &pl, const uint32_t *cread, con
                      const uint64_t *qs, uint32_t paths_cap, double *ms) {
     hipStream_t s = c->stream;
     const unsigned slots = pl.blocks * 4;
-    const uint64_t tb_dw = (uint64_t)pl.nstr * pl.steps * 64 * NW_KW;
+    const uint64_t tb_dw = (uint64_t)pl.nstr * pl.steps * 64;      // one dword per lane per step
     if (c->tb.ensure(slots * tb_dw * 4) || c->bnd.ensure((uint64_t)slots * 3 * pl.xcap * 4 + 64)) return IMSAME_E_OOM;
     NwLaunch P;
     memset(&P, 0, sizeof P);
@@ -435,7 +437,8 @@ static int launch_nw(imsame_ctx *c, const NwPlan &pl, const uint32_t *cread, con
     P.flags = (uint32_t *)(ctr + C_FLAGS);
     HIPCHK(hipMemsetAsync(work, 0, 4, s));
     HIPCHK(hipEventRecord(c->ev0, s));
-    nw_kernel<<<pl.blocks, 256, pl.lds, s>>>(P);
+    if (pl.nstr > 1) nw_kernel<true><<<pl.blocks, 256, pl.lds, s>>>(P);
+    else             nw_kernel<false><<<pl.blocks, 256, pl.lds, s>>>(P);
     HIPCHK(hipEventRecord(c->ev1, s));
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventSynchronize(c->ev1));
@@ -487,8 +490,13 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
         c->memo.ensure((uint64_t)n * 4 * MEMO) || c->nmemo.ensure(n) || c->rstat.ensure(n) ||
         c->act0.ensure((uint64_t)n * 4) || c->act1.ensure((uint64_t)n * 4) || c->cread.ensure((uint64_t)n * 4) ||
         c->csid.ensure((uint64_t)n * 4) || c->cread2.ensure((uint64_t)n * 4) || c->csid2.ensure((uint64_t)n * 4) ||
-        c->cout.ensure((uint64_t)n * 64) || c->cout2.ensure((uint64_t)n * 64))
+        c->cout.ensure((uint64_t)n * 64) || c->cout2.ensure((uint64_t)n * 64) || c->cbase.ensure((uint64_t)n * 4) ||
+        c->ccnt.ensure((uint64_t)n * 4) || c->perr.ensure((uint64_t)n * 4))
         return IMSAME_E_OOM;
+    // speculation: round 1 emits one candidate per read (most reads accept
+    // it); later rounds emit up to SPEC_MAX, bounded by the candidate buffers
+    const char *spec_env = getenv("IMSAME_SPEC");
+    const uint32_t spec_later = spec_env ? (uint32_t)std::max(1, std::min(SPEC_MAX, atoi(spec_env))) : 4u;
     uint64_t *ctr = c->ctr.as<uint64_t>();
     HIPCHK(hipMemsetAsync(ctr, 0, C_NSLOTS * 8, s));
     const unsigned long long errinit = ~0ull;
@@ -518,6 +526,8 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
         S.nmemo = c->nmemo.as<uint8_t>(); S.rstat = c->rstat.as<uint8_t>();
         S.minraw = c->minraw.as<uint64_t>(); S.n_minraw = ymax + 1;
         S.max_rs = p->max_read_size; S.short_ylen = short_y;
+        S.spec = (st.rounds == 1) ? 1u : std::max<uint32_t>(1u, std::min<uint32_t>(spec_later, n / nact));
+        S.cbase = c->cbase.as<uint32_t>(); S.ccnt = c->ccnt.as<uint32_t>(); S.perr = c->perr.as<uint32_t>();
         S.cread = c->cread.as<uint32_t>(); S.csid = c->csid.as<uint32_t>(); S.ncand = (uint32_t *)(ctr + C_NCAND);
         S.cread2 = c->cread2.as<uint32_t>(); S.csid2 = c->csid2.as<uint32_t>(); S.ncand2 = (uint32_t *)(ctr + C_NCAND2);
         S.err = (unsigned long long *)(ctr + C_ERR); S.nhits = (unsigned long long *)(ctr + C_HITS);
@@ -547,9 +557,11 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
             if (rc) return rc;
             st.ms_nw += ms; st.nw_launches++; st.n_nw += cls[k].n;
             UpdLaunch U = {cls[k].cr, cls[k].cs, cls[k].n, cls[k].o, read_from, c->res.as<imsame_read_result>(),
-                           c->rstat.as<uint8_t>(), c->memo.as<uint32_t>(), c->nmemo.as<uint8_t>(), nxt,
+                           c->rstat.as<uint8_t>(), c->memo.as<uint32_t>(), c->nmemo.as<uint8_t>(),
+                           c->cbase.as<uint32_t>(), c->ccnt.as<uint32_t>(), c->perr.as<uint32_t>(), nxt,
                            (uint32_t *)(ctr + C_NNEXT), (unsigned long long *)(ctr + C_CELLS),
-                           (unsigned long long *)(ctr + C_NACC), c->db_start.as<uint64_t>()};
+                           (unsigned long long *)(ctr + C_NACC), (unsigned long long *)(ctr + C_ERR),
+                           c->db_start.as<uint64_t>()};
             update_kernel<<<nblk(cls[k].n, 256), 256, 0, s>>>(U);
             HIPCHK(hipGetLastError());
         }
@@ -563,8 +575,8 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
                 HIPCHK(hipMemcpy(o.data(), c->cout.p, o.size() * 64, hipMemcpyDeviceToHost));
                 HIPCHK(hipMemcpy(cr.data(), c->cread.p, o.size() * 4, hipMemcpyDeviceToHost));
             }
-            fprintf(stderr, "[round %llu] active=%u cand=%u+%u next=%llu seed_ms=%.3f |", (unsigned long long)st.rounds,
-                    nact, n1, n2, (unsigned long long)nn, fs);
+            fprintf(stderr, "[round %llu] active=%u spec=%u cand=%u+%u next=%llu seed_ms=%.3f |",
+                    (unsigned long long)st.rounds, nact, S.spec, n1, n2, (unsigned long long)nn, fs);
             for (size_t k = 0; k < o.size(); ++k)
                 fprintf(stderr, " r%u/s%llu st%u len%u id%u y%u", cr[k], (unsigned long long)o[k].db_seq, o[k].status,
                         o[k].length, o[k].identities, o[k].ylen);

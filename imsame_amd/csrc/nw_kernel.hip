@@ -17,19 +17,21 @@
 // Reads longer than NW_W/2 use one group per wave and several strips, the
 // strip seam (T[i][c], mf) passing through a per-wave global buffer.
 //
-// Per cell one 16-bit traceback code is stored (skewed layout -> every step
-// is one contiguous 768-byte wave store):
-//     diagonal : 0 / 1 (1 = X[i]==Y[j], the identity bit)
-//     up       : 0x8000 | source row   (jump from mc[j-1], column j-1)
-//     left     : 0xC000 | source col   (jump from mf, row i-1)
-// After the sweep each group walks its path from the best cell with
-// G-wide speculative diagonal reads (ballot on the first non-diagonal code).
+// Traceback: 4 bits per cell, the 5 cells of a lane packed in one dword, so a
+// step is one coalesced 256-byte wave store (0.8 B/cell):
+//     bits 0-1  move: 0 diagonal, 1 up (jump from mc[j-1]), 2 left (from mf)
+//     bit  2    U: mc[j-1] took (T[i-2][j-1], row i-2) at this cell (:476-480)
+//     bit  3    L: mf took (T[i-1][j-1], col j-1) after this cell (:434-438)
+// A jump's source is recovered in the walk: an up move at (i,j) comes from
+// row (last U of column j above i) - 2 (row 0 if none); a left move from
+// column (last L of row i left of j) - 1.  Identities are X[i]==Y[j] on the
+// diagonal steps (:254-265).  The walk reads G cells per step (ballots find
+// the first jump / the last U or L bit).
 // Scores are int32: the host rejects gap parameters whose score range could
 // leave +-2^26 (IMSAME_E_RANGE); NW_BIG = 2^28 stands for INT64_MIN.
 #include "wave_ops.h"
 
 #define NW_K   5                  // columns per lane
-#define NW_KW  3                  // dwords of traceback per lane per step
 #define NW_W   (64 * NW_K)        // columns per strip
 #define NW_BIG (1 << 28)
 
@@ -59,78 +61,264 @@ struct NwLaunch {
 // LDS bytes one wave needs
 __host__ __device__ static inline size_t nw_wave_lds(int GPW, int xstride) { return (size_t)GPW * xstride + 64 * 16; }
 
-__device__ __forceinline__ uint32_t tb_index(int st, int t, int wl, int s, int steps) {
-    // u16 index of (strip st, step t, wave lane wl, sub-column s)
-    return ((((uint32_t)st * steps + t) * 64u + wl) * NW_KW + (s >> 1)) * 2u + (s & 1);
+// dword index of (strip st, step t, wave lane wl)
+__device__ __forceinline__ uint32_t tb_word(int st, int t, int wl, int steps) {
+    return ((uint32_t)st * steps + t) * 64u + wl;
+}
+// nibble of cell (i, j) of group g
+__device__ __forceinline__ uint32_t tb_cell(const uint32_t *tb, int i, int j, int g, int G, int steps) {
+    const int st = j / NW_W, jj = j - st * NW_W, l = jj / NW_K, s = jj - l * NW_K;
+    return (tb[tb_word(st, i + l, g * G + l, steps)] >> (4 * s)) & 0xFu;
 }
 
-// Walk the traceback of group g from (px,py).  Returns path statistics;
-// emits runs into `path` when emit (lane gl == 0 writes).
+// per-candidate constants of one group, as seen by one lane
+struct NwCand {
+    const uint8_t *X;      // LDS copy of the record
+    const uint8_t *Y;      // read in global memory
+    int xlen, ylen;
+};
+
+// The sweep of one strip: rows 1 .. xlen-1 of this lane's NW_K columns.
+// SEAM_IN: the strip's lead lane takes its left neighbour from the seam
+// buffer; SEAM_OUT: the strip's last lane writes its right edge there.
+template <bool SEAM_IN, bool SEAM_OUT>
+__device__ __forceinline__ void nw_sweep(const NwLaunch &P, const NwCand &cd, uint32_t *tbw, int *bnd, const int st,
+                                         const int lane, const int gl, const int G, const int xmax, const bool cvalid,
+                                         int &bestR, int &bestRj, int &bestC, int &bestCi) {
+    const int ig = P.igap, eg = P.egap;
+    const int xlen = cd.xlen, ylen = cd.ylen;
+    const int xl1 = xlen > 1 ? xlen - 1 : 1;
+    const int j0 = st * NW_W + gl * NW_K;
+    const bool lact = cvalid && j0 < ylen;
+    const bool leadc0 = (gl == 0) && st == 0;
+    const bool lead_seam = SEAM_IN && gl == 0;
+    const bool seam_out = SEAM_OUT && (gl == G - 1) && cvalid;
+    const int lastj = ylen - 1;
+    const bool owns_last = cvalid && lastj >= j0 && lastj < j0 + NW_K;
+    const int s_last = lastj - j0;
+    int Y[NW_K], cJ[NW_K], colc[NW_K];
+#pragma unroll
+    for (int s = 0; s < NW_K; ++s) {
+        const int j = j0 + s;
+        Y[s] = (cvalid && j < ylen) ? (int)cd.Y[j] : 0;
+        cJ[s] = (j <= 1) ? -NW_BIG : ig + (j - 1) * eg;        // left needs j > 1 (:443)
+        colc[s] = -eg * (j - 1);
+    }
+    // row 0 (:404-413): T[0][j] = s(X0,Yj); mc[j] = (T[0][j], row 0)
+    const int x0 = cvalid ? (int)cd.X[0] : 0;
+    const int yprev = (cvalid && j0 > 0) ? (int)cd.Y[j0 - 1] : 0;
+    const int t0prev = (x0 == yprev) ? 4 : -4;
+    // Three rotating row buffers (cur / own = row i-1 / own2 = row i-2), all
+    // starting as row 0.  A lane repeats row 0 until its first row and runs
+    // past its last row with bounded garbage nobody reads, so every step is
+    // branch-free; row 0 standing in for row -1 cannot trigger an mc update
+    // (T[0][j-1] is not > mc[j-1] = T[0][j-1]).
+    int A[NW_K], B[NW_K], C[NW_K], mcS[NW_K], mcAdj[NW_K];
+#pragma unroll
+    for (int s = 0; s < NW_K; ++s) { A[s] = (x0 == Y[s]) ? 4 : -4; B[s] = A[s]; C[s] = A[s]; }
+#pragma unroll
+    for (int s = 0; s < NW_K; ++s) {
+        mcS[s] = (s == 0) ? t0prev : A[s - 1];
+        mcAdj[s] = mcS[s];
+        if (j0 + s == 1) mcS[s] = NW_BIG;          // mc[0] is never updated (j > 1 test, :476)
+    }
+    int I1 = t0prev, I2 = t0prev, I3 = t0prev;     // left neighbour's column, rotating like A/B/C
+    // row state crossing lanes: (T[i][c], mf score, mf score - egap * mf column)
+    int outT = A[NW_K - 1], outMS = 0, outMA = 0;
+    const int tend = xmax - 1 + G;
+    int xnext = (int)cd.X[min(max(1 - gl, 0), xl1)];
+    int bnext0 = 0, bnext1 = 0, bnext2 = 0;
+    if (lead_seam && cvalid) { bnext0 = bnd[3]; bnext1 = bnd[4]; bnext2 = bnd[5]; }
+
+    // PRE: some lane may still be before its first row (t <= G); constant at every call
+    auto step = [&](const bool PRE, const int t, int (&cur)[NW_K], const int (&own)[NW_K], const int (&own2)[NW_K],
+                    int &in0, const int in1, const int in2) {
+        int sN = wv_shr1(outT), mS = wv_shr1(outMS), mA = wv_shr1(outMA);
+        const int i = t - gl;
+        const int xi = xnext;
+        xnext = (int)cd.X[min(max(i + 1, 0), xl1)];                    // next step's row, read ahead
+        if (SEAM_IN) {
+            if (lead_seam) { sN = bnext0; mS = bnext1; mA = bnext2; }
+            const int ni = min(max(i + 1, 1), xl1);
+            if (lead_seam && cvalid) { bnext0 = bnd[3 * ni]; bnext1 = bnd[3 * ni + 1]; bnext2 = bnd[3 * ni + 2]; }
+        }
+        const bool pre = PRE && i < 1;
+        const int cI = (i <= 1) ? -NW_BIG : ig + (i - 1) * eg;        // up needs i > 1 (:449)
+        const int rowc2 = -eg * (i - 2);
+        int mfS = mS, mfAdj = mA;
+        uint32_t word = 0;
+#pragma unroll
+        for (int s = 0; s < NW_K; ++s) {
+            const int d0 = (s == 0) ? in1 : own[s - 1];     // T[i-1][j-1]
+            const int u2 = (s == 0) ? in2 : own2[s - 1];    // T[i-2][j-1]
+            const int tl = (s == 0) ? sN : cur[s - 1];      // T[i][j-1]
+            const bool m = xi == Y[s];
+            const int l0 = mfAdj + cJ[s];                   // left - s  (:444)
+            const int u0 = mcAdj[s] + cI;                   // up   - s  (:450)
+            const int mx = wv_max3(d0, l0, u0);
+            int v = mx + (m ? 4 : -4);
+            // diag if >= both, else up if up > left, else left (:457-472)
+            const uint32_t mv = (mx == d0) ? 0u : ((u0 > l0) ? 1u : 2u);
+            if (s == 0) v = leadc0 ? (m ? 4 : -4) : v;       // column 0 (:426)
+            cur[s] = pre ? own[s] : v;
+            // column max of column j-1 over rows <= i-2, strict > (:476-480)
+            const bool cu = u2 > mcS[s];
+            mcAdj[s] = cu ? u2 + rowc2 : mcAdj[s];
+            mcS[s] = max(mcS[s], u2);
+            // row state for column j+1: tested on row i, taken from row i-1 (:434-438)
+            const bool cl = mfS <= tl;
+            mfAdj = cl ? d0 + colc[s] : mfAdj;             // mf - egap * (j - 1)
+            mfS = cl ? d0 : mfS;
+            if (s == 0) mfS = leadc0 ? -NW_BIG : mfS;        // then mf = T[i-1][0]
+            word |= (mv | (cu ? 4u : 0u) | (cl ? 8u : 0u)) << (4 * s);
+        }
+        tbw[tb_word(st, t, lane, P.steps)] = word;          // rows outside [1, xlen) are never read
+        if (lact && i == xlen - 1) {                         // last row (:481)
+#pragma unroll
+            for (int s = 0; s < NW_K; ++s) {
+                const int j = j0 + s;
+                if (j >= 1 && j < ylen && cur[s] >= bestR) { bestR = cur[s]; bestRj = j; }
+            }
+        }
+        {                                                    // last column, rows 1 .. xlen-2
+            int v = cur[0];
+#pragma unroll
+            for (int s = 1; s < NW_K; ++s) v = (s_last == s) ? cur[s] : v;
+            const bool up = owns_last && i >= 1 && i < xlen - 1 && v >= bestC;
+            bestC = up ? v : bestC;
+            bestCi = up ? i : bestCi;
+        }
+        in0 = pre ? in1 : sN;
+        outT = cur[NW_K - 1]; outMS = mfS; outMA = mfAdj;
+        if (seam_out && i >= 1 && i < xlen) { bnd[3 * i] = outT; bnd[3 * i + 1] = mfS; bnd[3 * i + 2] = mfAdj; }
+    };
+    // roles (cur, own, own2) and (in0 <- T[i][c], in1 = T[i-1][c], in2 = T[i-2][c]) rotate every step
+    int t = 1;
+    for (; t + 2 < tend && t <= G; t += 3) {      // skewed start: lanes may be before row 1
+        step(true, t, A, B, C, I3, I1, I2);
+        step(true, t + 1, C, A, B, I2, I3, I1);
+        step(true, t + 2, B, C, A, I1, I2, I3);
+    }
+    for (; t + 2 < tend; t += 3) {
+        step(false, t, A, B, C, I3, I1, I2);       // A = row i,   B = i-1, C = i-2
+        step(false, t + 1, C, A, B, I2, I3, I1);   // C = row i+1, A = i,   B = i-1
+        step(false, t + 2, B, C, A, I1, I2, I3);   // B = row i+2, C = i+1, A = i
+    }
+    if (t < tend) step(true, t, A, B, C, I3, I1, I2);
+    if (t + 1 < tend) step(true, t + 1, C, A, B, I2, I3, I1);
+}
+
+// Walk the traceback of group g from (px,py) (backtrackingNW, :493-560).
+// Returns path statistics; emits runs into `path` when emit (lane gl == 0).
 struct WalkOut { int len, idn, ig, eg, cx, cy, nent; bool bad; };
 
-__device__ WalkOut nw_walk(const uint16_t *tb16, int px, int py, bool walking, int g, int gl, int G,
-                           int steps, uint32_t *path, bool emit) {
+__device__ WalkOut nw_walk(const uint32_t *tb, const NwCand &cd, int px, int py, bool walking, int g, int gl,
+                           int G, int steps, uint32_t *path, bool emit) {
     WalkOut w = {0, 0, 0, 0, px, py, 0, false};
     const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1);
     int run = 0;                       // pending diagonal run (emit) / in-run flag
-    int guard = px + py + 4;           // every iteration moves at least one cell
+    int guard = 4 * (cd.xlen + cd.ylen) + 8;
     walking = walking && px > 0 && py > 0;
     while (wv_any(walking)) {
+        // G diagonal cells at once; the first non-diagonal one stops the run
         const int cx = px - gl, cy = py - gl;
         const bool valid = walking && cx >= 1 && cy >= 1;
-        uint32_t code = 0xFFFFu;
+        uint32_t nib = 0xFu;
+        bool match = false;
         if (valid) {
-            const int st = cy / NW_W, jj = cy - st * NW_W, l = jj / NW_K, s = jj - l * NW_K;
-            code = tb16[tb_index(st, cx + l, g * G + l, s, steps)];
+            nib = tb_cell(tb, cx, cy, g, G, steps);
+            match = cd.X[cx] == cd.Y[cy];
         }
-        const bool stop = !valid || (code >> 14) != 0;
-        const unsigned long long bs = wv_ballot(stop), bmatch = wv_ballot(valid && code == 1u);
+        const bool stop = !valid || (nib & 3u) != 0;
+        const unsigned long long bs = wv_ballot(stop), bm = wv_ballot(valid && match);
         const unsigned long long gs = (bs >> (g * G)) & gmask;
         const int first = gs ? __builtin_ctzll(gs) : G;
         const unsigned long long below = (first >= 64) ? ~0ull : ((1ull << first) - 1);
-        const int nm = __builtin_popcountll((bmatch >> (g * G)) & gmask & below);
-        const uint32_t gcode = (uint32_t)wv_shfl((int)code, g * G + (first < G ? first : 0));
+        const int nm = __builtin_popcountll((bm >> (g * G)) & gmask & below);
+        const uint32_t mvj = (uint32_t)wv_shfl((int)(nib & 3u), g * G + (first < G ? first : 0));
         if (walking) {
             if (first > 0) {
                 if (!run) w.nent++;
                 if (emit) run += first; else run = 1;
                 w.len += first; w.idn += nm; px -= first; py -= first;
             }
-            if (first < G && px > 0 && py > 0) {          // a jump at (px,py)
-                const int src = (int)(gcode & 0x3FFFu);
-                const bool up = (gcode >> 14) == 2u;
-                int n;
-                if (up) { n = px - src; px = src; py -= 1; }    // X run vs '-'  (:520-530)
-                else    { n = py - src; py = src; px -= 1; }    // '-' vs Y run  (:531-543)
-                if (n < 1 || (gcode >> 14) < 2u) { w.bad = true; walking = false; }
-                if (emit && gl == 0 && !w.bad) {
-                    if (run) path[w.nent - 1] = (IMSAME_MOVE_DIAG << 30) | (uint32_t)run;
-                    path[w.nent] = ((up ? IMSAME_MOVE_UP : IMSAME_MOVE_LEFT) << 30) | (uint32_t)n;
+        }
+        const bool jump = walking && first < G && px > 0 && py > 0;
+        if (walking && jump && (mvj == 0u || mvj == 3u)) { w.bad = true; walking = false; }
+        // up: last row i < px of column py with U set -> source row i-2 (0 if none)
+        const bool want_up = wv_any(jump && !w.bad && mvj == 1u);
+        const bool want_left = wv_any(jump && !w.bad && mvj == 2u);
+        int src = 0;
+        bool is_up = jump && mvj == 1u, is_left = jump && mvj == 2u;
+        if (want_up) {
+            bool searching = is_up;
+            int base = px - 1;
+            src = 0;
+            while (wv_any(searching)) {
+                const int r = base - gl;
+                const bool ok = searching && r >= 1;
+                const bool u = ok && ((tb_cell(tb, r, py, g, G, steps) >> 2) & 1u);
+                const unsigned long long gb = (wv_ballot(u) >> (g * G)) & gmask;
+                if (searching) {
+                    if (gb) { src = base - __builtin_ctzll(gb) - 2; searching = false; }
+                    else if (base - G < 1) { src = 0; searching = false; }
+                    else base -= G;
                 }
-                w.nent++;
-                run = 0;
-                w.len += n; w.eg += n - 1; w.ig += 1;
             }
-            walking = walking && px > 0 && py > 0;
+        }
+        if (want_left) {
+            bool searching = is_left;
+            int base = py - 1;
+            int lsrc = 0;
+            while (wv_any(searching)) {
+                const int c = base - gl;
+                const bool ok = searching && c >= 1;
+                const bool l = ok && ((tb_cell(tb, px, c, g, G, steps) >> 3) & 1u);
+                const unsigned long long gb = (wv_ballot(l) >> (g * G)) & gmask;
+                if (searching) {
+                    if (gb) { lsrc = base - __builtin_ctzll(gb) - 1; searching = false; }
+                    else if (base - G < 1) { w.bad = true; searching = false; }   // L(i,1) always set
+                    else base -= G;
+                }
+            }
+            if (is_left) src = lsrc;
+        }
+        if (walking && jump && !w.bad) {
+            int n;
+            if (is_up) { n = px - src; px = src; py -= 1; }     // X run vs '-'  (:520-530)
+            else       { n = py - src; py = src; px -= 1; }     // '-' vs Y run  (:531-543)
+            if (n < 1) { w.bad = true; walking = false; }
+            if (emit && gl == 0 && !w.bad) {
+                if (run) path[w.nent - 1] = (IMSAME_MOVE_DIAG << 30) | (uint32_t)run;
+                path[w.nent] = ((is_up ? IMSAME_MOVE_UP : IMSAME_MOVE_LEFT) << 30) | (uint32_t)n;
+            }
+            w.nent++;
+            run = 0;
+            w.len += n; w.eg += n - 1; w.ig += 1;
+        }
+        if (w.bad) walking = false;
+        if (walking) {
+            walking = px > 0 && py > 0;
             if (--guard < 0) { w.bad = true; walking = false; }
         }
     }
-    if (emit && gl == 0 && run) path[w.nent - 1] = (IMSAME_MOVE_DIAG << 30) | (uint32_t)run;
+    if (emit && gl == 0 && run && !w.bad) path[w.nent - 1] = (IMSAME_MOVE_DIAG << 30) | (uint32_t)run;
     w.cx = px; w.cy = py;
     return w;
 }
 
 // One wave's share of a launch: pulls groups of GPW candidates from the work
 // queue until it is empty.  wsm = this wave's LDS (nw_wave_lds bytes).
+// MULTI: the launch holds reads longer than one strip (one group per wave).
+template <bool MULTI>
 __device__ void nw_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const uint32_t slot) {
     const int G = P.G, GPW = P.GPW;
     const int g = lane / G, gl = lane - g * G;
     const bool in_group = g < GPW;
+    const int gg = in_group ? g : 0;
     int *red = (int *)(wsm + GPW * P.xstride);                      // 64 x 4 ints
     uint32_t *tbw = P.tb + (uint64_t)slot * P.tb_wave_dw;
-    const uint16_t *tb16 = (const uint16_t *)tbw;
     int *bnd = P.bnd + (uint64_t)slot * P.bnd_wave;
-    const int ig = P.igap, eg = P.egap;
 
     for (;;) {
         uint32_t base = 0;
@@ -139,125 +327,44 @@ __device__ void nw_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const u
         if (base >= P.n_cand) break;
         const uint32_t c = base + g;
         const bool cvalid = in_group && c < P.n_cand;
-        int xlen = 0, ylen = 0;
-        uint64_t xo = 0, yo = 0;
+        NwCand cd;
+        cd.X = wsm + gg * P.xstride;
+        cd.Y = P.q;
+        cd.xlen = 0; cd.ylen = 0;
+        uint64_t xo = 0;
         uint32_t sid = 0;
         if (cvalid) {
             const uint32_t rd = P.cand_read[c];
             sid = P.cand_sid[c];
-            xo = P.db_start[sid]; xlen = (int)(P.db_start[sid + 1] - xo);
-            yo = P.q_start[rd];   ylen = (int)(P.q_start[rd + 1] - yo);
+            xo = P.db_start[sid]; cd.xlen = (int)(P.db_start[sid + 1] - xo);
+            const uint64_t yo = P.q_start[rd];
+            cd.Y = P.q + yo; cd.ylen = (int)(P.q_start[rd + 1] - yo);
         }
-        uint8_t *X = wsm + (in_group ? g : 0) * P.xstride;
         if (cvalid)
-            for (int k = gl; k < xlen; k += G) X[k] = P.db[xo + k];
+            for (int k = gl; k < cd.xlen; k += G) ((uint8_t *)cd.X)[k] = P.db[xo + k];
         wv_lds_sync();
 
-        int xmax = xlen, nstr = cvalid ? (ylen + NW_W - 1) / NW_W : 0;
+        int xmax = cd.xlen, nstr = cvalid ? (cd.ylen + NW_W - 1) / NW_W : 0;
         for (int o = 32; o > 0; o >>= 1) {
             xmax = max(xmax, wv_shfl_xor(xmax, o));
             nstr = max(nstr, wv_shfl_xor(nstr, o));
         }
         int bestR = INT_MIN, bestRj = 0, bestC = INT_MIN, bestCi = 0;
-        const int lastj = ylen - 1;
-
-        for (int st = 0; st < nstr; ++st) {
-            const int j0 = st * NW_W + gl * NW_K;
-            const bool lact = cvalid && j0 < ylen;
-            const bool leadc0 = (gl == 0) && st == 0;
-            const bool lead_seam = (gl == 0) && st > 0;
-            const bool seam_out = (gl == G - 1) && (st + 1) * NW_W < ylen && cvalid;
-            const bool owns_last = cvalid && lastj >= j0 && lastj < j0 + NW_K;
-            const int s_last = lastj - j0;
-            int Y[NW_K], cJ[NW_K], colc[NW_K], colcode[NW_K];
-#pragma unroll
-            for (int s = 0; s < NW_K; ++s) {
-                const int j = j0 + s;
-                Y[s] = (cvalid && j < ylen) ? (int)P.q[yo + j] : 0;
-                cJ[s] = (j <= 1) ? -NW_BIG : ig + (j - 1) * eg;        // left needs j > 1 (:443)
-                colc[s] = -eg * (j - 1);
-                colcode[s] = 0xC000 | ((j - 1) & 0x3FFF);
+        if (!MULTI) {
+            nw_sweep<false, false>(P, cd, tbw, bnd, 0, lane, gl, G, xmax, cvalid, bestR, bestRj, bestC, bestCi);
+        } else {
+            for (int st = 0; st < nstr; ++st) {
+                const bool in = st > 0, outs = st + 1 < nstr;
+                if (!in && outs)
+                    nw_sweep<false, true>(P, cd, tbw, bnd, st, lane, gl, G, xmax, cvalid, bestR, bestRj, bestC, bestCi);
+                else if (in && outs)
+                    nw_sweep<true, true>(P, cd, tbw, bnd, st, lane, gl, G, xmax, cvalid, bestR, bestRj, bestC, bestCi);
+                else
+                    nw_sweep<true, false>(P, cd, tbw, bnd, st, lane, gl, G, xmax, cvalid, bestR, bestRj, bestC, bestCi);
+                wv_mem_sync();                    // seam written by the last lane, read by the lead
             }
-            // row 0 (alignmentFunctions.c:404-413): T[0][j] = s(X0,Yj), mc[j] = (T[0][j], row 0)
-            const int x0 = cvalid ? (int)X[0] : 0;
-            const int yprev = (cvalid && j0 > 0) ? (int)P.q[yo + j0 - 1] : 0;
-            const int t0prev = (x0 == yprev) ? 4 : -4;
-            int own[NW_K], own2[NW_K], mcS[NW_K], mcAdj[NW_K], mcCode[NW_K];
-#pragma unroll
-            for (int s = 0; s < NW_K; ++s) {
-                own[s] = (x0 == Y[s]) ? 4 : -4;
-                own2[s] = -NW_BIG;
-            }
-#pragma unroll
-            for (int s = 0; s < NW_K; ++s) {
-                mcS[s] = (s == 0) ? t0prev : own[s - 1];
-                mcAdj[s] = mcS[s];
-                mcCode[s] = 0x8000;
-                if (j0 + s == 1) mcS[s] = NW_BIG;     // mc[0] is never updated (j > 1 test, :476)
-            }
-            int in1 = t0prev, in2 = -NW_BIG;
-            int outT = own[NW_K - 1], outMS = 0, outMC = 0;
-            const int tend = xmax - 1 + G;
-            for (int t = 1; t < tend; ++t) {
-                int sN = wv_shr1(outT), mS = wv_shr1(outMS), mC = wv_shr1(outMC);
-                const int i = t - gl;
-                const bool act = lact && i >= 1 && i < xlen;
-                if (lead_seam && act) { sN = bnd[3 * i]; mS = bnd[3 * i + 1]; mC = bnd[3 * i + 2]; }
-                if (act) {
-                    const int xi = X[i];
-                    const int cI = (i == 1) ? -NW_BIG : ig + (i - 1) * eg;   // up needs i > 1 (:449)
-                    const int rowc2 = -eg * (i - 2);
-                    const int code2 = 0x8000 | ((i - 2) & 0x3FFF);
-                    int mfS = mS, mfCode = mC, mfAdj = mS - eg * (mC & 0x3FFF);
-                    int cur[NW_K];
-                    uint32_t code[NW_K];
-#pragma unroll
-                    for (int s = 0; s < NW_K; ++s) {
-                        const int d0 = (s == 0) ? in1 : own[s - 1];     // T[i-1][j-1]
-                        const int u2 = (s == 0) ? in2 : own2[s - 1];    // T[i-2][j-1]
-                        const int tl = (s == 0) ? sN : cur[s - 1];      // T[i][j-1]
-                        const bool m = xi == Y[s];
-                        const int sc = m ? 4 : -4;
-                        const int l0 = mfAdj + cJ[s];                   // left  - s  (:444)
-                        const int u0 = mcAdj[s] + cI;                   // up    - s  (:450)
-                        const int mx = max(l0, u0);
-                        int v = max(d0, mx) + sc;
-                        // diag if >= both, else up if up > left, else left (:457-472)
-                        const uint32_t cd = (d0 >= mx) ? (uint32_t)m : (uint32_t)((u0 > l0) ? mcCode[s] : mfCode);
-                        if (s == 0) v = leadc0 ? sc : v;                 // column 0 (:426)
-                        cur[s] = v;
-                        code[s] = cd;
-                        // column max of column j-1 over rows <= i-2, strict > (:476-480)
-                        if (u2 > mcS[s]) { mcS[s] = u2; mcAdj[s] = u2 + rowc2; mcCode[s] = code2; }
-                        // row state for column j+1: tested on row i, taken from row i-1 (:434-438)
-                        if (mfS <= tl) { mfS = d0; mfAdj = d0 + colc[s]; mfCode = colcode[s]; }
-                        if (s == 0) mfS = leadc0 ? -NW_BIG : mfS;        // then mf = T[i-1][0]
-                    }
-                    uint32_t *dst = tbw + (((uint32_t)st * P.steps + t) * 64u + lane) * NW_KW;
-                    dst[0] = code[0] | (code[1] << 16);
-                    dst[1] = code[2] | (code[3] << 16);
-                    dst[2] = code[4];
-                    if (i == xlen - 1) {                                 // last row (:481)
-#pragma unroll
-                        for (int s = 0; s < NW_K; ++s) {
-                            const int j = j0 + s;
-                            if (j >= 1 && j < ylen && cur[s] >= bestR) { bestR = cur[s]; bestRj = j; }
-                        }
-                    } else if (owns_last) {                              // last column, rows < xlen-1
-                        int v = cur[0];
-#pragma unroll
-                        for (int s = 1; s < NW_K; ++s) v = (s_last == s) ? cur[s] : v;
-                        if (v >= bestC) { bestC = v; bestCi = i; }
-                    }
-                    in2 = in1; in1 = sN;
-#pragma unroll
-                    for (int s = 0; s < NW_K; ++s) { own2[s] = own[s]; own[s] = cur[s]; }
-                    outT = cur[NW_K - 1]; outMS = mfS; outMC = mfCode;
-                    if (seam_out) { bnd[3 * i] = outT; bnd[3 * i + 1] = mfS; bnd[3 * i + 2] = mfCode; }
-                }
-            }
-            wv_mem_sync();
         }
+        wv_mem_sync();                            // traceback written by all lanes, read by the walkers
 
         // best cell (:481-484): row-major order, ">=" -> last visited wins:
         // last-row cells (largest j) beat last-column cells (largest i).
@@ -272,15 +379,14 @@ __device__ void nw_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const u
                 if (e[2] > bC || (e[2] == bC && e[3] > bCi)) { bC = e[2]; bCi = e[3]; }
             }
         int bscore, bx, by;
-        if (bR >= bC) { bscore = bR; bx = xlen - 1; by = bRj; }
-        else          { bscore = bC; bx = bCi; by = ylen - 1; }
+        if (bR >= bC) { bscore = bR; bx = cd.xlen - 1; by = bRj; }
+        else          { bscore = bC; bx = bCi; by = cd.ylen - 1; }
         wv_lds_sync();
 
-        const int gg = in_group ? g : 0;
-        WalkOut w = nw_walk(tb16, bx, by, cvalid, gg, gl, G, P.steps, nullptr, false);
+        WalkOut w = nw_walk(tbw, cd, bx, by, cvalid, gg, gl, G, P.steps, nullptr, false);
         bool acc = false;
         if (cvalid && !w.bad) {
-            acc = (uint32_t)ylen < P.n_minlen && (uint32_t)w.len >= P.minlen[ylen] &&
+            acc = (uint32_t)cd.ylen < P.n_minlen && (uint32_t)w.len >= P.minlen[cd.ylen] &&
                   (uint32_t)w.len < P.n_minident && (uint32_t)w.idn >= P.minident[w.len];
         }
         if (cvalid && w.bad && gl == 0) wv_atomic_or(P.flags, 2u);
@@ -294,19 +400,19 @@ __device__ void nw_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const u
             }
             off = (uint32_t)wv_shfl((int)off, gg * G);
             const bool ok = want && off != 0xFFFFFFFFu;
-            nw_walk(tb16, bx, by, ok, gg, gl, G, P.steps, ok ? P.paths + off : nullptr, true);
+            nw_walk(tbw, cd, bx, by, ok, gg, gl, G, P.steps, ok ? P.paths + off : nullptr, true);
             if (ok) { poff = off; plen = (uint32_t)w.nent; }
         }
         if (cvalid && gl == 0) {
-            const int M = 2 * max(xlen, ylen);
+            const int M = 2 * max(cd.xlen, cd.ylen);
             const int tail = w.cx + w.cy;                    // one of them is 0
             imsame_read_result r;
             r.db_seq = sid; r.score = bscore; r.bx = (uint32_t)bx; r.by = (uint32_t)by;
             r.length = (uint32_t)w.len; r.identities = (uint32_t)w.idn;
             r.igaps = (uint32_t)w.ig; r.egaps = (uint32_t)w.eg;
-            r.head_x = (uint32_t)(M - ((xlen - 1 - bx) + w.len + tail));
-            r.head_y = (uint32_t)(M - ((ylen - 1 - by) + w.len + tail));
-            r.ylen = (uint32_t)ylen; r.status = acc ? 1u : 2u;
+            r.head_x = (uint32_t)(M - ((cd.xlen - 1 - bx) + w.len + tail));
+            r.head_y = (uint32_t)(M - ((cd.ylen - 1 - by) + w.len + tail));
+            r.ylen = (uint32_t)cd.ylen; r.status = acc ? 1u : 2u;
             r.path_off = poff; r.path_len = plen;
             P.out[c] = r;
         }
@@ -333,12 +439,15 @@ __host__ static inline NwShape nw_shape(uint32_t ymax, uint32_t xcap) {
     s.steps = s.xcap + s.G;
     return s;
 }
+// traceback dwords per wave slot
+__host__ static inline uint64_t nw_tb_words(const NwShape &s) { return (uint64_t)s.nstr * s.steps * 64; }
 
 #ifndef IMSAME_WAVE_EMU
+template <bool MULTI>
 __global__ __launch_bounds__(256) void nw_kernel(NwLaunch P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
     const uint32_t slot = blockIdx.x * (blockDim.x >> 6) + wib;
-    nw_wave(P, smem + wib * nw_wave_lds(P.GPW, P.xstride), lane, slot);
+    nw_wave<MULTI>(P, smem + wib * nw_wave_lds(P.GPW, P.xstride), lane, slot);
 }
 #endif

@@ -10,7 +10,7 @@
 // record is not already known to be rejected for this read.
 #include "wave_ops.h"
 
-#define MEMO 4
+#define MEMO 16
 #define NBUCKETS (1u << 24)
 enum { RS_ACTIVE = 0, RS_DONE = 1, RS_ACCEPTED = 2, RS_ERROR = 3 };
 
@@ -25,11 +25,15 @@ struct SeedLaunch {
     uint64_t *cur_p; uint32_t *cur_h; uint32_t *memo; uint8_t *nmemo; uint8_t *rstat;
     const uint64_t *minraw; uint32_t n_minraw;
     uint64_t max_rs; uint32_t short_ylen;
+    uint32_t spec;                         // candidates a read may emit this round (1..SPEC_MAX)
+    uint32_t *cbase, *ccnt;                // per read: first slot and count of this round's candidates
+    uint32_t *perr;                        // per read: 1 + record of a pending size error, 0 = none
     uint32_t *cread, *csid, *ncand;        // class 0: ylen <= short_ylen
     uint32_t *cread2, *csid2, *ncand2;     // class 1: longer reads
     unsigned long long *err;               // min (read << 32 | record)
     unsigned long long *nhits;
 };
+#define SPEC_MAX 8
 
 // alignmentFromQuickHits (alignmentFunctions.c:276-387): the raw score in the
 // reference's u64 wrap arithmetic (:373).  Loop bounds fold the reference's
@@ -77,9 +81,15 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint
     for (int m = 0; m < MEMO; ++m) memo[m] = (m < (int)nm) ? S.memo[k * MEMO + m] : 0xFFFFFFFFu;
     const uint64_t mraw = ylen < S.n_minraw ? S.minraw[ylen] : ~0ull;
     const int64_t ys = (int64_t)rs, ye = (r == S.n_q - 1) ? (int64_t)S.q_len : (int64_t)re - 1;
+    // Up to `spec` e-value-passing hits of distinct, not-yet-rejected records,
+    // in visiting order.  NW(record, read) is pure (Q18): whichever of them is
+    // accepted first in this order is exactly the reference's accepted hit,
+    // and a later hit of an emitted or rejected record cannot change that.
+    uint32_t emit[SPEC_MAX];
+    uint32_t ne = 0, perr = 0;
     uint32_t code = 0;
-    bool have = false, found = false;
-    for (; p < up_to; ++p, h = 0) {
+    bool have = false, stop = false;
+    for (; p < up_to && !stop; ++p, h = 0) {
         if (!have) {
             code = 0;
             for (int t = IMSAME_FIXED_K - 1; t >= 0; --t) code = (code << 2) | base2(S.q[p - t]);
@@ -94,7 +104,8 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint
             bool skip = false;
 #pragma unroll
             for (int m = 0; m < MEMO; ++m) skip |= memo[m] == sid;
-            if (skip) continue;                 // NW(sid, r) already rejected (Q18)
+            for (uint32_t m = 0; m < ne; ++m) skip |= emit[m] == sid;
+            if (skip) continue;                 // NW(sid, r) already rejected or pending (Q18)
             const int64_t xs = (int64_t)S.db_start[sid];
             const int64_t xe = (sid == S.n_db - 1) ? (int64_t)S.db_len : (int64_t)S.db_start[sid + 1] - 1;
             ++hits;
@@ -102,26 +113,37 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint
                                               (int64_t)S.db_len, (int64_t)S.q_len);
             if (mraw != ~0ull && raw >= mraw) {                      // e < min_e (:139)
                 const uint64_t xlen = S.db_start[sid + 1] - S.db_start[sid];
-                if (xlen > S.max_rs || ylen > S.max_rs) {            // terror (:155)
-                    S.rstat[k] = RS_ERROR;
-                    wv_atomic_min64(S.err, (unsigned long long)((r << 32) | sid));
-                } else {
-                    S.cur_p[k] = p; S.cur_h[k] = h + 1;
-                    if (ylen <= S.short_ylen) {
-                        const uint32_t o = wv_atomic_add(S.ncand, 1u);
-                        S.cread[o] = (uint32_t)r; S.csid[o] = sid;
-                    } else {
-                        const uint32_t o = wv_atomic_add(S.ncand2, 1u);
-                        S.cread2[o] = (uint32_t)r; S.csid2[o] = sid;
-                    }
+                if (xlen > S.max_rs || ylen > S.max_rs) {            // terror (:155) if reached
+                    perr = sid + 1;
+                    stop = true;
+                    break;
                 }
-                found = true;
-                break;
+                emit[ne++] = sid;
+                if (ne == S.spec) {
+                    S.cur_p[k] = p; S.cur_h[k] = h + 1;              // resume after this hit
+                    stop = true;
+                    break;
+                }
             }
         }
-        if (found) break;
+        if (stop) break;
     }
-    if (!found) S.rstat[k] = RS_DONE;
+    if (ne == 0) {
+        if (perr) {
+            S.rstat[k] = RS_ERROR;
+            wv_atomic_min64(S.err, (unsigned long long)((r << 32) | (perr - 1)));
+        } else {
+            S.rstat[k] = RS_DONE;
+        }
+        return;
+    }
+    if (ne < S.spec && !perr) { S.cur_p[k] = up_to; S.cur_h[k] = 0; }   // scan exhausted
+    S.perr[k] = perr;
+    const bool shortc = ylen <= S.short_ylen;
+    const uint32_t o = wv_atomic_add(shortc ? S.ncand : S.ncand2, ne);
+    uint32_t *cr = shortc ? S.cread : S.cread2, *cs = shortc ? S.csid : S.csid2;
+    for (uint32_t m = 0; m < ne; ++m) { cr[o + m] = (uint32_t)r; cs[o + m] = emit[m]; }
+    S.cbase[k] = o; S.ccnt[k] = ne;
 }
 
 struct UpdLaunch {
@@ -130,27 +152,44 @@ struct UpdLaunch {
     uint64_t read_from;
     imsame_read_result *res;
     uint8_t *rstat; uint32_t *memo; uint8_t *nmemo;
+    const uint32_t *cbase, *ccnt, *perr;
     uint32_t *next; uint32_t *nnext;
     unsigned long long *cells; unsigned long long *nacc;
+    unsigned long long *err;
     const uint64_t *db_start;
 };
 
-// accepted -> the read's result (NWaligned = 1, :172); rejected -> remember
-// the record and keep scanning from the cursor next round
+// Per read (run by its first candidate): the first accepted candidate in
+// visiting order is the read's result (NWaligned = 1, :172); rejected ones
+// before it are remembered; none accepted -> a pending size error fires
+// (terror, :155) or the read continues from its cursor next round.
 __device__ __forceinline__ void update_one(const UpdLaunch &U, uint32_t c, uint64_t &cells, uint64_t &acc) {
     const uint32_t r = U.cread[c];
     const uint64_t k = r - U.read_from;
-    const imsame_read_result o = U.out[c];
-    cells += (uint64_t)(U.db_start[o.db_seq + 1] - U.db_start[o.db_seq]) * o.ylen;
-    if (o.status == 1) {
-        U.res[k] = o;
-        U.rstat[k] = RS_ACCEPTED;
-        acc += 1;
-    } else {
-        const uint32_t nm = U.nmemo[k];
-        if (nm < MEMO) { U.memo[k * MEMO + nm] = (uint32_t)o.db_seq; U.nmemo[k] = (uint8_t)(nm + 1); }
-        U.next[wv_atomic_add(U.nnext, 1u)] = r;
+    const imsame_read_result oc = U.out[c];
+    cells += (uint64_t)(U.db_start[oc.db_seq + 1] - U.db_start[oc.db_seq]) * oc.ylen;
+    const uint32_t base = U.cbase[k];
+    if (c != base) return;
+    const uint32_t cnt = U.ccnt[k];
+    uint32_t nm = U.nmemo[k];
+    for (uint32_t m = 0; m < cnt; ++m) {
+        const imsame_read_result o = U.out[base + m];
+        if (o.status == 1) {
+            U.res[k] = o;
+            U.rstat[k] = RS_ACCEPTED;
+            acc += 1;
+            U.nmemo[k] = (uint8_t)nm;
+            return;
+        }
+        if (nm < MEMO) U.memo[k * MEMO + nm++] = (uint32_t)o.db_seq;
     }
+    U.nmemo[k] = (uint8_t)nm;
+    if (U.perr[k]) {
+        U.rstat[k] = RS_ERROR;
+        wv_atomic_min64(U.err, (unsigned long long)(((uint64_t)r << 32) | (U.perr[k] - 1)));
+        return;
+    }
+    U.next[wv_atomic_add(U.nnext, 1u)] = r;
 }
 
 struct InitLaunch {

@@ -13,6 +13,12 @@
 
 // lane l receives lane l-1's value (lane 0 receives 0): DPP wave_shr:1
 WV_DEVICE int wv_shr1(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, false); }
+// max of three signed ints in one VALU op (v_max3_i32)
+WV_DEVICE int wv_max3(int a, int b, int c) {
+    int r;
+    asm("v_max3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
 WV_DEVICE unsigned long long wv_ballot(bool p) { return __ballot(p); }
 WV_DEVICE bool wv_any(bool p) { return __any(p); }
 WV_DEVICE int wv_shfl(int v, int src) { return __shfl(v, src); }
@@ -61,6 +67,8 @@ extern thread_local uint64_t *t_xch;
 }
 
 inline int wv_lane() { return wvemu::t_lane; }
+inline int __mul24(int a, int b) { return a * b; }
+inline int wv_max3(int a, int b, int c) { return std::max(a, std::max(b, c)); }
 inline int wv_shr1(int v) {
     wvemu::t_xch[wvemu::t_lane] = (uint64_t)(uint32_t)v;
     wvemu::sync();

@@ -47,7 +47,7 @@ static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, cons
                   uint32_t xmax, const std::vector<uint32_t> &ml, const std::vector<uint32_t> &mi,
                   imsame_read_result *out, uint32_t *paths, uint32_t pcap, uint32_t *pused, uint32_t *flags) {
     const NwShape sh = nw_shape(ymax, xmax);
-    std::vector<uint32_t> tb((size_t)sh.nstr * sh.steps * 64 * NW_KW + 64, 0xABABABABu);
+    std::vector<uint32_t> tb(nw_tb_words(sh) + 64, 0xABABABABu);
     std::vector<int32_t> bnd((size_t)3 * sh.xcap + 64);
     std::vector<uint8_t> lds(nw_wave_lds(sh.GPW, sh.xstride) + 64);
     uint32_t counter = 0;
@@ -64,7 +64,8 @@ static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, cons
     P.counter = &counter; P.out = out;
     P.paths = paths; P.paths_cap = pcap; P.paths_used = pused; P.want_paths = p->want_paths;
     P.flags = flags;
-    run_wave([&](int lane) { nw_wave(P, lds.data(), lane, 0); });
+    if (sh.nstr > 1) run_wave([&](int lane) { nw_wave<true>(P, lds.data(), lane, 0); });
+    else             run_wave([&](int lane) { nw_wave<false>(P, lds.data(), lane, 0); });
     return 0;
 }
 
@@ -140,6 +141,9 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
     const uint32_t n = (uint32_t)(read_to - read_from);
     std::vector<uint64_t> cur_p(n);
     std::vector<uint32_t> cur_h(n), memo((size_t)n * MEMO), act(n), nxt(n), cr(n), cs(n), cr2(n), cs2(n);
+    std::vector<uint32_t> cbase(n), ccnt(n), perr(n);
+    const char *spec_env = getenv("IMSAME_SPEC");
+    const uint32_t spec_later = spec_env ? (uint32_t)std::max(1, std::min(SPEC_MAX, atoi(spec_env))) : 4u;
     std::vector<uint8_t> nmemo(n), rstat(n);
     std::vector<imsame_read_result> o1(n), o2(n);
     InitLaunch I = {qs.data(), read_from, n, res, cur_p.data(), cur_h.data(), nmemo.data(), rstat.data(), act.data()};
@@ -164,6 +168,8 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
         S.rstat = rstat.data();
         S.minraw = mr.data(); S.n_minraw = ymax + 1;
         S.max_rs = p->max_read_size; S.short_ylen = short_y;
+        S.spec = (st.rounds == 1) ? 1u : std::max<uint32_t>(1u, std::min<uint32_t>(spec_later, n / nact));
+        S.cbase = cbase.data(); S.ccnt = ccnt.data(); S.perr = perr.data();
         S.cread = cr.data(); S.csid = cs.data(); S.ncand = &nc[0];
         S.cread2 = cr2.data(); S.csid2 = cs2.data(); S.ncand2 = &nc[1];
         S.err = &err; S.nhits = &nhits;
@@ -177,7 +183,8 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
                    (uint32_t)paths_cap, &pused, &flags);
             st.n_nw += c.n;
             UpdLaunch U = {c.r, c.s, c.n, c.o, read_from, res, rstat.data(), memo.data(), nmemo.data(),
-                           nxt.data(), &nc[2], &cells, &nacc, dbs.data()};
+                           cbase.data(), ccnt.data(), perr.data(), nxt.data(), &nc[2], &cells, &nacc, &err,
+                           dbs.data()};
             for (uint32_t k = 0; k < c.n; ++k) { uint64_t ce = 0, ac = 0; update_one(U, k, ce, ac); cells += ce; nacc += ac; }
         }
         nact = nc[2];
