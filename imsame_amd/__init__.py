@@ -23,7 +23,7 @@ from . import abi
 from .abi import Params, Stats, RESULT_DTYPE, PARITY_FIELDS  # noqa: F401
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_DEV = os.path.join(HERE, "lib", "libimsame_dev.so")
+LIB_DEV = os.environ.get("IMSAME_LIB_DEV") or os.path.join(HERE, "lib", "libimsame_dev.so")
 LIB_HOST = os.path.join(HERE, "lib", "libimsame_host.so")
 CLI = os.path.join(HERE, "bin", "imsame")
 

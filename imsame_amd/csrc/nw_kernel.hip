@@ -443,8 +443,14 @@ __host__ static inline NwShape nw_shape(uint32_t ymax, uint32_t xcap) {
 __host__ static inline uint64_t nw_tb_words(const NwShape &s) { return (uint64_t)s.nstr * s.steps * 64; }
 
 #ifndef IMSAME_WAVE_EMU
+// Waves per SIMD the register budget is cut for (4 = 128 VGPRs: the sweep
+// loop fits without spills; the few spills land outside it).
+#ifndef NW_WAVES_PER_EU
+#define NW_WAVES_PER_EU 4
+#endif
 template <bool MULTI>
-__global__ __launch_bounds__(256) void nw_kernel(NwLaunch P) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MULTI ? 3 : NW_WAVES_PER_EU)))
+void nw_kernel(NwLaunch P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
     const uint32_t slot = blockIdx.x * (blockDim.x >> 6) + wib;

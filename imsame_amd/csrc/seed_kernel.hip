@@ -35,29 +35,82 @@ struct SeedLaunch {
 };
 #define SPEC_MAX 8
 
+// 16 bytes p[a .. a+15] as 4 dwords (a >= 0; buffers carry >= 20 B of tail
+// padding): 5 aligned dword loads + byte alignment.
+struct Bytes16 { uint32_t w[4]; };
+__device__ __forceinline__ Bytes16 load16(const uint8_t *__restrict__ p, int64_t a) {
+    const uint32_t *b = (const uint32_t *)(p + (a & ~(int64_t)3));
+    const uint32_t sh = (uint32_t)(a & 3);
+    uint32_t v[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) v[k] = b[k];
+    Bytes16 r;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r.w[k] = sh ? ((v[k] >> (8 * sh)) | (v[k + 1] << (32 - 8 * sh))) : v[k];
+    return r;
+}
+__device__ __forceinline__ bool byte_eq(const Bytes16 &a, const Bytes16 &b, int k) {
+    return ((a.w[k >> 2] ^ b.w[k >> 2]) & (0xFFu << (8 * (k & 3)))) == 0;
+}
+
 // alignmentFromQuickHits (alignmentFunctions.c:276-387): the raw score in the
 // reference's u64 wrap arithmetic (:373).  Loop bounds fold the reference's
-// per-step tests (:321-322, :344-345) into one limit per direction.
+// per-step tests (:321-322, :344-345) into one limit per direction.  The
+// byte-serial walk of the reference runs over 16-byte chunks (one round of
+// loads per chunk instead of per byte); the first chunk of each direction is
+// fetched before either walk starts.
 __device__ __forceinline__ uint64_t ungapped_raw(const uint8_t *__restrict__ db, const uint8_t *__restrict__ q,
                                                  int64_t pd0, int64_t pq0, int64_t xs, int64_t xe, int64_t ys,
                                                  int64_t ye, int64_t dbl, int64_t ql) {
     int64_t end_x = pd0 - 1, beg_x = end_x - IMSAME_FIXED_K + 1;
     int sc = IMSAME_FIXED_K * IMSAME_POINT, best_r = sc, best_l = sc;
-    uint64_t idents = IMSAME_FIXED_K;
+    uint32_t idents = IMSAME_FIXED_K;
+    const int64_t bx0 = pd0 - IMSAME_FIXED_K - 1, by0 = pq0 - IMSAME_FIXED_K - 1;
+    const bool lwin = bx0 >= 15 && by0 >= 15;            // left chunks need 15 bytes below the start
+    Bytes16 rd = load16(db, pd0), rq = load16(q, pq0);
+    Bytes16 ld = rd, lq = rq;
+    if (lwin) { ld = load16(db, bx0 - 15); lq = load16(q, by0 - 15); }
     const int64_t fx = min(min(dbl - 1, xe), pd0 + (min(ql - 1, ye) - pq0));
-    for (int64_t x = pd0, y = pq0; sc > 0 && x <= fx; ++x, ++y) {
-        if (db[x] == q[y]) { sc += IMSAME_POINT; ++idents; } else sc -= IMSAME_POINT;
-        if (best_r <= sc) { best_r = sc; end_x = x; }
+    for (int64_t x = pd0, y = pq0; sc > 0 && x <= fx;) {
+        const int64_t n = min((int64_t)16, fx - x + 1);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            if (k < n && sc > 0) {
+                const bool eq = byte_eq(rd, rq, k);
+                sc += eq ? IMSAME_POINT : -IMSAME_POINT;
+                idents += eq;
+                if (best_r <= sc) { best_r = sc; end_x = x + k; }
+            }
+        }
+        x += n; y += n;
+        if (sc > 0 && x <= fx) { rd = load16(db, x); rq = load16(q, y); }
     }
     sc = best_r;                        // left pass restarts from the right max, best_l stays 48 (:339)
-    const int64_t bx0 = pd0 - IMSAME_FIXED_K - 1, by0 = pq0 - IMSAME_FIXED_K - 1;
     const int64_t lx = max(max((int64_t)0, xs), bx0 - (by0 - max((int64_t)0, ys)));
-    for (int64_t x = bx0, y = by0; sc > 0 && x >= lx; --x, --y) {
+    int64_t x = bx0, y = by0;
+    if (lwin) {
+        // chunk = bytes x-15 .. x, walked downwards (byte 15 first)
+        while (sc > 0 && x >= lx && x >= 15 && y >= 15) {
+            const int64_t n = min((int64_t)16, x - lx + 1);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                if (k < n && sc > 0) {
+                    const bool eq = byte_eq(ld, lq, 15 - k);
+                    sc += eq ? IMSAME_POINT : -IMSAME_POINT;
+                    idents += eq;
+                    if (best_l <= sc) { best_l = sc; beg_x = x - k; }
+                }
+            }
+            x -= n; y -= n;
+            if (sc > 0 && x >= lx && x >= 15 && y >= 15) { ld = load16(db, x - 15); lq = load16(q, y - 15); }
+        }
+    }
+    for (; sc > 0 && x >= lx; --x, --y) {                 // the first 15 bytes of a buffer
         if (db[x] == q[y]) { sc += IMSAME_POINT; ++idents; } else sc -= IMSAME_POINT;
         if (best_l <= sc) { best_l = sc; beg_x = x; }
     }
     const uint64_t t_len = (uint64_t)(end_x - beg_x);
-    return idents * IMSAME_POINT - (t_len - idents) * IMSAME_POINT;
+    return (uint64_t)idents * IMSAME_POINT - (t_len - idents) * IMSAME_POINT;
 }
 
 __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint64_t &hits) {

@@ -1,0 +1,112 @@
+// valu_rate.hip -- measured VALU issue cost of the instruction forms the NW
+// sweep (nw_kernel.hip) is built from, on gfx950.  DESIGN.md prices the
+// sweep with these numbers.
+//
+//   hipcc --offload-arch=gfx950 -O3 -o valu_rate valu_rate.hip && ./valu_rate
+//
+// Each kernel runs ITER iterations of 8 independent chains of one
+// instruction form; waves per SIMD is set by the grid (4-wave blocks, one
+// per SIMD).  Prints SIMD cycles per wave-instruction (clock from
+// s_memtime / s_memrealtime), so 2.0 = the 64-lane/2-cycle issue peak.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdint.h>
+
+#define ITER 8192
+#define CHK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s\n", hipGetErrorString(e)); return 1; } } while (0)
+
+#define K8(stmt) _Pragma("unroll") for (int i = 0; i < 8; ++i) { stmt; }
+
+template <int KIND>
+__global__ __launch_bounds__(256) void k_rate(int *out, int seed, unsigned long long *clk) {
+    int a[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = seed + threadIdx.x * (i + 1);
+    const int b = seed * 3 + threadIdx.x, c = seed ^ 0x55;
+    unsigned long long m = 0x5555aaaa3333ccccull ^ (unsigned long long)seed;
+    unsigned long long t0 = 0, r0 = 0;
+    if (threadIdx.x == 0 && blockIdx.x == 0) { t0 = __builtin_amdgcn_s_memtime(); r0 = __builtin_amdgcn_s_memrealtime(); }
+    for (int it = 0; it < ITER; ++it) {
+        if (KIND == 0) K8(asm volatile("v_add_u32_e32 %0, %0, %1" : "+v"(a[i]) : "v"(b)))
+        if (KIND == 1) K8(asm volatile("v_add_u32_e64 %0, %0, %1" : "+v"(a[i]) : "v"(b)))
+        if (KIND == 2) K8(asm volatile("v_max3_i32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(b), "v"(c)))
+        if (KIND == 3) K8(asm volatile("v_max_i32_e32 %0, %0, %1" : "+v"(a[i]) : "v"(b)))
+        if (KIND == 4) K8(asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(a[i]) : "v"(b), "s"(m)))
+        if (KIND == 5) K8(asm volatile("v_cndmask_b32_e64 %0, 0, 4, %1" : "=v"(a[i]) : "s"(m ^ (unsigned)i)))
+        if (KIND == 6) K8(asm volatile("v_cmp_gt_i32_e64 %0, %1, %2" : "=s"(m) : "v"(a[i]), "v"(b)))
+        if (KIND == 7) K8(asm volatile("v_cmp_gt_i32_e32 vcc, %0, %1" : : "v"(a[i]), "v"(b) : "vcc"))
+        if (KIND == 8) K8(asm volatile("s_mov_b64 vcc, %1\n\tv_cndmask_b32_e32 %0, %0, %2, vcc" : "+v"(a[i]) : "s"(m), "v"(b) : "vcc"))
+        if (KIND == 9) K8(asm volatile("s_mov_b64 vcc, %1\n\tv_addc_co_u32_e32 %0, vcc, %0, %0, vcc" : "+v"(a[i]) : "s"(m) : "vcc"))
+        if (KIND == 10) K8(asm volatile("v_or3_b32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(b), "v"(c)))
+        if (KIND == 11) K8(asm volatile("v_lshl_or_b32 %0, %0, 1, %1" : "+v"(a[i]) : "v"(b)))
+        if (KIND == 12) K8(asm volatile("v_mov_b32_dpp %0, %1 wave_shr:1 row_mask:0xf bank_mask:0xf" : "=v"(a[i]) : "v"(a[(i + 4) & 7])))
+        if (KIND == 13) K8(asm volatile("v_sub_u32_e32 %0, %1, %0\n\tv_max_i32_e32 %0, %0, %1" : "+v"(a[i]) : "v"(b)))
+        if (KIND == 14) K8(asm volatile("v_pk_max_i16 %0, %0, %1" : "+v"(a[i]) : "v"(b)))
+        if (KIND == 15) K8(asm volatile("v_cmp_eq_u32_sdwa %0, %1, %2 src0_sel:BYTE_1 src1_sel:DWORD" : "=s"(m) : "v"(a[i]), "v"(b)))
+        if (KIND == 16) K8(asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(b), "v"(c)))
+        if (KIND == 17) K8(asm volatile("v_mad_u32_u24 %0, %0, %1, %2" : "+v"(a[i]) : "v"(b), "v"(c)))
+    }
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        clk[0] = __builtin_amdgcn_s_memtime() - t0;
+        clk[1] = __builtin_amdgcn_s_memrealtime() - r0;
+    }
+    int s = (int)m;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += a[i];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+template <int KIND>
+static int run(const char *name, int ninstr, int *d_out, unsigned long long *d_clk, int cus) {
+    printf("%-40s", name);
+    for (int wps = 1; wps <= 8; wps *= 2) {              // waves per SIMD
+        const int blocks = cus * wps;
+        hipEvent_t e0, e1;
+        CHK(hipEventCreate(&e0)); CHK(hipEventCreate(&e1));
+        hipLaunchKernelGGL(k_rate<KIND>, dim3(blocks), dim3(256), 0, 0, d_out, 7, d_clk);
+        CHK(hipEventRecord(e0));
+        hipLaunchKernelGGL(k_rate<KIND>, dim3(blocks), dim3(256), 0, 0, d_out, 7, d_clk);
+        CHK(hipEventRecord(e1));
+        CHK(hipEventSynchronize(e1));
+        float ms = 0;
+        CHK(hipEventElapsedTime(&ms, e0, e1));
+        unsigned long long clk[2];
+        CHK(hipMemcpy(clk, d_clk, sizeof clk, hipMemcpyDeviceToHost));
+        const double ghz = (double)clk[0] / ((double)clk[1] / 100e6) / 1e9;
+        const double winstr = (double)wps * ITER * 8 * ninstr;                // per SIMD
+        printf("  w%d %5.2f", wps, ms * 1e-3 * ghz * 1e9 / winstr);
+        CHK(hipEventDestroy(e0)); CHK(hipEventDestroy(e1));
+    }
+    printf("   cyc/instr/SIMD\n");
+    return 0;
+}
+
+int main() {
+    hipDeviceProp_t p;
+    CHK(hipGetDeviceProperties(&p, 0));
+    const int cus = p.multiProcessorCount;
+    printf("%s  CUs %d\n", p.gcnArchName, cus);
+    int *d_out; unsigned long long *d_clk;
+    CHK(hipMalloc(&d_out, (size_t)cus * 8 * 256 * sizeof(int)));
+    CHK(hipMalloc(&d_clk, 16));
+#define R(K, N, S) if (run<K>(S, N, d_out, d_clk, cus)) return 1;
+    R(0, 1, "v_add_u32_e32")
+    R(1, 1, "v_add_u32_e64")
+    R(2, 1, "v_max3_i32")
+    R(3, 1, "v_max_i32_e32")
+    R(4, 1, "v_cndmask_b32_e64 (sgpr mask)")
+    R(5, 1, "v_cndmask_b32_e64 0,4 (const)")
+    R(6, 1, "v_cmp_gt_i32_e64 (-> sgpr)")
+    R(7, 1, "v_cmp_gt_i32_e32 (-> vcc)")
+    R(8, 1, "s_mov vcc + v_cndmask_b32_e32 [valu only]")
+    R(9, 1, "s_mov vcc + v_addc_co_u32_e32 [valu only]")
+    R(10, 1, "v_or3_b32")
+    R(11, 1, "v_lshl_or_b32")
+    R(12, 1, "v_mov_b32_dpp wave_shr:1")
+    R(13, 2, "v_sub_u32_e32 + v_max_i32_e32")
+    R(14, 1, "v_pk_max_i16")
+    R(15, 1, "v_cmp_eq_u32_sdwa")
+    R(16, 1, "v_add3_u32")
+    R(17, 1, "v_mad_u32_u24")
+    return 0;
+}

@@ -126,6 +126,12 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
                          imsame_stats *stats) {
     std::vector<uint64_t> dbs(db_start, db_start + n_db), qs(q_start, q_start + n_q);
     dbs.push_back(db_len); qs.push_back(q_len);
+    // aligned copies with the 64-byte tail padding the device buffers carry (chunked loads)
+    std::vector<uint32_t> dbpad(db_len / 4 + 17, 0), qpad(q_len / 4 + 17, 0);
+    if (db_len) memcpy(dbpad.data(), db, db_len);
+    if (q_len) memcpy(qpad.data(), q, q_len);
+    db = (const uint8_t *)dbpad.data();
+    q = (const uint8_t *)qpad.data();
     std::vector<uint32_t> off;
     std::vector<uint2> ent;
     build_csr(db, db_len, dbs.data(), n_db, db_brk, off, ent);
@@ -198,6 +204,22 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
     if ((flags & 1) && !ret) ret = IMSAME_E_PATHS;
     if (stats) *stats = st;
     return ret;
+}
+
+// seed_kernel.hip:ungapped_raw for one hit (pd0 = DB position after the
+// seed, pq0 = query position after it), bounds as seed_one derives them
+extern "C" uint64_t emu_ungapped(const uint8_t *db, uint64_t db_len, const uint64_t *db_start, uint64_t n_db,
+                                 const uint8_t *q, uint64_t q_len, const uint64_t *q_start, uint64_t n_q,
+                                 uint64_t pd0, uint64_t pq0, uint64_t read, uint64_t sid) {
+    std::vector<uint32_t> dbpad(db_len / 4 + 17, 0), qpad(q_len / 4 + 17, 0);
+    if (db_len) memcpy(dbpad.data(), db, db_len);
+    if (q_len) memcpy(qpad.data(), q, q_len);
+    const int64_t xs = (int64_t)db_start[sid];
+    const int64_t xe = (sid == n_db - 1) ? (int64_t)db_len : (int64_t)db_start[sid + 1] - 1;
+    const int64_t ys = (int64_t)q_start[read];
+    const int64_t ye = (read == n_q - 1) ? (int64_t)q_len : (int64_t)q_start[read + 1] - 1;
+    return ungapped_raw((const uint8_t *)dbpad.data(), (const uint8_t *)qpad.data(), (int64_t)pd0, (int64_t)pq0,
+                        xs, xe, ys, ye, (int64_t)db_len, (int64_t)q_len);
 }
 
 // table entry points for tests/test_host.py

@@ -96,6 +96,56 @@ def test_emulated_nw_kernel_matches_reference_golden(emu, oracle):
                 assert int(res[k][f]) == r[f], (f, ig, eg, len(r["X"]), len(r["Y"]))
 
 
+def _emu_ungapped(emu, db, dbs, q, qs, pd0, pq0, read, sid):
+    f = emu.lib.emu_ungapped
+    f.restype = C.c_uint64
+    u8, u64 = C.POINTER(C.c_uint8), C.POINTER(C.c_uint64)
+    f.argtypes = [u8, C.c_uint64, u64, C.c_uint64, u8, C.c_uint64, u64, C.c_uint64] + [C.c_uint64] * 4
+    return f(db.ctypes.data_as(u8), len(db), dbs.ctypes.data_as(u64), len(dbs), q.ctypes.data_as(u8), len(q),
+             qs.ctypes.data_as(u64), len(qs), pd0, pq0, read, sid)
+
+
+def test_emulated_ungapped_matches_reference_golden(emu, oracle):
+    """seed_kernel.hip:ungapped_raw (16-byte chunked walk) == the reference's
+    byte walk on every golden hit, plus random hits incl. buffer starts."""
+    rows, cases = G.ungapped_rows()
+    arrs = {c: (G.seqs_arrays(v["db"]), G.seqs_arrays(v["reads"])) for c, v in cases.items()}
+    for r in rows:
+        (db, dbs), (q, qs) = arrs[r["case"]]
+        exp = oracle.ungapped(db, dbs, q, qs, r["pos_db"], r["pos_q"], r["read"], r["dbseq"]).raw
+        got = _emu_ungapped(emu, db, dbs, q, qs, r["pos_db"], r["pos_q"], r["read"], r["dbseq"])
+        assert got == exp, r
+    from tests import synth
+    rng = np.random.default_rng(5)
+    ref, rst = synth.make_reference_arr(60_000, 700, seed=9)
+    q, qs = synth.make_reads_arr(ref, 300, 120, seed=10)
+    n = 0
+    for _ in range(3000):
+        sid = int(rng.integers(len(rst)))
+        rd = int(rng.integers(len(qs)))
+        xs, xe = int(rst[sid]), (int(rst[sid + 1]) if sid + 1 < len(rst) else len(ref))
+        ys, ye = int(qs[rd]), (int(qs[rd + 1]) if rd + 1 < len(qs) else len(q))
+        if xe - xs < 13 or ye - ys < 13:
+            continue
+        if rng.random() < 0.5:      # true-hit diagonal: the read's own origin, long extensions
+            pq0 = int(rng.integers(ys + 12, ye + 1))
+            pd0 = int(rng.integers(xs + 12, xe + 1))
+        else:                       # buffer starts and record edges
+            pq0 = ys + 12 + int(rng.integers(0, 3))
+            pd0 = xs + 12 + int(rng.integers(0, 20))
+        exp = oracle.ungapped(ref, rst, q, qs, pd0, pq0, rd, sid).raw
+        assert _emu_ungapped(emu, ref, rst, q, qs, pd0, pq0, rd, sid) == exp, (pd0, pq0, rd, sid)
+        n += 1
+    assert n > 2000
+    # exact matches far past one 16-byte chunk in both directions
+    q2 = ref[1000:1400].copy()
+    qs2 = np.array([0], dtype=np.uint64)
+    sid = int(np.searchsorted(rst, 1000, side="right") - 1)
+    for off in (12, 13, 40, 200, 399, 400):
+        exp = oracle.ungapped(ref, rst, q2, qs2, 1000 + off, off, 0, sid).raw
+        assert _emu_ungapped(emu, ref, rst, q2, qs2, 1000 + off, off, 0, sid) == exp
+
+
 @pytest.mark.parametrize("name", ["borrowed", "edges", "reads_vs_reads", "toolong"])
 def test_emulated_pipeline_matches_oracle(emu, oracle, name):
     """Seed scan + rounds + NW (kernel source, emulated) vs the oracle."""
