@@ -26,6 +26,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DEV = os.environ.get("IMSAME_LIB_DEV") or os.path.join(HERE, "lib", "libimsame_dev.so")
 LIB_HOST = os.path.join(HERE, "lib", "libimsame_host.so")
 CLI = os.path.join(HERE, "bin", "imsame")
+FLAG_NW32 = 1          # imsame_params.flags: force the int32 NW kernel (include/imsame_dev.h)
 
 _lib = None
 _host = None

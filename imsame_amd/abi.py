@@ -33,7 +33,7 @@ class Params(C.Structure):
         ("egap", C.c_int64),
         ("max_read_size", C.c_uint64),
         ("want_paths", C.c_uint32),
-        ("reserved", C.c_uint32),
+        ("flags", C.c_uint32),
     ]
 
 

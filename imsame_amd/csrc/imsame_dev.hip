@@ -24,6 +24,7 @@
 
 #include "tables.h"
 #include "nw_kernel.hip"
+#include "nw16_kernel.hip"
 #include "seed_kernel.hip"
 
 
@@ -392,21 +393,26 @@ static int build_tables(imsame_ctx *c, const imsame_params *p, uint32_t ymax, ui
     return 0;
 }
 
-struct NwPlan { int G, GPW, xcap, xstride, steps, nstr; size_t lds; unsigned blocks; };
+struct NwPlan { int G, GPW, xcap, xstride, steps, nstr; bool pk; size_t lds; unsigned blocks; uint64_t tb_dw; };
 
-static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, NwPlan *pl) {
+// pk: the packed-pair int16 kernel (nw16_kernel.hip) when the launch fits it
+static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, const imsame_params *p, NwPlan *pl) {
     const int wpb = 4;
-    const NwShape sh = nw_shape(ymax, xcap);
+    pl->pk = !(p->flags & IMSAME_FLAG_NW32) && nw16_fits(p->igap, p->egap, xcap, ymax);
+    const NwShape sh = pl->pk ? nw16_shape(ymax, xcap) : nw_shape(ymax, xcap);
     pl->G = sh.G; pl->GPW = sh.GPW; pl->nstr = sh.nstr; pl->xcap = sh.xcap; pl->xstride = sh.xstride;
     pl->steps = sh.steps;
-    pl->lds = (size_t)wpb * nw_wave_lds(pl->GPW, pl->xstride);
+    pl->tb_dw = pl->pk ? nw16_tb_words(sh) : nw_tb_words(sh);
+    pl->lds = (size_t)wpb * (pl->pk ? nw16_wave_lds(pl->GPW, pl->xstride) : nw_wave_lds(pl->GPW, pl->xstride));
     int per_cu = 0;
-    hipError_t oe = (pl->nstr > 1)
-        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw_kernel<true>, wpb * 64, pl->lds)
-        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw_kernel<false>, wpb * 64, pl->lds);
+    hipError_t oe = pl->pk ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw16_kernel, wpb * 64, pl->lds)
+                  : (pl->nstr > 1)
+                      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw_kernel<true>, wpb * 64, pl->lds)
+                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw_kernel<false>, wpb * 64, pl->lds);
     if (oe != hipSuccess || per_cu < 1) per_cu = 1;
     per_cu = std::min(per_cu, 8);
-    const uint64_t waves_needed = (ncand + pl->GPW - 1) / pl->GPW;
+    const uint32_t cpw = pl->pk ? 2 * pl->GPW : pl->GPW;            // candidates per wave pull
+    const uint64_t waves_needed = (ncand + cpw - 1) / cpw;
     pl->blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)c->ncu * per_cu, (waves_needed + wpb - 1) / wpb));
     return 0;
 }
@@ -417,7 +423,7 @@ static int launch_nw(imsame_ctx *c, const NwPlan &pl, const uint32_t *cread, con
                      const uint64_t *qs, uint32_t paths_cap, double *ms) {
     hipStream_t s = c->stream;
     const unsigned slots = pl.blocks * 4;
-    const uint64_t tb_dw = (uint64_t)pl.nstr * pl.steps * 64;      // one dword per lane per step
+    const uint64_t tb_dw = pl.tb_dw;
     if (c->tb.ensure(slots * tb_dw * 4) || c->bnd.ensure((uint64_t)slots * 3 * pl.xcap * 4 + 64)) return IMSAME_E_OOM;
     NwLaunch P;
     memset(&P, 0, sizeof P);
@@ -437,8 +443,9 @@ static int launch_nw(imsame_ctx *c, const NwPlan &pl, const uint32_t *cread, con
     P.flags = (uint32_t *)(ctr + C_FLAGS);
     HIPCHK(hipMemsetAsync(work, 0, 4, s));
     HIPCHK(hipEventRecord(c->ev0, s));
-    if (pl.nstr > 1) nw_kernel<true><<<pl.blocks, 256, pl.lds, s>>>(P);
-    else             nw_kernel<false><<<pl.blocks, 256, pl.lds, s>>>(P);
+    if (pl.pk)            nw16_kernel<<<pl.blocks, 256, pl.lds, s>>>(P);
+    else if (pl.nstr > 1) nw_kernel<true><<<pl.blocks, 256, pl.lds, s>>>(P);
+    else                  nw_kernel<false><<<pl.blocks, 256, pl.lds, s>>>(P);
     HIPCHK(hipEventRecord(c->ev1, s));
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventSynchronize(c->ev1));
@@ -549,7 +556,7 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
         for (int k = 0; k < 2; ++k) {
             if (!cls[k].n) continue;
             NwPlan pl;
-            plan_nw(c, cls[k].ylim, xcap, cls[k].n, &pl);
+            plan_nw(c, cls[k].ylim, xcap, cls[k].n, p, &pl);
             double ms = 0;
             rc = launch_nw(c, pl, cls[k].cr, cls[k].cs, cls[k].n, cls[k].o, p->igap, p->egap, p, ymax, xcap,
                            (uint32_t *)(ctr + cls[k].work), c->db.as<uint8_t>(), c->db_start.as<uint64_t>(),
@@ -653,7 +660,7 @@ extern "C" int imsame_dev_nw_pairs(imsame_ctx *c, const uint8_t *xs, const uint6
     uint64_t *ctr = c->ctr.as<uint64_t>();
     HIPCHK(hipMemsetAsync(ctr, 0, C_NSLOTS * 8, s));
     NwPlan pl;
-    plan_nw(c, ymax, xmax, (uint32_t)npairs, &pl);
+    plan_nw(c, ymax, xmax, (uint32_t)npairs, p, &pl);
     double ms = 0;
     rc = launch_nw(c, pl, dc.as<uint32_t>(), dc.as<uint32_t>(), (uint32_t)npairs, dout.as<imsame_read_result>(),
                    p->igap, p->egap, p, ymax, xmax, (uint32_t *)(ctr + C_WORK), dx.as<uint8_t>(), dxs.as<uint64_t>(),

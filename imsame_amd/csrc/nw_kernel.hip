@@ -210,14 +210,23 @@ __device__ __forceinline__ void nw_sweep(const NwLaunch &P, const NwCand &cd, ui
 
 // Walk the traceback of group g from (px,py) (backtrackingNW, :493-560).
 // Returns path statistics; emits runs into `path` when emit (lane gl == 0).
+// TB gives nib(i, j) -- the cell's nibble in the layout above -- and
+// match(i, j) = X[i] == Y[j]; one accessor per traceback layout.
 struct WalkOut { int len, idn, ig, eg, cx, cy, nent; bool bad; };
 
-__device__ WalkOut nw_walk(const uint32_t *tb, const NwCand &cd, int px, int py, bool walking, int g, int gl,
-                           int G, int steps, uint32_t *path, bool emit) {
+struct TbAcc32 {                       // this file's layout: one candidate per group
+    const uint32_t *tb; const NwCand *cd; int g, G, steps;
+    __device__ uint32_t nib(int i, int j) const { return tb_cell(tb, i, j, g, G, steps); }
+    __device__ bool match(int i, int j) const { return cd->X[i] == cd->Y[j]; }
+};
+
+template <class TB>
+__device__ WalkOut nw_walk(const TB &tbk, int xlen, int ylen, int px, int py, bool walking, int g, int gl,
+                           int G, uint32_t *path, bool emit) {
     WalkOut w = {0, 0, 0, 0, px, py, 0, false};
     const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1);
     int run = 0;                       // pending diagonal run (emit) / in-run flag
-    int guard = 4 * (cd.xlen + cd.ylen) + 8;
+    int guard = 4 * (xlen + ylen) + 8;
     walking = walking && px > 0 && py > 0;
     while (wv_any(walking)) {
         // G diagonal cells at once; the first non-diagonal one stops the run
@@ -226,8 +235,8 @@ __device__ WalkOut nw_walk(const uint32_t *tb, const NwCand &cd, int px, int py,
         uint32_t nib = 0xFu;
         bool match = false;
         if (valid) {
-            nib = tb_cell(tb, cx, cy, g, G, steps);
-            match = cd.X[cx] == cd.Y[cy];
+            nib = tbk.nib(cx, cy);
+            match = tbk.match(cx, cy);
         }
         const bool stop = !valid || (nib & 3u) != 0;
         const unsigned long long bs = wv_ballot(stop), bm = wv_ballot(valid && match);
@@ -257,7 +266,7 @@ __device__ WalkOut nw_walk(const uint32_t *tb, const NwCand &cd, int px, int py,
             while (wv_any(searching)) {
                 const int r = base - gl;
                 const bool ok = searching && r >= 1;
-                const bool u = ok && ((tb_cell(tb, r, py, g, G, steps) >> 2) & 1u);
+                const bool u = ok && ((tbk.nib(r, py) >> 2) & 1u);
                 const unsigned long long gb = (wv_ballot(u) >> (g * G)) & gmask;
                 if (searching) {
                     if (gb) { src = base - __builtin_ctzll(gb) - 2; searching = false; }
@@ -273,7 +282,7 @@ __device__ WalkOut nw_walk(const uint32_t *tb, const NwCand &cd, int px, int py,
             while (wv_any(searching)) {
                 const int c = base - gl;
                 const bool ok = searching && c >= 1;
-                const bool l = ok && ((tb_cell(tb, px, c, g, G, steps) >> 3) & 1u);
+                const bool l = ok && ((tbk.nib(px, c) >> 3) & 1u);
                 const unsigned long long gb = (wv_ballot(l) >> (g * G)) & gmask;
                 if (searching) {
                     if (gb) { lsrc = base - __builtin_ctzll(gb) - 1; searching = false; }
@@ -305,6 +314,47 @@ __device__ WalkOut nw_walk(const uint32_t *tb, const NwCand &cd, int px, int py,
     if (emit && gl == 0 && run && !w.bad) path[w.nent - 1] = (IMSAME_MOVE_DIAG << 30) | (uint32_t)run;
     w.cx = px; w.cy = py;
     return w;
+}
+
+// Backtrack + acceptance + result of one candidate per group (all lanes of
+// the wave call it; lanes with !cvalid only take part in the wave votes).
+template <class TB>
+__device__ void nw_finish(const NwLaunch &P, const TB &acc32, const int xlen, const int ylen, const bool cvalid,
+                          const int gg, const int gl, const int G, const int bscore, const int bx, const int by,
+                          const uint32_t c, const uint32_t sid) {
+        WalkOut w = nw_walk(acc32, xlen, ylen, bx, by, cvalid, gg, gl, G, nullptr, false);
+        bool acc = false;
+        if (cvalid && !w.bad) {
+            acc = (uint32_t)ylen < P.n_minlen && (uint32_t)w.len >= P.minlen[ylen] &&
+                  (uint32_t)w.len < P.n_minident && (uint32_t)w.idn >= P.minident[w.len];
+        }
+        if (cvalid && w.bad && gl == 0) wv_atomic_or(P.flags, 2u);
+        uint32_t poff = 0, plen = 0;
+        const bool want = cvalid && acc && P.want_paths;
+        if (wv_any(want)) {
+            uint32_t off = 0;
+            if (want && gl == 0) {
+                off = wv_atomic_add(P.paths_used, (uint32_t)w.nent);
+                if (off + (uint32_t)w.nent > P.paths_cap) { wv_atomic_or(P.flags, 1u); off = 0xFFFFFFFFu; }
+            }
+            off = (uint32_t)wv_shfl((int)off, gg * G);
+            const bool ok = want && off != 0xFFFFFFFFu;
+            nw_walk(acc32, xlen, ylen, bx, by, ok, gg, gl, G, ok ? P.paths + off : nullptr, true);
+            if (ok) { poff = off; plen = (uint32_t)w.nent; }
+        }
+        if (cvalid && gl == 0) {
+            const int M = 2 * max(xlen, ylen);
+            const int tail = w.cx + w.cy;                    // one of them is 0
+            imsame_read_result r;
+            r.db_seq = sid; r.score = bscore; r.bx = (uint32_t)bx; r.by = (uint32_t)by;
+            r.length = (uint32_t)w.len; r.identities = (uint32_t)w.idn;
+            r.igaps = (uint32_t)w.ig; r.egaps = (uint32_t)w.eg;
+            r.head_x = (uint32_t)(M - ((xlen - 1 - bx) + w.len + tail));
+            r.head_y = (uint32_t)(M - ((ylen - 1 - by) + w.len + tail));
+            r.ylen = (uint32_t)ylen; r.status = acc ? 1u : 2u;
+            r.path_off = poff; r.path_len = plen;
+            P.out[c] = r;
+        }
 }
 
 // One wave's share of a launch: pulls groups of GPW candidates from the work
@@ -383,39 +433,8 @@ __device__ void nw_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const u
         else          { bscore = bC; bx = bCi; by = cd.ylen - 1; }
         wv_lds_sync();
 
-        WalkOut w = nw_walk(tbw, cd, bx, by, cvalid, gg, gl, G, P.steps, nullptr, false);
-        bool acc = false;
-        if (cvalid && !w.bad) {
-            acc = (uint32_t)cd.ylen < P.n_minlen && (uint32_t)w.len >= P.minlen[cd.ylen] &&
-                  (uint32_t)w.len < P.n_minident && (uint32_t)w.idn >= P.minident[w.len];
-        }
-        if (cvalid && w.bad && gl == 0) wv_atomic_or(P.flags, 2u);
-        uint32_t poff = 0, plen = 0;
-        const bool want = cvalid && acc && P.want_paths;
-        if (wv_any(want)) {
-            uint32_t off = 0;
-            if (want && gl == 0) {
-                off = wv_atomic_add(P.paths_used, (uint32_t)w.nent);
-                if (off + (uint32_t)w.nent > P.paths_cap) { wv_atomic_or(P.flags, 1u); off = 0xFFFFFFFFu; }
-            }
-            off = (uint32_t)wv_shfl((int)off, gg * G);
-            const bool ok = want && off != 0xFFFFFFFFu;
-            nw_walk(tbw, cd, bx, by, ok, gg, gl, G, P.steps, ok ? P.paths + off : nullptr, true);
-            if (ok) { poff = off; plen = (uint32_t)w.nent; }
-        }
-        if (cvalid && gl == 0) {
-            const int M = 2 * max(cd.xlen, cd.ylen);
-            const int tail = w.cx + w.cy;                    // one of them is 0
-            imsame_read_result r;
-            r.db_seq = sid; r.score = bscore; r.bx = (uint32_t)bx; r.by = (uint32_t)by;
-            r.length = (uint32_t)w.len; r.identities = (uint32_t)w.idn;
-            r.igaps = (uint32_t)w.ig; r.egaps = (uint32_t)w.eg;
-            r.head_x = (uint32_t)(M - ((cd.xlen - 1 - bx) + w.len + tail));
-            r.head_y = (uint32_t)(M - ((cd.ylen - 1 - by) + w.len + tail));
-            r.ylen = (uint32_t)cd.ylen; r.status = acc ? 1u : 2u;
-            r.path_off = poff; r.path_len = plen;
-            P.out[c] = r;
-        }
+        const TbAcc32 acc32 = {tbw, &cd, gg, G, P.steps};
+        nw_finish(P, acc32, cd.xlen, cd.ylen, cvalid, gg, gl, G, bscore, bx, by, c, sid);
         wv_lds_sync();
     }
 }

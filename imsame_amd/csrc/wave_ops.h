@@ -39,6 +39,33 @@ WV_DEVICE void wv_mem_sync() {
     __threadfence_block();
 }
 
+// Packed pairs: two int16 lanes in one 32-bit register (bits 0-15 = candidate
+// A, bits 16-31 = candidate B).  The v_pk_*_i16 forms issue at the same cost
+// as one v_max_i32 (scripts/micro/valu_rate.hip), so each does two cells.
+typedef short wv_s2 __attribute__((ext_vector_type(2)));
+WV_DEVICE wv_s2 pk_v(uint32_t a) { return __builtin_bit_cast(wv_s2, a); }
+WV_DEVICE uint32_t pk_u(wv_s2 a) { return __builtin_bit_cast(uint32_t, a); }
+WV_DEVICE uint32_t pk_add(uint32_t a, uint32_t b) { return pk_u(pk_v(a) + pk_v(b)); }          // v_pk_add_u16
+WV_DEVICE uint32_t pk_sub(uint32_t a, uint32_t b) { return pk_u(pk_v(a) - pk_v(b)); }          // v_pk_sub_u16
+WV_DEVICE uint32_t pk_max(uint32_t a, uint32_t b) { return pk_u(__builtin_elementwise_max(pk_v(a), pk_v(b))); }
+// 0xFFFF in each half that is negative.  Opaque on purpose: seen as a sign
+// splat, LLVM turns the bfi/and_or users into per-half v_cmp + v_cndmask.
+WV_DEVICE uint32_t pk_neg_mask(uint32_t a) {
+    uint32_t r;
+    // op_sel_hi:[0,1]: the high lane takes its shift from the constant's LOW
+    // half too (by default it would read bits 16-31 of 15, i.e. 0)
+    asm("v_pk_ashrrev_i16 %0, 15, %1 op_sel_hi:[0,1]" : "=v"(r) : "v"(a));
+    return r;
+}
+// (m & c) | w in one v_and_or_b32 (left to itself LLVM emits and + or3)
+WV_DEVICE uint32_t wv_and_or(uint32_t m, uint32_t c, uint32_t w) {
+    uint32_t r;
+    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(c), "v"(w));
+    return r;
+}
+// byte permute of the 8 bytes {hi:lo}: selector byte k picks byte sel_k (0-3 of lo, 4-7 of hi)
+WV_DEVICE uint32_t wv_perm(uint32_t hi, uint32_t lo, uint32_t sel) { return __builtin_amdgcn_perm(hi, lo, sel); }
+
 #else  // ---------------------------------------------------------- CPU emu
 #include <stdint.h>
 #include <string.h>
@@ -104,4 +131,28 @@ inline void wv_atomic_min64(unsigned long long *p, unsigned long long v) {
 }
 inline void wv_lds_sync() { wvemu::sync(); }
 inline void wv_mem_sync() { wvemu::sync(); }
+
+inline uint32_t pk_map(uint32_t a, uint32_t b, int (*f)(int, int)) {
+    const int lo = f((int16_t)(a & 0xFFFF), (int16_t)(b & 0xFFFF)), hi = f((int16_t)(a >> 16), (int16_t)(b >> 16));
+    return ((uint32_t)(uint16_t)lo) | ((uint32_t)(uint16_t)hi << 16);
+}
+inline uint32_t pk_add(uint32_t a, uint32_t b) { return pk_map(a, b, [](int x, int y) { return x + y; }); }
+inline uint32_t pk_sub(uint32_t a, uint32_t b) { return pk_map(a, b, [](int x, int y) { return x - y; }); }
+inline uint32_t pk_max(uint32_t a, uint32_t b) { return pk_map(a, b, [](int x, int y) { return x > y ? x : y; }); }
+inline uint32_t pk_neg_mask(uint32_t a) { return pk_map(a, 0, [](int x, int) { return x < 0 ? -1 : 0; }); }
+inline uint32_t wv_and_or(uint32_t m, uint32_t c, uint32_t w) { return (m & c) | w; }
+inline uint32_t wv_perm(uint32_t hi, uint32_t lo, uint32_t sel) {
+    const uint64_t v = ((uint64_t)hi << 32) | lo;
+    uint32_t r = 0;
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t s = (sel >> (8 * k)) & 0xFF;
+        uint32_t b;
+        if (s < 8) b = (uint32_t)(v >> (8 * s)) & 0xFF;
+        else if (s == 12) b = 0;
+        else if (s > 12) b = 0xFF;
+        else b = ((v >> (s == 8 ? 15 : s == 9 ? 31 : s == 10 ? 47 : 63)) & 1) ? 0xFF : 0;
+        r |= b << (8 * k);
+    }
+    return r;
+}
 #endif

@@ -55,8 +55,12 @@ typedef struct imsame_params {
     int64_t     egap;
     uint64_t    max_read_size;  /* IMSAME_MAX_READ_SIZE unless raised (C5)  */
     uint32_t    want_paths;     /* 1: return alignment paths of accepted reads */
-    uint32_t    reserved;
+    uint32_t    flags;          /* IMSAME_FLAG_* (0 = defaults)                 */
 } imsame_params;
+
+/* flags: force the int32 NW kernel even where the packed int16 one fits
+ * (results are identical; used by the tests to cover both kernels) */
+#define IMSAME_FLAG_NW32 1u
 
 /* Fill the reference defaults: min_e = 1/powl(10,20), cov = id = 0.5,
  * igap = -5, egap = -2, max_read_size = 3000, want_paths = 0. */

@@ -1,0 +1,21 @@
+#!/usr/bin/env bash
+# One GPU-box pass: VALU micro, GPU test suite, smoke, bench + kernel-trace stats.
+#   gpurun -- bash scripts/gpu_round.sh <tag> [micro] [tests] [bench] [prof]
+set -euo pipefail
+TAG=${1:-x}; shift || true
+STEPS=${*:-"micro tests bench prof"}
+cd "${GRAFT_REPO_ROOT:-.}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+for s in $STEPS; do
+  case $s in
+    micro) timeout -k 10 120 ./scripts/micro/valu_rate > gpurun_out/micro_${TAG}.txt 2>&1 ;;
+    tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_${TAG}.log 2>&1 ;;
+    smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_${TAG}.log 2>&1 ;;
+    bench) timeout -k 10 600 python -u bench.py > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err ;;
+    benchq) timeout -k 10 300 python -u bench.py --cpu-sample 0 > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err ;;
+    prof) timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d gpurun_out/prof_${TAG} -o kt --output-format csv \
+            -- python3 bench.py --steps 2 --warmup 1 --cpu-sample 0 > gpurun_out/bench_prof_${TAG}.json 2> gpurun_out/bench_prof_${TAG}.err ;;
+  esac
+  echo "$s ok" >> gpurun_out/steps_${TAG}.txt
+done

@@ -45,6 +45,17 @@ __global__ __launch_bounds__(256) void k_rate(int *out, int seed, unsigned long 
         if (KIND == 15) K8(asm volatile("v_cmp_eq_u32_sdwa %0, %1, %2 src0_sel:BYTE_1 src1_sel:DWORD" : "=s"(m) : "v"(a[i]), "v"(b)))
         if (KIND == 16) K8(asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(b), "v"(c)))
         if (KIND == 17) K8(asm volatile("v_mad_u32_u24 %0, %0, %1, %2" : "+v"(a[i]) : "v"(b), "v"(c)))
+        if (KIND == 18) K8(asm volatile("v_pk_add_u16 %0, %0, %1" : "+v"(a[i]) : "v"(b)))
+        if (KIND == 19) K8(asm volatile("v_pk_sub_i16 %0, %0, %1" : "+v"(a[i]) : "v"(b)))
+        if (KIND == 20) K8(asm volatile("v_pk_ashrrev_i16 %0, 15, %0" : "+v"(a[i])))
+        if (KIND == 21) K8(asm volatile("v_bfi_b32 %0, %1, %0, %2" : "+v"(a[i]) : "v"(b), "v"(c)))
+        if (KIND == 22) K8(asm volatile("v_and_or_b32 %0, %1, %2, %0" : "+v"(a[i]) : "v"(b), "v"(c)))
+        if (KIND == 23) K8(asm volatile("v_perm_b32 %0, %1, %2, %0" : "+v"(a[i]) : "v"(b), "v"(c)))
+        if (KIND == 24) K8(asm volatile("v_xor_b32_e32 %0, %1, %0" : "+v"(a[i]) : "v"(b)))
+        if (KIND == 25) K8(asm volatile("v_pk_min_u16 %0, %0, %1" : "+v"(a[i]) : "v"(b)))
+        if (KIND == 26) K8(asm volatile("v_pk_max_i16 %0, %0, %1" : "+v"(a[0]) : "v"(b)))
+        if (KIND == 27) K8(asm volatile("v_add_u32_e32 %0, %0, %1" : "+v"(a[0]) : "v"(b)))
+        if (KIND == 28) K8(asm volatile("v_pk_mad_i16 %0, %0, %1, %2" : "+v"(a[i]) : "v"(b), "v"(c)))
     }
     if (threadIdx.x == 0 && blockIdx.x == 0) {
         clk[0] = __builtin_amdgcn_s_memtime() - t0;
@@ -108,5 +119,16 @@ int main() {
     R(15, 1, "v_cmp_eq_u32_sdwa")
     R(16, 1, "v_add3_u32")
     R(17, 1, "v_mad_u32_u24")
+    R(18, 1, "v_pk_add_u16")
+    R(19, 1, "v_pk_sub_i16")
+    R(20, 1, "v_pk_ashrrev_i16")
+    R(21, 1, "v_bfi_b32")
+    R(22, 1, "v_and_or_b32")
+    R(23, 1, "v_perm_b32")
+    R(24, 1, "v_xor_b32_e32")
+    R(25, 1, "v_pk_min_u16")
+    R(26, 1, "v_pk_max_i16 (one dependent chain)")
+    R(27, 1, "v_add_u32 (one dependent chain)")
+    R(28, 1, "v_pk_mad_i16")
     return 0;
 }

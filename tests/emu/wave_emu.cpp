@@ -28,6 +28,7 @@ void sync() { t_wave->bar.arrive_and_wait(); }
 #include "../../include/imsame_dev.h"
 #include "../../imsame_amd/csrc/tables.h"
 #include "../../imsame_amd/csrc/nw_kernel.hip"
+#include "../../imsame_amd/csrc/nw16_kernel.hip"
 #include "../../imsame_amd/csrc/seed_kernel.hip"
 
 static void run_wave(const std::function<void(int)> &f) {
@@ -46,10 +47,12 @@ static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, cons
                   const uint32_t *cread, const uint32_t *csid, uint32_t n, const imsame_params *p, uint32_t ymax,
                   uint32_t xmax, const std::vector<uint32_t> &ml, const std::vector<uint32_t> &mi,
                   imsame_read_result *out, uint32_t *paths, uint32_t pcap, uint32_t *pused, uint32_t *flags) {
-    const NwShape sh = nw_shape(ymax, xmax);
-    std::vector<uint32_t> tb(nw_tb_words(sh) + 64, 0xABABABABu);
+    // same kernel choice as imsame_dev.hip:plan_nw
+    const bool pk = !(p->flags & IMSAME_FLAG_NW32) && nw16_fits(p->igap, p->egap, xmax, ymax);
+    const NwShape sh = pk ? nw16_shape(ymax, xmax) : nw_shape(ymax, xmax);
+    std::vector<uint32_t> tb((pk ? nw16_tb_words(sh) : nw_tb_words(sh)) + 64, 0xABABABABu);
     std::vector<int32_t> bnd((size_t)3 * sh.xcap + 64);
-    std::vector<uint8_t> lds(nw_wave_lds(sh.GPW, sh.xstride) + 64);
+    std::vector<uint8_t> lds((pk ? nw16_wave_lds(sh.GPW, sh.xstride) : nw_wave_lds(sh.GPW, sh.xstride)) + 64, 0xA5);
     uint32_t counter = 0;
     NwLaunch P;
     memset(&P, 0, sizeof P);
@@ -64,7 +67,8 @@ static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, cons
     P.counter = &counter; P.out = out;
     P.paths = paths; P.paths_cap = pcap; P.paths_used = pused; P.want_paths = p->want_paths;
     P.flags = flags;
-    if (sh.nstr > 1) run_wave([&](int lane) { nw_wave<true>(P, lds.data(), lane, 0); });
+    if (pk)               run_wave([&](int lane) { nw16_wave(P, lds.data(), lane, 0); });
+    else if (sh.nstr > 1) run_wave([&](int lane) { nw_wave<true>(P, lds.data(), lane, 0); });
     else             run_wave([&](int lane) { nw_wave<false>(P, lds.data(), lane, 0); });
     return 0;
 }

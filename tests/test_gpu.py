@@ -9,7 +9,7 @@ import tempfile
 import numpy as np
 import pytest
 
-from imsame_amd import Device, render, fasta, CLI, PARITY_FIELDS
+from imsame_amd import Device, render, fasta, CLI, PARITY_FIELDS, FLAG_NW32
 from imsame_amd import abi
 from tests import golden_io as G
 from tests import synth
@@ -33,14 +33,17 @@ def _cmp(r_dev, r_ref, limit=None):
     return bad
 
 
-def test_nw_pairs_match_reference_golden(dev, oracle):
+@pytest.mark.parametrize("flags", [0, FLAG_NW32], ids=["auto", "nw32"])
+def test_nw_pairs_match_reference_golden(dev, oracle, flags):
+    """auto: short reads (one strip) take the packed-pair int16 kernel where
+    the launch fits it; nw32: the int32 kernel for everything."""
     rows = G.nw_pairs()
     groups = collections.defaultdict(list)
     for r in rows:
-        groups[(r["igap"], r["egap"])].append(r)
+        groups[(r["igap"], r["egap"], len(r["Y"]) <= 160)].append(r)
     checked_text = 0
-    for (ig, eg), rs in groups.items():
-        p = dev.params(igap=ig, egap=eg, min_coverage=1e-9, min_identity=1e-9)
+    for (ig, eg, _), rs in groups.items():
+        p = dev.params(igap=ig, egap=eg, min_coverage=1e-9, min_identity=1e-9, flags=flags)
         X = [r["X"].encode() for r in rs]
         Y = [r["Y"].encode() for r in rs]
         res, paths, _ = dev.nw_pairs(X, Y, p, want_paths=True)
@@ -53,6 +56,41 @@ def test_nw_pairs_match_reference_golden(dev, oracle):
                 assert ident == r["identities"]
                 checked_text += 1
     assert checked_text > 250
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_nw_packed_pairs_random_vs_oracle(dev, oracle, seed):
+    """Packed-pair kernel on mixed shapes: every launch mixes record lengths
+    12..3000 and read lengths 12..160 (unequal halves, idle groups at the
+    tail), similarity 0-100 %, gap parameters up to the int16 range limit."""
+    rng = np.random.default_rng(100 + seed)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    gaps = [(-5, -2), (0, 0), (-1, 0), (-40, -2), (-7, -1), (-5, -3)]   # (-5,-3) leaves int16 range: int32
+    for ig, eg in gaps:
+        X, Y = [], []
+        for k in range(97):
+            xl = int(rng.choice([12, 13, 40, 150, 700, 1999, 2000, 2001, int(rng.integers(12, 3001))]))
+            yl = int(rng.choice([12, 31, 100, 149, 150, 151, 155, 160, int(rng.integers(12, 161))]))
+            x = acgt[rng.integers(0, 4, xl)]
+            if rng.random() < 0.7:                      # read drawn from the record, mutated
+                o = int(rng.integers(0, max(1, xl - yl)))
+                y = x[o:o + yl].copy()
+                if len(y) < yl:
+                    y = np.concatenate([y, acgt[rng.integers(0, 4, yl - len(y))]])
+                mut = rng.random(yl) < rng.choice([0.0, 0.02, 0.1, 0.3])
+                y[mut] = acgt[rng.integers(0, 4, int(mut.sum()))]
+            else:
+                y = acgt[rng.integers(0, 4, yl)]
+            X.append(x.tobytes()); Y.append(y.tobytes())
+        p = dev.params(igap=ig, egap=eg, min_coverage=1e-9, min_identity=1e-9)
+        res, _, _ = dev.nw_pairs(X, Y, p)
+        p32 = dev.params(igap=ig, egap=eg, min_coverage=1e-9, min_identity=1e-9, flags=FLAG_NW32)
+        res32, _, _ = dev.nw_pairs(X, Y, p32)
+        for k in range(len(X)):
+            o = oracle.nw(X[k], Y[k], igap=ig, egap=eg, text=False)
+            for f in ("score", "bx", "by", "length", "identities", "igaps", "egaps", "head_x", "head_y"):
+                assert int(res[k][f]) == int(o[f]), (f, k, ig, eg, len(X[k]), len(Y[k]))
+                assert int(res32[k][f]) == int(o[f]), ("nw32", f, k, ig, eg)
 
 
 def _params_for(dev, case):
@@ -121,6 +159,9 @@ def test_synthetic_c2_shape_vs_oracle_all_T(dev, oracle):
         assert rc == 0
         assert not _cmp(res, exp), _cmp(res, exp)
         assert (res["status"] == 1).sum() > 10_000
+    # the int32 kernel gives the same results as the packed-pair one
+    res32, _, _ = dev.align(n_threads=16, params=dev.params(flags=FLAG_NW32))
+    assert not _cmp(res32, res), _cmp(res32, res)
     # shards with the global chunk-head semantics equal the full run
     full, _, _ = dev.align(n_threads=8)
     parts = [dev.align(a, b, n_threads=8)[0] for a, b in ((0, 3001), (3001, 7777), (7777, 12_000))]

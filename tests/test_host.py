@@ -7,6 +7,7 @@ import subprocess
 import numpy as np
 import pytest
 
+import imsame_amd
 from imsame_amd import abi, fasta
 from imsame_amd import PARITY_FIELDS
 from tests import golden_io as G
@@ -80,20 +81,53 @@ def test_fasta_loader_matches_oracle_loader(oracle):
         assert bk[:nb].tobytes() == b2[:nb].tobytes()
 
 
-def test_emulated_nw_kernel_matches_reference_golden(emu, oracle):
-    """The NW kernel source, run lane by lane, against the reference's NW."""
+@pytest.mark.parametrize("flags", [0, imsame_amd.FLAG_NW32], ids=["auto", "nw32"])
+def test_emulated_nw_kernel_matches_reference_golden(emu, oracle, flags):
+    """The NW kernel source, run lane by lane, against the reference's NW.
+    auto: short reads take the packed-pair int16 kernel (nw16_kernel.hip)
+    wherever it fits; nw32: the int32 kernel (nw_kernel.hip) everywhere."""
     rows = [r for r in G.nw_pairs() if len(r["X"]) * len(r["Y"]) <= 80_000]
     assert len(rows) > 200
     groups = {}
-    for r in rows:
-        groups.setdefault((r["igap"], r["egap"]), []).append(r)
-    for (ig, eg), rs in groups.items():
-        p = oracle.params(igap=ig, egap=eg)
+    for r in rows:       # short reads (one strip) apart, as imsame_dev_align launches them
+        groups.setdefault((r["igap"], r["egap"], len(r["Y"]) <= 160), []).append(r)
+    for (ig, eg, _), rs in groups.items():
+        p = oracle.params(igap=ig, egap=eg, flags=flags)
         rc, res, _, flags = emu.nw_pairs([r["X"].encode() for r in rs], [r["Y"].encode() for r in rs], p)
         assert rc == 0 and flags == 0
         for k, r in enumerate(rs):
             for f in ("score", "bx", "by", "length", "identities", "igaps", "egaps", "head_x", "head_y"):
                 assert int(res[k][f]) == r[f], (f, ig, eg, len(r["X"]), len(r["Y"]))
+
+
+def test_emulated_packed_nw_mixed_shapes(emu, oracle):
+    """nw16_kernel.hip (emulated) on launches mixing record lengths, read
+    lengths (unequal halves of a pair, idle groups) and gap parameters."""
+    rng = np.random.default_rng(77)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    for ig, eg in [(-5, -2), (0, 0), (-40, -2)]:
+        X, Y = [], []
+        for k in range(11):
+            xl = int(rng.choice([12, 13, 40, 150, 333, int(rng.integers(12, 600))]))
+            yl = int(rng.choice([12, 31, 100, 149, 150, 160, int(rng.integers(12, 161))]))
+            x = acgt[rng.integers(0, 4, xl)]
+            if rng.random() < 0.7:
+                o = int(rng.integers(0, max(1, xl - yl)))
+                y = x[o:o + yl].copy()
+                if len(y) < yl:
+                    y = np.concatenate([y, acgt[rng.integers(0, 4, yl - len(y))]])
+                mut = rng.random(yl) < 0.05
+                y[mut] = acgt[rng.integers(0, 4, int(mut.sum()))]
+            else:
+                y = acgt[rng.integers(0, 4, yl)]
+            X.append(x.tobytes()); Y.append(y.tobytes())
+        p = oracle.params(igap=ig, egap=eg)
+        rc, res, _, flags = emu.nw_pairs(X, Y, p)
+        assert rc == 0 and flags == 0
+        for k in range(len(X)):
+            o = oracle.nw(X[k], Y[k], igap=ig, egap=eg, text=False)
+            for f in ("score", "bx", "by", "length", "identities", "igaps", "egaps", "head_x", "head_y"):
+                assert int(res[k][f]) == int(o[f]), (f, k, ig, eg, len(X[k]), len(Y[k]))
 
 
 def _emu_ungapped(emu, db, dbs, q, qs, pd0, pq0, read, sid):
@@ -146,8 +180,9 @@ def test_emulated_ungapped_matches_reference_golden(emu, oracle):
         assert _emu_ungapped(emu, ref, rst, q2, qs2, 1000 + off, off, 0, sid) == exp
 
 
+@pytest.mark.parametrize("flags", [0, imsame_amd.FLAG_NW32], ids=["auto", "nw32"])
 @pytest.mark.parametrize("name", ["borrowed", "edges", "reads_vs_reads", "toolong"])
-def test_emulated_pipeline_matches_oracle(emu, oracle, name):
+def test_emulated_pipeline_matches_oracle(emu, oracle, name, flags):
     """Seed scan + rounds + NW (kernel source, emulated) vs the oracle."""
     case = G.e2e_case(name)
     db, dbs, brk = fasta.load(case["db"], True)
@@ -155,6 +190,7 @@ def test_emulated_pipeline_matches_oracle(emu, oracle, name):
     for T in [int(t) for t in case["meta"]["runs"]]:
         p = oracle.params()
         rc1, r1, er = oracle.align(db, dbs, q, qs, p, T, brk)
+        p.flags = flags
         rc2, r2, _, st = emu.align(db, dbs, q, qs, p, T, db_brk=brk)
         assert rc1 == rc2
         n = er if rc1 else len(r1)
