@@ -188,6 +188,7 @@ struct imsame_ctx {
     uint64_t n_q = 0, q_len = 0;
     std::vector<uint64_t> h_q_start;
     bool have_query = false;
+    bool q_len_mult = false;         // every read length is a multiple of NW_K
     // per-read state
     DBuf res, cur_p, cur_h, memo, nmemo, rstat, act0, act1, cbase, ccnt, perr;
     // candidates
@@ -372,6 +373,8 @@ extern "C" int imsame_dev_set_query(imsame_ctx *c, const uint8_t *q_seq, uint64_
     c->n_q = n_q; c->q_len = q_len;
     c->h_q_start.assign(q_start, q_start + n_q);
     c->h_q_start.push_back(q_len);
+    c->q_len_mult = true;
+    for (uint64_t r = 0; r < n_q; ++r) c->q_len_mult = c->q_len_mult && (c->h_q_start[r + 1] - c->h_q_start[r]) % NW_K == 0;
     if (c->q.ensure(q_len + 64) || c->q_start.ensure((n_q + 1) * 8)) return IMSAME_E_OOM;
     if (q_len) HIPCHK(hipMemcpyAsync(c->q.p, q_seq, q_len, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(c->q_start.p, c->h_q_start.data(), (n_q + 1) * 8, hipMemcpyHostToDevice, c->stream));
@@ -393,19 +396,22 @@ static int build_tables(imsame_ctx *c, const imsame_params *p, uint32_t ymax, ui
     return 0;
 }
 
-struct NwPlan { int G, GPW, xcap, xstride, steps, nstr; bool pk; size_t lds; unsigned blocks; uint64_t tb_dw; };
+struct NwPlan { int G, GPW, xcap, xstride, steps, nstr; bool pk, last4; size_t lds; unsigned blocks; uint64_t tb_dw; };
 
 // pk: the packed-pair int16 kernel (nw16_kernel.hip) when the launch fits it
-static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, const imsame_params *p, NwPlan *pl) {
+// ylen_mult: every read of the launch has a length that is a multiple of NW_K
+static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, const imsame_params *p,
+                   bool ylen_mult, NwPlan *pl) {
     const int wpb = 4;
     pl->pk = !(p->flags & IMSAME_FLAG_NW32) && nw16_fits(p->igap, p->egap, xcap, ymax);
+    pl->last4 = pl->pk && ylen_mult;
     const NwShape sh = pl->pk ? nw16_shape(ymax, xcap) : nw_shape(ymax, xcap);
     pl->G = sh.G; pl->GPW = sh.GPW; pl->nstr = sh.nstr; pl->xcap = sh.xcap; pl->xstride = sh.xstride;
     pl->steps = sh.steps;
     pl->tb_dw = pl->pk ? nw16_tb_words(sh) : nw_tb_words(sh);
     pl->lds = (size_t)wpb * (pl->pk ? nw16_wave_lds(pl->GPW, pl->xstride) : nw_wave_lds(pl->GPW, pl->xstride));
     int per_cu = 0;
-    hipError_t oe = pl->pk ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw16_kernel, wpb * 64, pl->lds)
+    hipError_t oe = pl->pk ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw16_kernel<false>, wpb * 64, pl->lds)
                   : (pl->nstr > 1)
                       ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw_kernel<true>, wpb * 64, pl->lds)
                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw_kernel<false>, wpb * 64, pl->lds);
@@ -443,7 +449,8 @@ static int launch_nw(imsame_ctx *c, const NwPlan &pl, const uint32_t *cread, con
     P.flags = (uint32_t *)(ctr + C_FLAGS);
     HIPCHK(hipMemsetAsync(work, 0, 4, s));
     HIPCHK(hipEventRecord(c->ev0, s));
-    if (pl.pk)            nw16_kernel<<<pl.blocks, 256, pl.lds, s>>>(P);
+    if (pl.pk && pl.last4) nw16_kernel<true><<<pl.blocks, 256, pl.lds, s>>>(P);
+    else if (pl.pk)       nw16_kernel<false><<<pl.blocks, 256, pl.lds, s>>>(P);
     else if (pl.nstr > 1) nw_kernel<true><<<pl.blocks, 256, pl.lds, s>>>(P);
     else                  nw_kernel<false><<<pl.blocks, 256, pl.lds, s>>>(P);
     HIPCHK(hipEventRecord(c->ev1, s));
@@ -504,6 +511,8 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
     // it); later rounds emit up to SPEC_MAX, bounded by the candidate buffers
     const char *spec_env = getenv("IMSAME_SPEC");
     const uint32_t spec_later = spec_env ? (uint32_t)std::max(1, std::min(SPEC_MAX, atoi(spec_env))) : 4u;
+    const char *bud_env = getenv("IMSAME_SEED_BUDGET");
+    const uint32_t budget1 = bud_env ? (uint32_t)std::max(0, atoi(bud_env)) : SEED_BUDGET1;
     uint64_t *ctr = c->ctr.as<uint64_t>();
     HIPCHK(hipMemsetAsync(ctr, 0, C_NSLOTS * 8, s));
     const unsigned long long errinit = ~0ull;
@@ -534,6 +543,8 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
         S.minraw = c->minraw.as<uint64_t>(); S.n_minraw = ymax + 1;
         S.max_rs = p->max_read_size; S.short_ylen = short_y;
         S.spec = (st.rounds == 1) ? 1u : std::max<uint32_t>(1u, std::min<uint32_t>(spec_later, n / nact));
+        S.budget = seed_budget(budget1, (uint32_t)st.rounds);
+        S.next = nxt; S.nnext = (uint32_t *)(ctr + C_NNEXT);
         S.cbase = c->cbase.as<uint32_t>(); S.ccnt = c->ccnt.as<uint32_t>(); S.perr = c->perr.as<uint32_t>();
         S.cread = c->cread.as<uint32_t>(); S.csid = c->csid.as<uint32_t>(); S.ncand = (uint32_t *)(ctr + C_NCAND);
         S.cread2 = c->cread2.as<uint32_t>(); S.csid2 = c->csid2.as<uint32_t>(); S.ncand2 = (uint32_t *)(ctr + C_NCAND2);
@@ -542,21 +553,21 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
         seed_kernel<<<nblk(nact, 256), 256, 0, s>>>(S);
         HIPCHK(hipEventRecord(c->ev1, s));
         HIPCHK(hipGetLastError());
-        uint64_t hc[2];
-        HIPCHK(hipMemcpyAsync(hc, ctr + C_NCAND, 16, hipMemcpyDeviceToHost, s));
+        uint64_t hc[3];
+        HIPCHK(hipMemcpyAsync(hc, ctr + C_NCAND, 24, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         float fs = 0;
         HIPCHK(hipEventElapsedTime(&fs, c->ev0, c->ev1));
         st.ms_seed += fs;
         const uint32_t n1 = (uint32_t)hc[0], n2 = (uint32_t)hc[1];
-        if (n1 + n2 == 0) break;
+        if (n1 + n2 + hc[2] == 0) break;                          // no candidates, nobody paused
         struct Cls { uint32_t n; uint32_t *cr, *cs; imsame_read_result *o; uint32_t ylim; int work; };
         Cls cls[2] = {{n1, c->cread.as<uint32_t>(), c->csid.as<uint32_t>(), c->cout.as<imsame_read_result>(), short_y, C_WORK},
                       {n2, c->cread2.as<uint32_t>(), c->csid2.as<uint32_t>(), c->cout2.as<imsame_read_result>(), ycap, C_WORK2}};
         for (int k = 0; k < 2; ++k) {
             if (!cls[k].n) continue;
             NwPlan pl;
-            plan_nw(c, cls[k].ylim, xcap, cls[k].n, p, &pl);
+            plan_nw(c, cls[k].ylim, xcap, cls[k].n, p, c->q_len_mult, &pl);
             double ms = 0;
             rc = launch_nw(c, pl, cls[k].cr, cls[k].cs, cls[k].n, cls[k].o, p->igap, p->egap, p, ymax, xcap,
                            (uint32_t *)(ctr + cls[k].work), c->db.as<uint8_t>(), c->db_start.as<uint64_t>(),
@@ -660,7 +671,9 @@ extern "C" int imsame_dev_nw_pairs(imsame_ctx *c, const uint8_t *xs, const uint6
     uint64_t *ctr = c->ctr.as<uint64_t>();
     HIPCHK(hipMemsetAsync(ctr, 0, C_NSLOTS * 8, s));
     NwPlan pl;
-    plan_nw(c, ymax, xmax, (uint32_t)npairs, p, &pl);
+    bool ymult = true;
+    for (uint64_t k = 0; k < npairs; ++k) ymult = ymult && (y_start[k + 1] - y_start[k]) % NW_K == 0;
+    plan_nw(c, ymax, xmax, (uint32_t)npairs, p, ymult, &pl);
     double ms = 0;
     rc = launch_nw(c, pl, dc.as<uint32_t>(), dc.as<uint32_t>(), (uint32_t)npairs, dout.as<imsame_read_result>(),
                    p->igap, p->egap, p, ymax, xmax, (uint32_t *)(ctr + C_WORK), dx.as<uint8_t>(), dxs.as<uint64_t>(),

@@ -82,6 +82,9 @@ __host__ __device__ static inline size_t nw16_wave_lds(int GPW, int xstride) {
     return (size_t)GPW * 2 * xstride + 64 * 8 * 4;
 }
 
+// LAST4: every read length of the launch is a multiple of NW_K, so each
+// candidate's last column is slot NW_K-1 of its owner lane (no select).
+template <bool LAST4>
 __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const uint32_t slot) {
     const int G = P.G, GPW = P.GPW;
     const int g = lane / G, gl = lane - g * G;
@@ -232,11 +235,14 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
                 w = wv_and_or(cum, 0x40004u << sh, w);
                 w = wv_and_or(nclm, 0x80008u << sh, w);
             }
-            tb2[(uint32_t)t * 64u + (uint32_t)lane] = make_uint2(w0, w1);   // rows outside [1, xlen) never read
+            // rows outside [1, xlen) are never read; 32-bit byte offset from the
+            // wave-uniform slot base (global_store saddr form)
+            *(uint2 *)((uint8_t *)tb2 + ((uint32_t)t * 512u + (uint32_t)lane * 8u)) = make_uint2(w0, w1);
             // last column (rows 1 .. xlen-2) and last row (:481-484)
-            uint32_t vl = cur[0];
+            uint32_t vl = cur[LAST4 ? NW_K - 1 : 0];
+            if (!LAST4)
 #pragma unroll
-            for (int s = 1; s < NW_K; ++s) vl = wv_bfi(lastm[s], cur[s], vl);
+                for (int s = 1; s < NW_K; ++s) vl = wv_bfi(lastm[s], cur[s], vl);
             uint32_t km = pk_neg_mask(pk_sub(vl, bestC));             // keep where vl < best (">=" takes)
             if (CAREFUL) {
                 km |= pk_neg_mask(pk_sub(limp, ipk)) | pk_neg_mask(pk_sub(ipk, pk1(1)));
@@ -327,11 +333,12 @@ __host__ static inline uint64_t nw16_tb_words(const NwShape &s) { return (uint64
 #ifndef NW16_WAVES_PER_EU
 #define NW16_WAVES_PER_EU 4
 #endif
+template <bool LAST4>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NW16_WAVES_PER_EU)))
 void nw16_kernel(NwLaunch P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
-    const uint32_t slot = blockIdx.x * (blockDim.x >> 6) + wib;
-    nw16_wave(P, smem + wib * nw16_wave_lds(P.GPW, P.xstride), lane, slot);
+    const uint32_t slot = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + wib);   // wave-uniform
+    nw16_wave<LAST4>(P, smem + wib * nw16_wave_lds(P.GPW, P.xstride), lane, slot);
 }
 #endif

@@ -472,7 +472,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MULTI ? 3 :
 void nw_kernel(NwLaunch P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
-    const uint32_t slot = blockIdx.x * (blockDim.x >> 6) + wib;
+    const uint32_t slot = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + wib);   // wave-uniform
     nw_wave<MULTI>(P, smem + wib * nw_wave_lds(P.GPW, P.xstride), lane, slot);
 }
 #endif

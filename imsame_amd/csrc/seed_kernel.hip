@@ -26,6 +26,8 @@ struct SeedLaunch {
     const uint64_t *minraw; uint32_t n_minraw;
     uint64_t max_rs; uint32_t short_ylen;
     uint32_t spec;                         // candidates a read may emit this round (1..SPEC_MAX)
+    uint32_t budget;                       // ungapped extensions a read may run this round (0: no limit)
+    uint32_t *next, *nnext;                // reads that paused on the budget (next round's active list)
     uint32_t *cbase, *ccnt;                // per read: first slot and count of this round's candidates
     uint32_t *perr;                        // per read: 1 + record of a pending size error, 0 = none
     uint32_t *cread, *csid, *ncand;        // class 0: ylen <= short_ylen
@@ -34,6 +36,16 @@ struct SeedLaunch {
     unsigned long long *nhits;
 };
 #define SPEC_MAX 8
+// Hit budget per read and round: round 1 lets a read run SEED_BUDGET1
+// ungapped extensions (true reads accept within a few), each later round 8x
+// more, so reads that scan every window finish in a compacted list.
+#define SEED_BUDGET1 32u
+__host__ __device__ static inline uint32_t seed_budget(uint32_t b1, uint32_t round) {
+    if (b1 == 0) return 0;
+    uint64_t b = b1;
+    for (uint32_t k = 1; k < round && b < (1ull << 31); ++k) b *= 8;
+    return b >= (1ull << 31) ? 0u : (uint32_t)b;
+}
 
 // 16 bytes p[a .. a+15] as 4 dwords (a >= 0; buffers carry >= 20 B of tail
 // padding): 5 aligned dword loads + byte alignment.
@@ -141,7 +153,15 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint
     uint32_t emit[SPEC_MAX];
     uint32_t ne = 0, perr = 0;
     uint32_t code = 0;
-    bool have = false, stop = false;
+    bool have = false, stop = false, paused = false;
+    // A read that runs out of budget pauses at the hit it has not examined
+    // and resumes there next round: the visiting order is unchanged, so this
+    // only reshapes the work (reads that scan every window -- no true hit --
+    // stop holding back the waves of reads that accept at their first hits).
+    uint32_t budget = S.budget ? S.budget : 0xFFFFFFFFu;
+    // speculate only for reads that already had a candidate rejected: a
+    // read's first candidate is usually accepted (paused reads included)
+    const uint32_t spec = nm ? S.spec : 1u;
     for (; p < up_to && !stop; ++p, h = 0) {
         if (!have) {
             code = 0;
@@ -159,6 +179,12 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint
             for (int m = 0; m < MEMO; ++m) skip |= memo[m] == sid;
             for (uint32_t m = 0; m < ne; ++m) skip |= emit[m] == sid;
             if (skip) continue;                 // NW(sid, r) already rejected or pending (Q18)
+            if (budget == 0) {
+                S.cur_p[k] = p; S.cur_h[k] = h;                      // resume at this hit
+                paused = stop = true;
+                break;
+            }
+            --budget;
             const int64_t xs = (int64_t)S.db_start[sid];
             const int64_t xe = (sid == S.n_db - 1) ? (int64_t)S.db_len : (int64_t)S.db_start[sid + 1] - 1;
             ++hits;
@@ -172,7 +198,7 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint
                     break;
                 }
                 emit[ne++] = sid;
-                if (ne == S.spec) {
+                if (ne == spec) {
                     S.cur_p[k] = p; S.cur_h[k] = h + 1;              // resume after this hit
                     stop = true;
                     break;
@@ -185,12 +211,14 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint
         if (perr) {
             S.rstat[k] = RS_ERROR;
             wv_atomic_min64(S.err, (unsigned long long)((r << 32) | (perr - 1)));
+        } else if (paused) {
+            S.next[wv_atomic_add(S.nnext, 1u)] = (uint32_t)r;       // still active
         } else {
             S.rstat[k] = RS_DONE;
         }
         return;
     }
-    if (ne < S.spec && !perr) { S.cur_p[k] = up_to; S.cur_h[k] = 0; }   // scan exhausted
+    if (ne < spec && !perr && !paused) { S.cur_p[k] = up_to; S.cur_h[k] = 0; }   // scan exhausted
     S.perr[k] = perr;
     const bool shortc = ylen <= S.short_ylen;
     const uint32_t o = wv_atomic_add(shortc ? S.ncand : S.ncand2, ne);

@@ -11,8 +11,9 @@
 
 #define WV_DEVICE __device__ __forceinline__
 
-// lane l receives lane l-1's value (lane 0 receives 0): DPP wave_shr:1
-WV_DEVICE int wv_shr1(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, false); }
+// lane l receives lane l-1's value (lane 0 receives 0): DPP wave_shr:1 with
+// bound_ctrl zero fill (no v_mov to seed the destination's old value)
+WV_DEVICE int wv_shr1(int v) { return __builtin_amdgcn_mov_dpp(v, 0x138, 0xf, 0xf, true); }
 // max of three signed ints in one VALU op (v_max3_i32)
 WV_DEVICE int wv_max3(int a, int b, int c) {
     int r;

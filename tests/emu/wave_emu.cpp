@@ -67,7 +67,10 @@ static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, cons
     P.counter = &counter; P.out = out;
     P.paths = paths; P.paths_cap = pcap; P.paths_used = pused; P.want_paths = p->want_paths;
     P.flags = flags;
-    if (pk)               run_wave([&](int lane) { nw16_wave(P, lds.data(), lane, 0); });
+    bool ymult = true;        // every read length a multiple of NW_K (imsame_dev.hip: q_len_mult)
+    for (uint32_t k = 0; k < n; ++k) ymult = ymult && (qs[cread[k] + 1] - qs[cread[k]]) % NW_K == 0;
+    if (pk && ymult)      run_wave([&](int lane) { nw16_wave<true>(P, lds.data(), lane, 0); });
+    else if (pk)          run_wave([&](int lane) { nw16_wave<false>(P, lds.data(), lane, 0); });
     else if (sh.nstr > 1) run_wave([&](int lane) { nw_wave<true>(P, lds.data(), lane, 0); });
     else             run_wave([&](int lane) { nw_wave<false>(P, lds.data(), lane, 0); });
     return 0;
@@ -154,6 +157,8 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
     std::vector<uint32_t> cbase(n), ccnt(n), perr(n);
     const char *spec_env = getenv("IMSAME_SPEC");
     const uint32_t spec_later = spec_env ? (uint32_t)std::max(1, std::min(SPEC_MAX, atoi(spec_env))) : 4u;
+    const char *bud_env = getenv("IMSAME_SEED_BUDGET");
+    const uint32_t budget1 = bud_env ? (uint32_t)std::max(0, atoi(bud_env)) : SEED_BUDGET1;
     std::vector<uint8_t> nmemo(n), rstat(n);
     std::vector<imsame_read_result> o1(n), o2(n);
     InitLaunch I = {qs.data(), read_from, n, res, cur_p.data(), cur_h.data(), nmemo.data(), rstat.data(), act.data()};
@@ -179,12 +184,14 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
         S.minraw = mr.data(); S.n_minraw = ymax + 1;
         S.max_rs = p->max_read_size; S.short_ylen = short_y;
         S.spec = (st.rounds == 1) ? 1u : std::max<uint32_t>(1u, std::min<uint32_t>(spec_later, n / nact));
+        S.budget = seed_budget(budget1, (uint32_t)st.rounds);
+        S.next = nxt.data(); S.nnext = &nc[2];
         S.cbase = cbase.data(); S.ccnt = ccnt.data(); S.perr = perr.data();
         S.cread = cr.data(); S.csid = cs.data(); S.ncand = &nc[0];
         S.cread2 = cr2.data(); S.csid2 = cs2.data(); S.ncand2 = &nc[1];
         S.err = &err; S.nhits = &nhits;
         for (uint32_t i = 0; i < nact; ++i) { uint64_t h = 0; seed_one(S, i, h); nhits += h; }
-        if (nc[0] + nc[1] == 0) break;
+        if (nc[0] + nc[1] + nc[2] == 0) break;
         struct { uint32_t n; uint32_t *r, *s; imsame_read_result *o; uint32_t y; } cls[2] = {
             {nc[0], cr.data(), cs.data(), o1.data(), short_y}, {nc[1], cr2.data(), cs2.data(), o2.data(), ycap}};
         for (auto &c : cls) {

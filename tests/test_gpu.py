@@ -65,12 +65,17 @@ def test_nw_packed_pairs_random_vs_oracle(dev, oracle, seed):
     tail), similarity 0-100 %, gap parameters up to the int16 range limit."""
     rng = np.random.default_rng(100 + seed)
     acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
-    gaps = [(-5, -2), (0, 0), (-1, 0), (-40, -2), (-7, -1), (-5, -3)]   # (-5,-3) leaves int16 range: int32
-    for ig, eg in gaps:
+    # (-5,-3) leaves the int16 range (int32 kernel); mult5: every read length a
+    # multiple of NW_K (the static-last-column variant)
+    gaps = [(-5, -2, 0), (0, 0, 0), (-1, 0, 0), (-40, -2, 0), (-7, -1, 0), (-5, -3, 0), (-5, -2, 1), (-2, -1, 1)]
+    for ig, eg, mult5 in gaps:
         X, Y = [], []
         for k in range(97):
             xl = int(rng.choice([12, 13, 40, 150, 700, 1999, 2000, 2001, int(rng.integers(12, 3001))]))
-            yl = int(rng.choice([12, 31, 100, 149, 150, 151, 155, 160, int(rng.integers(12, 161))]))
+            if mult5:
+                yl = int(rng.choice([15, 100, 150, 160, 5 * int(rng.integers(3, 33))]))
+            else:
+                yl = int(rng.choice([12, 31, 100, 149, 150, 151, 155, 160, int(rng.integers(12, 161))]))
             x = acgt[rng.integers(0, 4, xl)]
             if rng.random() < 0.7:                      # read drawn from the record, mutated
                 o = int(rng.integers(0, max(1, xl - yl)))
@@ -159,6 +164,15 @@ def test_synthetic_c2_shape_vs_oracle_all_T(dev, oracle):
         assert rc == 0
         assert not _cmp(res, exp), _cmp(res, exp)
         assert (res["status"] == 1).sum() > 10_000
+    # tiny seed budgets (reads pause and resume every hit or three) change nothing
+    for b in ("1", "3"):
+        os.environ["IMSAME_SEED_BUDGET"] = b
+        try:
+            resb, _, stb = dev.align(n_threads=16)
+        finally:
+            del os.environ["IMSAME_SEED_BUDGET"]
+        assert not _cmp(resb, res), (b, _cmp(resb, res))
+        assert stb.rounds > st.rounds
     # the int32 kernel gives the same results as the packed-pair one
     res32, _, _ = dev.align(n_threads=16, params=dev.params(flags=FLAG_NW32))
     assert not _cmp(res32, res), _cmp(res32, res)

@@ -105,11 +105,14 @@ def test_emulated_packed_nw_mixed_shapes(emu, oracle):
     lengths (unequal halves of a pair, idle groups) and gap parameters."""
     rng = np.random.default_rng(77)
     acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
-    for ig, eg in [(-5, -2), (0, 0), (-40, -2)]:
+    for ig, eg, mult5 in [(-5, -2, False), (0, 0, False), (-40, -2, False), (-5, -2, True), (-3, -1, True)]:
         X, Y = [], []
         for k in range(11):
             xl = int(rng.choice([12, 13, 40, 150, 333, int(rng.integers(12, 600))]))
-            yl = int(rng.choice([12, 31, 100, 149, 150, 160, int(rng.integers(12, 161))]))
+            if mult5:       # every read length a multiple of NW_K: the LAST4 variant
+                yl = int(rng.choice([15, 100, 150, 160, 5 * int(rng.integers(3, 33))]))
+            else:
+                yl = int(rng.choice([12, 31, 100, 149, 150, 160, int(rng.integers(12, 161))]))
             x = acgt[rng.integers(0, 4, xl)]
             if rng.random() < 0.7:
                 o = int(rng.integers(0, max(1, xl - yl)))
@@ -198,6 +201,27 @@ def test_emulated_pipeline_matches_oracle(emu, oracle, name, flags):
             assert np.array_equal(r1[f][:n], r2[f][:n]), (name, T, f)
         if rc1:
             assert st.err_read == er
+
+
+@pytest.mark.parametrize("budget", ["1", "3"])
+def test_emulated_pipeline_seed_budget(emu, oracle, budget, monkeypatch):
+    """Reads that pause on the per-round hit budget (seed_kernel.hip) resume
+    at the same hit: results equal the oracle's for every budget."""
+    monkeypatch.setenv("IMSAME_SEED_BUDGET", budget)
+    rounds = 0
+    for name in ("borrowed", "reads_vs_reads", "toolong"):
+        case = G.e2e_case(name)
+        db, dbs, brk = fasta.load(case["db"], True)
+        q, qs, _ = fasta.load(case["query"])
+        T = int(list(case["meta"]["runs"])[-1])
+        rc1, r1, er = oracle.align(db, dbs, q, qs, oracle.params(), T, brk)
+        rc2, r2, _, st = emu.align(db, dbs, q, qs, oracle.params(), T, db_brk=brk)
+        assert rc1 == rc2
+        n = er if rc1 else len(r1)
+        for f in PARITY_FIELDS:
+            assert np.array_equal(r1[f][:n], r2[f][:n]), (name, budget, f)
+        rounds = max(rounds, st.rounds)
+    assert rounds >= 3
 
 
 def test_thresholds_match_long_double_tests(emu, oracle):
