@@ -53,7 +53,6 @@ __host__ static inline bool nw16_fits(int64_t ig, int64_t eg, uint64_t xcap, uin
 WV_DEVICE uint32_t pk1(int v) { return (uint32_t)(uint16_t)v * 0x10001u; }
 WV_DEVICE uint32_t pk2(int lo, int hi) { return (uint32_t)(uint16_t)lo | ((uint32_t)(uint16_t)hi << 16); }
 WV_DEVICE int pk_half(uint32_t v, int h) { return (int)(int16_t)(h ? (v >> 16) : (v & 0xFFFFu)); }
-WV_DEVICE uint32_t wv_bfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
 WV_DEVICE uint32_t base_code(uint8_t b) { return (b >> 1) & 3u; }          // A0 C1 T2 G3: distinct
 
 // score table for v_perm: selector byte d = xcode ^ ycode picks the low byte

@@ -48,17 +48,12 @@ __host__ __device__ static inline uint32_t seed_budget(uint32_t b1, uint32_t rou
 }
 
 // 16 bytes p[a .. a+15] as 4 dwords (a >= 0; buffers carry >= 20 B of tail
-// padding): 5 aligned dword loads + byte alignment.
+// padding): one unaligned global_load_dwordx4 (the ROCm runtime runs the
+// GPU in unaligned-access mode; hipcc emits the single load for this memcpy).
 struct Bytes16 { uint32_t w[4]; };
 __device__ __forceinline__ Bytes16 load16(const uint8_t *__restrict__ p, int64_t a) {
-    const uint32_t *b = (const uint32_t *)(p + (a & ~(int64_t)3));
-    const uint32_t sh = (uint32_t)(a & 3);
-    uint32_t v[5];
-#pragma unroll
-    for (int k = 0; k < 5; ++k) v[k] = b[k];
     Bytes16 r;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) r.w[k] = sh ? ((v[k] >> (8 * sh)) | (v[k + 1] << (32 - 8 * sh))) : v[k];
+    __builtin_memcpy(&r, p + a, 16);
     return r;
 }
 __device__ __forceinline__ bool byte_eq(const Bytes16 &a, const Bytes16 &b, int k) {

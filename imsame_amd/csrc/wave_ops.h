@@ -58,10 +58,17 @@ WV_DEVICE uint32_t pk_neg_mask(uint32_t a) {
     asm("v_pk_ashrrev_i16 %0, 15, %1 op_sel_hi:[0,1]" : "=v"(r) : "v"(a));
     return r;
 }
-// (m & c) | w in one v_and_or_b32 (left to itself LLVM emits and + or3)
+// (m & c) | w and m ? a : b as v_bitop3_b32 (truth tables 0xEA / 0xCA):
+// bitop3 issues at the full VALU rate, v_and_or_b32 / v_bfi_b32 at half
+// (scripts/micro/valu_rate.hip); asm so LLVM cannot pick the slow forms.
 WV_DEVICE uint32_t wv_and_or(uint32_t m, uint32_t c, uint32_t w) {
     uint32_t r;
-    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(c), "v"(w));
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xea" : "=v"(r) : "v"(m), "v"(c), "v"(w));
+    return r;
+}
+WV_DEVICE uint32_t wv_bfi(uint32_t m, uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(r) : "v"(m), "v"(a), "v"(b));
     return r;
 }
 // byte permute of the 8 bytes {hi:lo}: selector byte k picks byte sel_k (0-3 of lo, 4-7 of hi)
@@ -142,6 +149,7 @@ inline uint32_t pk_sub(uint32_t a, uint32_t b) { return pk_map(a, b, [](int x, i
 inline uint32_t pk_max(uint32_t a, uint32_t b) { return pk_map(a, b, [](int x, int y) { return x > y ? x : y; }); }
 inline uint32_t pk_neg_mask(uint32_t a) { return pk_map(a, 0, [](int x, int) { return x < 0 ? -1 : 0; }); }
 inline uint32_t wv_and_or(uint32_t m, uint32_t c, uint32_t w) { return (m & c) | w; }
+inline uint32_t wv_bfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
 inline uint32_t wv_perm(uint32_t hi, uint32_t lo, uint32_t sel) {
     const uint64_t v = ((uint64_t)hi << 32) | lo;
     uint32_t r = 0;

@@ -56,6 +56,32 @@ __global__ __launch_bounds__(256) void k_rate(int *out, int seed, unsigned long 
         if (KIND == 26) K8(asm volatile("v_pk_max_i16 %0, %0, %1" : "+v"(a[0]) : "v"(b)))
         if (KIND == 27) K8(asm volatile("v_add_u32_e32 %0, %0, %1" : "+v"(a[0]) : "v"(b)))
         if (KIND == 28) K8(asm volatile("v_pk_mad_i16 %0, %0, %1, %2" : "+v"(a[i]) : "v"(b), "v"(c)))
+        if (KIND == 29) K8(asm volatile("v_sub_u32_e32 %0, %0, %1" : "+v"(a[i]) : "v"(b)))
+        if (KIND == 30) K8(asm volatile("v_lshrrev_b32_e32 %0, 3, %0" : "+v"(a[i])))
+        if (KIND == 31) K8(asm volatile("v_or_b32_e32 %0, %0, %1" : "+v"(a[i]) : "v"(b)))
+        if (KIND == 32) K8(asm volatile("v_and_b32_e32 %0, %0, %1" : "+v"(a[i]) : "v"(b)))
+        if (KIND == 33) K8(asm volatile("v_mov_b32_e32 %0, %1" : "=v"(a[i]) : "v"(a[(i + 1) & 7])))
+        if (KIND == 34) K8(asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(a[i]) : "v"(b) : "vcc"))
+        if (KIND == 35) K8(asm volatile("v_max_u16_e32 %0, %0, %1" : "+v"(a[i]) : "v"(b)))
+        if (KIND == 36) K8(asm volatile("v_add_u16_e32 %0, %0, %1" : "+v"(a[i]) : "v"(b)))
+        if (KIND == 37) K8(asm volatile("v_max_f32_e32 %0, %0, %1" : "+v"(a[i]) : "v"(b)))
+        if (KIND == 38) K8(asm volatile("v_add_f32_e32 %0, %0, %1" : "+v"(a[i]) : "v"(b)))
+        if (KIND == 39) K8(asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(*(double *)&a[i & 6]) : "v"(*(double *)&a[(i + 2) & 6])))
+        if (KIND == 40) K8(asm volatile("v_bfe_u32 %0, %0, 3, 5" : "+v"(a[i])))
+        if (KIND == 41) K8(asm volatile("v_lshlrev_b32_e32 %0, 3, %0" : "+v"(a[i])))
+        if (KIND == 42) K8(asm volatile("v_ashrrev_i32_e32 %0, 3, %0" : "+v"(a[i])))
+        if (KIND == 43) K8(asm volatile("v_subrev_u32_e32 %0, %1, %0" : "+v"(a[i]) : "v"(b)))
+        if (KIND == 44) K8(asm volatile("v_min_u32_e32 %0, %0, %1" : "+v"(a[i]) : "v"(b)))
+        if (KIND == 45) K8(asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0xca" : "+v"(a[i]) : "v"(b), "v"(c)))
+        if (KIND == 46) K8(asm volatile("v_add_u32_e32 %0, %0, %1\n\tv_pk_max_i16 %0, %0, %1" : "+v"(a[i]) : "v"(b)))
+        if (KIND == 47) K8(asm volatile("v_sub_u32_dpp %0, %1, %0 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(a[i]) : "v"(a[(i + 4) & 7])))
+        if (KIND == 48) K8(asm volatile("v_pk_max_u16 %0, %0, %1" : "+v"(a[i]) : "v"(b)))
+        if (KIND == 49) K8(asm volatile("v_not_b32_e32 %0, %0" : "+v"(a[i])))
+        if (KIND == 50) K8(asm volatile("v_pk_max_i16 %0, %0, %1\n\tv_add_u32_e32 %0, %0, %1\n\tv_sub_u32_e32 %0, %0, %2" : "+v"(a[i]) : "v"(b), "v"(c)))
+        if (KIND == 51) K8(asm volatile("v_pk_max_i16 %0, %0, %1\n\tv_bitop3_b32 %0, %0, %1, %2 bitop3:0xca" : "+v"(a[i]) : "v"(b), "v"(c)))
+        if (KIND == 52) K8(asm volatile("v_pk_max_i16 %0, %0, %1\n\tv_pk_add_u16 %0, %0, %2\n\tv_add_u32_e32 %0, %0, %1" : "+v"(a[i]) : "v"(b), "v"(c)))
+        if (KIND == 53) K8(asm volatile("v_add_u32_e32 %0, %0, %1\n\tv_sub_u32_e32 %0, %0, %2" : "+v"(a[i]) : "v"(b), "v"(c)))
+        if (KIND == 54) K8(asm volatile("v_bfi_b32 %0, %1, %0, %2\n\tv_pk_max_i16 %0, %0, %1" : "+v"(a[i]) : "v"(b), "v"(c)))
     }
     if (threadIdx.x == 0 && blockIdx.x == 0) {
         clk[0] = __builtin_amdgcn_s_memtime() - t0;
@@ -130,5 +156,31 @@ int main() {
     R(26, 1, "v_pk_max_i16 (one dependent chain)")
     R(27, 1, "v_add_u32 (one dependent chain)")
     R(28, 1, "v_pk_mad_i16")
+    R(29, 1, "v_sub_u32_e32")
+    R(30, 1, "v_lshrrev_b32_e32")
+    R(31, 1, "v_or_b32_e32")
+    R(32, 1, "v_and_b32_e32")
+    R(33, 1, "v_mov_b32_e32")
+    R(34, 1, "v_cndmask_b32_e32 (vcc)")
+    R(35, 1, "v_max_u16_e32")
+    R(36, 1, "v_add_u16_e32")
+    R(37, 1, "v_max_f32_e32")
+    R(38, 1, "v_add_f32_e32")
+    R(39, 1, "v_pk_add_f32")
+    R(40, 1, "v_bfe_u32")
+    R(41, 1, "v_lshlrev_b32_e32")
+    R(42, 1, "v_ashrrev_i32_e32")
+    R(43, 1, "v_subrev_u32_e32")
+    R(44, 1, "v_min_u32_e32")
+    R(45, 1, "v_bitop3_b32")
+    R(46, 2, "v_add_u32 + v_pk_max_i16 (mixed)")
+    R(47, 1, "v_sub_u32_dpp wave_shr:1")
+    R(48, 1, "v_pk_max_u16")
+    R(49, 1, "v_not_b32_e32")
+    R(50, 3, "pk_max + add + sub (mixed)")
+    R(51, 2, "pk_max + bitop3 (mixed)")
+    R(52, 3, "pk_max + pk_add + add (mixed)")
+    R(53, 2, "add + sub (full-rate pair)")
+    R(54, 2, "bfi + pk_max (half-rate pair)")
     return 0;
 }
