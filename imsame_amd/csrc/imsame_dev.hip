@@ -549,8 +549,13 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
         S.cread = c->cread.as<uint32_t>(); S.csid = c->csid.as<uint32_t>(); S.ncand = (uint32_t *)(ctr + C_NCAND);
         S.cread2 = c->cread2.as<uint32_t>(); S.csid2 = c->csid2.as<uint32_t>(); S.ncand2 = (uint32_t *)(ctr + C_NCAND2);
         S.err = (unsigned long long *)(ctr + C_ERR); S.nhits = (unsigned long long *)(ctr + C_HITS);
+        const char *l_env = getenv("IMSAME_SEED_L");
+        const int L = l_env ? atoi(l_env) : seed_lanes(nact);
+        const size_t slds = 256 * SEED_LDS_PER_LANE;
         HIPCHK(hipEventRecord(c->ev0, s));
-        seed_kernel<<<nblk(nact, 256), 256, 0, s>>>(S);
+        if (L >= 16)     seed_group_kernel<16><<<nblk((uint64_t)nact * 16, 256), 256, slds, s>>>(S);
+        else if (L >= 4) seed_group_kernel<4><<<nblk((uint64_t)nact * 4, 256), 256, slds, s>>>(S);
+        else             seed_kernel<<<nblk(nact, 256), 256, 0, s>>>(S);
         HIPCHK(hipEventRecord(c->ev1, s));
         HIPCHK(hipGetLastError());
         uint64_t hc[3];

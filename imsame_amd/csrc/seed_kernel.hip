@@ -222,6 +222,166 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint
     S.cbase[k] = o; S.ccnt[k] = ne;
 }
 
+// ---------------------------------------------------------------------------
+// Grouped scan for rounds with few active reads (latency-bound otherwise): a
+// group of L lanes scans L consecutive windows of ONE read at a time, lane wl
+// window p + wl in full (memory-level parallelism x L), each lane keeping the
+// first `need` e-value-passing hits of its window that are not memo'd or
+// already emitted.  The group then merges the lane lists in window order --
+// exactly the single-lane visiting order -- with seed_one's semantics:
+// distinct records up to `spec`, a size error stops the scan where it is
+// reached, and the cursor lands right after the last consumed hit (a lane
+// that stopped early because its list filled hands the rest of its window to
+// the next round).  Pauses happen at window boundaries once the group has run
+// `budget` extensions; like seed_one's pauses they only reshape the work.
+// LDS: SEED_LDS_PER_LANE bytes per lane (the lane's list).
+#define SEED_LDS_PER_LANE (SPEC_MAX * 8)
+// lanes per read: enough lanes in flight to hide the probe latency
+// (~2M lanes) without scanning many windows a read will not reach
+__host__ __device__ static inline int seed_lanes(uint32_t nact) {
+    return nact >= 1000000u ? 1 : nact >= 250000u ? 4 : 16;
+}
+
+__device__ __forceinline__ uint32_t kmer_code_at(const uint8_t *__restrict__ q, uint64_t p) {
+    const Bytes16 b = load16(q, (int64_t)p - (IMSAME_FIXED_K - 1));     // bases p-11 .. p
+    uint32_t code = 0;
+#pragma unroll
+    for (int t = 0; t < IMSAME_FIXED_K; ++t) code = (code << 2) | base2((b.w[t >> 2] >> (8 * (t & 3))) & 0xFFu);
+    return code;
+}
+
+// emit[] lives in registers, identical in every lane of the group (each lane
+// runs the same merge); statically indexed so it never spills to scratch.
+__device__ __forceinline__ bool emit_has(const uint32_t (&em)[SPEC_MAX], uint32_t ne, uint32_t sid) {
+    bool f = false;
+#pragma unroll
+    for (int m = 0; m < SPEC_MAX; ++m) f |= (uint32_t)m < ne && em[m] == sid;
+    return f;
+}
+
+template <int L>
+__device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane, uint2 *lst, uint64_t &hits) {
+    const bool gvalid = gidx < S.n_active;
+    const int gbase = lane - wl;                                  // first lane of the group
+    uint64_t r = 0, k = 0, rs = 0, re = 0, ylen = 0, up_to = 0, p = 0;
+    uint32_t h = 0, nm = 0, spec = 1, budget = 0xFFFFFFFFu;
+    uint64_t mraw = ~0ull;
+    int64_t ys = 0, ye = 0;
+    if (gvalid) {
+        r = S.active[gidx]; k = r - S.read_from;
+        rs = S.q_start[r]; re = S.q_start[r + 1]; ylen = re - rs;
+        const uint64_t from_c = (S.rpt == 0) ? 0 : min(r / S.rpt, S.T - 1) * S.rpt;   // chunk heads (Q4)
+        const bool head = S.q_start[from_c] == rs;
+        const uint64_t p0 = rs - (head ? 0 : 1);
+        up_to = (r + 1 < S.n_q) ? (re ? re - 1 : 0) : S.q_len;                     // :93
+        p = S.cur_p[k]; h = S.cur_h[k];
+        if (p == ~0ull) { p = p0 + IMSAME_FIXED_K - 1; h = 0; }
+        nm = S.nmemo[k];
+        spec = nm ? S.spec : 1u;
+        budget = S.budget ? S.budget : 0xFFFFFFFFu;
+        mraw = ylen < S.n_minraw ? S.minraw[ylen] : ~0ull;
+        ys = (int64_t)rs; ye = (r == S.n_q - 1) ? (int64_t)S.q_len : (int64_t)re - 1;
+    }
+    uint32_t emit[SPEC_MAX];
+#pragma unroll
+    for (int m = 0; m < SPEC_MAX; ++m) emit[m] = 0xFFFFFFFFu;
+    uint32_t ne = 0, perr = 0, used = 0;
+    bool done = !gvalid || p >= up_to, paused = false, exhausted = gvalid && p >= up_to;
+    while (wv_any(!done)) {
+        // ---- every lane scans its window (no wave ops in here)
+        const uint64_t pw = p + (uint64_t)wl;
+        uint32_t nl = 0, last_rel = 0, ev = 0;
+        bool full = false;
+        if (!done && pw < up_to) {
+            const uint32_t need = spec - ne;
+            const uint32_t code = kmer_code_at(S.q, pw);
+            const uint32_t wbase = S.off[code], hi = S.off[code + 1];
+            for (uint32_t e = wbase + (wl == 0 ? h : 0u); e < hi; ++e) {
+                const uint2 ent = S.ent[e];
+                const uint32_t sid = ent.y;
+                bool skip = emit_has(emit, ne, sid);
+                for (uint32_t m = 0; m < nm; ++m) skip |= S.memo[k * MEMO + m] == sid;
+                for (uint32_t m = 0; m < nl; ++m) skip |= lst[m].x == sid;
+                if (skip) continue;                       // NW(sid, r) rejected, pending or listed (Q18)
+                ++ev;
+                const int64_t xs = (int64_t)S.db_start[sid];
+                const int64_t xe = (sid == S.n_db - 1) ? (int64_t)S.db_len : (int64_t)S.db_start[sid + 1] - 1;
+                const uint64_t raw = ungapped_raw(S.db, S.q, ent.x, (int64_t)pw + 1, xs, xe, ys, ye,
+                                                  (int64_t)S.db_len, (int64_t)S.q_len);
+                if (mraw != ~0ull && raw >= mraw) {                      // e < min_e (:139)
+                    const uint64_t xlen = S.db_start[sid + 1] - S.db_start[sid];
+                    const bool bad = xlen > S.max_rs || ylen > S.max_rs;   // terror (:155) if reached
+                    lst[nl++] = make_uint2(sid, (e - wbase) | (bad ? 0x80000000u : 0u));
+                    last_rel = e - wbase;
+                    if (bad || nl == need) { full = true; break; }
+                }
+            }
+        }
+        hits += ev;
+        wv_lds_sync();                                    // lane lists written -> read by the group
+        // ---- merge in window order (every lane of the group runs the same merge)
+        uint32_t tot = 0;
+        bool stop = done;
+        for (int wk = 0; wk < L; ++wk) {
+            const uint32_t cnt = (uint32_t)wv_shfl((int)nl, gbase + wk);
+            const bool fullk = wv_shfl((int)full, gbase + wk) != 0;
+            const uint32_t lastk = (uint32_t)wv_shfl((int)last_rel, gbase + wk);
+            tot += (uint32_t)wv_shfl((int)ev, gbase + wk);
+            if (stop) continue;
+            const uint64_t pk = p + (uint64_t)wk;
+            if (pk >= up_to) { exhausted = true; stop = true; continue; }
+            const uint2 *lk = lst + (wk - wl) * SPEC_MAX;           // lane wk's list
+            for (uint32_t m = 0; m < cnt && !stop; ++m) {
+                const uint2 it = lk[m];
+                if (emit_has(emit, ne, it.x)) continue;            // emitted by an earlier window
+                if (it.y & 0x80000000u) { perr = it.x + 1; stop = true; break; }
+#pragma unroll
+                for (int q2 = 0; q2 < SPEC_MAX; ++q2) emit[q2] = ((uint32_t)q2 == ne) ? it.x : emit[q2];
+                ++ne;
+                if (ne == spec) {                                  // resume after this hit
+                    if (wl == 0) { S.cur_p[k] = pk; S.cur_h[k] = (it.y & 0x7FFFFFFFu) + 1; }
+                    stop = true;
+                }
+            }
+            if (!stop && fullk) {                                  // lane list ran dry mid-window
+                if (wl == 0) { S.cur_p[k] = pk; S.cur_h[k] = lastk + 1; }
+                paused = true; stop = true;
+            }
+        }
+        if (!stop) {
+            p += L; h = 0; used += tot;
+            if (p >= up_to) { exhausted = true; stop = true; }
+            else if (used >= budget) {
+                if (wl == 0) { S.cur_p[k] = p; S.cur_h[k] = 0; }
+                paused = true; stop = true;
+            }
+        }
+        done = stop;
+        wv_lds_sync();                                    // lists read before the next scan rewrites them
+    }
+    if (!gvalid || wl != 0) return;
+    if (ne == 0) {
+        if (perr) {
+            S.rstat[k] = RS_ERROR;
+            wv_atomic_min64(S.err, (unsigned long long)((r << 32) | (perr - 1)));
+        } else if (paused) {
+            S.next[wv_atomic_add(S.nnext, 1u)] = (uint32_t)r;       // still active
+        } else {
+            S.rstat[k] = RS_DONE;
+        }
+        return;
+    }
+    if (exhausted && !perr) { S.cur_p[k] = up_to; S.cur_h[k] = 0; }   // scan exhausted
+    S.perr[k] = perr;
+    const bool shortc = ylen <= S.short_ylen;
+    const uint32_t o = wv_atomic_add(shortc ? S.ncand : S.ncand2, ne);
+    uint32_t *cr = shortc ? S.cread : S.cread2, *cs = shortc ? S.csid : S.csid2;
+#pragma unroll
+    for (int m = 0; m < SPEC_MAX; ++m)
+        if ((uint32_t)m < ne) { cr[o + m] = (uint32_t)r; cs[o + m] = emit[m]; }
+    S.cbase[k] = o; S.ccnt[k] = ne;
+}
+
 struct UpdLaunch {
     const uint32_t *cread, *csid; uint32_t n;
     const imsame_read_result *out;
@@ -285,6 +445,17 @@ __device__ __forceinline__ void init_one(const InitLaunch &I, uint32_t k) {
 }
 
 #ifndef IMSAME_WAVE_EMU
+template <int L>
+__global__ __launch_bounds__(256) void seed_group_kernel(SeedLaunch S) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int lane = threadIdx.x & 63, wl = lane % L;
+    uint2 *lst = (uint2 *)smem + threadIdx.x * SPEC_MAX;
+    const uint32_t gidx = (blockIdx.x * blockDim.x + threadIdx.x) / L;
+    uint64_t hits = 0;
+    seed_group<L>(S, gidx, wl, lane, lst, hits);
+    if (hits) atomicAdd(S.nhits, (unsigned long long)hits);
+}
+
 __global__ __launch_bounds__(256) void seed_kernel(SeedLaunch S) {
     const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t hits = 0;

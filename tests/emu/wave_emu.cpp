@@ -190,7 +190,23 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
         S.cread = cr.data(); S.csid = cs.data(); S.ncand = &nc[0];
         S.cread2 = cr2.data(); S.csid2 = cs2.data(); S.ncand2 = &nc[1];
         S.err = &err; S.nhits = &nhits;
-        for (uint32_t i = 0; i < nact; ++i) { uint64_t h = 0; seed_one(S, i, h); nhits += h; }
+        const char *l_env = getenv("IMSAME_SEED_L");
+        const int L = l_env ? atoi(l_env) : seed_lanes(nact);
+        if (L <= 1) {
+            for (uint32_t i = 0; i < nact; ++i) { uint64_t h = 0; seed_one(S, i, h); nhits += h; }
+        } else {                   // seed_group_kernel: one 64-lane wave at a time
+            std::vector<uint2> lds(64 * SPEC_MAX);
+            std::atomic<unsigned long long> wh{0};
+            for (uint64_t w0 = 0; w0 < (uint64_t)nact * L; w0 += 64)
+                run_wave([&](int lane) {
+                    uint64_t h = 0;
+                    const uint32_t gidx = (uint32_t)((w0 + lane) / L);
+                    if (L == 16) seed_group<16>(S, gidx, lane % 16, lane, lds.data() + lane * SPEC_MAX, h);
+                    else         seed_group<4>(S, gidx, lane % 4, lane, lds.data() + lane * SPEC_MAX, h);
+                    wh += h;
+                });
+            nhits += wh;
+        }
         if (nc[0] + nc[1] + nc[2] == 0) break;
         struct { uint32_t n; uint32_t *r, *s; imsame_read_result *o; uint32_t y; } cls[2] = {
             {nc[0], cr.data(), cs.data(), o1.data(), short_y}, {nc[1], cr2.data(), cs2.data(), o2.data(), ycap}};

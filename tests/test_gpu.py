@@ -164,15 +164,16 @@ def test_synthetic_c2_shape_vs_oracle_all_T(dev, oracle):
         assert rc == 0
         assert not _cmp(res, exp), _cmp(res, exp)
         assert (res["status"] == 1).sum() > 10_000
-    # tiny seed budgets (reads pause and resume every hit or three) change nothing
-    for b in ("1", "3"):
+    # tiny seed budgets (reads pause and resume every hit or three) and every
+    # scan group size (lanes per read) change nothing
+    for b, lanes in (("1", "1"), ("3", "1"), ("3", "4"), ("0", "4"), ("1", "16"), ("0", "16")):
         os.environ["IMSAME_SEED_BUDGET"] = b
+        os.environ["IMSAME_SEED_L"] = lanes
         try:
             resb, _, stb = dev.align(n_threads=16)
         finally:
-            del os.environ["IMSAME_SEED_BUDGET"]
-        assert not _cmp(resb, res), (b, _cmp(resb, res))
-        assert stb.rounds > st.rounds
+            del os.environ["IMSAME_SEED_BUDGET"], os.environ["IMSAME_SEED_L"]
+        assert not _cmp(resb, res), (b, lanes, _cmp(resb, res))
     # the int32 kernel gives the same results as the packed-pair one
     res32, _, _ = dev.align(n_threads=16, params=dev.params(flags=FLAG_NW32))
     assert not _cmp(res32, res), _cmp(res32, res)
