@@ -30,6 +30,16 @@ METRIC = "reads aligned/sec (node), 1M×150bp vs 50Mbp ref, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md, chip-level parameters
 
 
+def nw_kernel_name(read_len, record_bp, igap=-5, egap=-2):
+    """The NW kernel imsame_dev.hip:plan_nw picks for this shape (mirror of
+    nw16_kernel.hip:nw16_fits for the default gap parameters)."""
+    if igap > 0 or egap > 0 or read_len > 160:
+        return "nw_kernel"
+    ycols = -(-read_len // 10) * 10
+    R = 4 * ycols - igap - egap * (record_bp + 64 + ycols + 2) + 16
+    return "nw16_kernel" if R <= 8191 else "nw_kernel"
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -107,16 +117,18 @@ def main():
     seq_bytes = n_nw * (a.record_bp + a.read_len)
     alg_bytes = 2 * cells + seq_bytes
     achieved = alg_bytes / (nw_ms / 1e3) / 1e9 if nw_ms else 0.0
+    kernel = nw_kernel_name(a.read_len, a.record_bp)
     traffic = None
     if os.path.exists(a.traffic_json):
         try:
             tj = json.load(open(a.traffic_json))
-            traffic = tj.get("hbm_bytes_per_launch")
+            if tj.get("kernel") == kernel:          # PMC pass of THIS kernel (profiles/)
+                traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "nw_kernel", "launches": nw_launches,
+                "kernel": kernel, "launches": nw_launches,
                 "avg_launch_ms": round(nw_ms / max(nw_launches, 1), 4),
                 "alg_bytes_per_launch": int(alg_bytes / max(nw_launches, 1)),
                 "cells_per_s": round(cells / (nw_ms / 1e3), 1) if nw_ms else 0.0}

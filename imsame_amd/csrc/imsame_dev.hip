@@ -188,7 +188,7 @@ struct imsame_ctx {
     uint64_t n_q = 0, q_len = 0;
     std::vector<uint64_t> h_q_start;
     bool have_query = false;
-    bool q_len_mult = false;         // every read length is a multiple of NW_K
+    bool q_len_mult = false;         // every read length is a multiple of NW16_K
     // per-read state
     DBuf res, cur_p, cur_h, memo, nmemo, rstat, act0, act1, cbase, ccnt, perr;
     // candidates
@@ -374,7 +374,7 @@ extern "C" int imsame_dev_set_query(imsame_ctx *c, const uint8_t *q_seq, uint64_
     c->h_q_start.assign(q_start, q_start + n_q);
     c->h_q_start.push_back(q_len);
     c->q_len_mult = true;
-    for (uint64_t r = 0; r < n_q; ++r) c->q_len_mult = c->q_len_mult && (c->h_q_start[r + 1] - c->h_q_start[r]) % NW_K == 0;
+    for (uint64_t r = 0; r < n_q; ++r) c->q_len_mult = c->q_len_mult && (c->h_q_start[r + 1] - c->h_q_start[r]) % NW16_K == 0;
     if (c->q.ensure(q_len + 64) || c->q_start.ensure((n_q + 1) * 8)) return IMSAME_E_OOM;
     if (q_len) HIPCHK(hipMemcpyAsync(c->q.p, q_seq, q_len, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(c->q_start.p, c->h_q_start.data(), (n_q + 1) * 8, hipMemcpyHostToDevice, c->stream));
@@ -399,7 +399,7 @@ static int build_tables(imsame_ctx *c, const imsame_params *p, uint32_t ymax, ui
 struct NwPlan { int G, GPW, xcap, xstride, steps, nstr; bool pk, last4; size_t lds; unsigned blocks; uint64_t tb_dw; };
 
 // pk: the packed-pair int16 kernel (nw16_kernel.hip) when the launch fits it
-// ylen_mult: every read of the launch has a length that is a multiple of NW_K
+// ylen_mult: every read of the launch has a length that is a multiple of NW16_K
 static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, const imsame_params *p,
                    bool ylen_mult, NwPlan *pl) {
     const int wpb = 4;
@@ -549,12 +549,13 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
         S.cread = c->cread.as<uint32_t>(); S.csid = c->csid.as<uint32_t>(); S.ncand = (uint32_t *)(ctr + C_NCAND);
         S.cread2 = c->cread2.as<uint32_t>(); S.csid2 = c->csid2.as<uint32_t>(); S.ncand2 = (uint32_t *)(ctr + C_NCAND2);
         S.err = (unsigned long long *)(ctr + C_ERR); S.nhits = (unsigned long long *)(ctr + C_HITS);
-        const char *l_env = getenv("IMSAME_SEED_L");
+        const char *l_env = getenv(st.rounds == 1 && getenv("IMSAME_SEED_L1") ? "IMSAME_SEED_L1" : "IMSAME_SEED_L");
         const int L = l_env ? atoi(l_env) : seed_lanes(nact);
         const size_t slds = 256 * SEED_LDS_PER_LANE;
         HIPCHK(hipEventRecord(c->ev0, s));
         if (L >= 16)     seed_group_kernel<16><<<nblk((uint64_t)nact * 16, 256), 256, slds, s>>>(S);
         else if (L >= 4) seed_group_kernel<4><<<nblk((uint64_t)nact * 4, 256), 256, slds, s>>>(S);
+        else if (L >= 2) seed_group_kernel<2><<<nblk((uint64_t)nact * 2, 256), 256, slds, s>>>(S);
         else             seed_kernel<<<nblk(nact, 256), 256, 0, s>>>(S);
         HIPCHK(hipEventRecord(c->ev1, s));
         HIPCHK(hipGetLastError());
@@ -677,7 +678,7 @@ extern "C" int imsame_dev_nw_pairs(imsame_ctx *c, const uint8_t *xs, const uint6
     HIPCHK(hipMemsetAsync(ctr, 0, C_NSLOTS * 8, s));
     NwPlan pl;
     bool ymult = true;
-    for (uint64_t k = 0; k < npairs; ++k) ymult = ymult && (y_start[k + 1] - y_start[k]) % NW_K == 0;
+    for (uint64_t k = 0; k < npairs; ++k) ymult = ymult && (y_start[k + 1] - y_start[k]) % NW16_K == 0;
     plan_nw(c, ymax, xmax, (uint32_t)npairs, p, ymult, &pl);
     double ms = 0;
     rc = launch_nw(c, pl, dc.as<uint32_t>(), dc.as<uint32_t>(), (uint32_t)npairs, dout.as<imsame_read_result>(),

@@ -67,8 +67,8 @@ static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, cons
     P.counter = &counter; P.out = out;
     P.paths = paths; P.paths_cap = pcap; P.paths_used = pused; P.want_paths = p->want_paths;
     P.flags = flags;
-    bool ymult = true;        // every read length a multiple of NW_K (imsame_dev.hip: q_len_mult)
-    for (uint32_t k = 0; k < n; ++k) ymult = ymult && (qs[cread[k] + 1] - qs[cread[k]]) % NW_K == 0;
+    bool ymult = true;        // every read length a multiple of NW16_K (imsame_dev.hip: q_len_mult)
+    for (uint32_t k = 0; k < n; ++k) ymult = ymult && (qs[cread[k] + 1] - qs[cread[k]]) % NW16_K == 0;
     if (pk && ymult)      run_wave([&](int lane) { nw16_wave<true>(P, lds.data(), lane, 0); });
     else if (pk)          run_wave([&](int lane) { nw16_wave<false>(P, lds.data(), lane, 0); });
     else if (sh.nstr > 1) run_wave([&](int lane) { nw_wave<true>(P, lds.data(), lane, 0); });

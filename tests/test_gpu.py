@@ -66,14 +66,14 @@ def test_nw_packed_pairs_random_vs_oracle(dev, oracle, seed):
     rng = np.random.default_rng(100 + seed)
     acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
     # (-5,-3) leaves the int16 range (int32 kernel); mult5: every read length a
-    # multiple of NW_K (the static-last-column variant)
+    # multiple of NW16_K (the static-last-column variant)
     gaps = [(-5, -2, 0), (0, 0, 0), (-1, 0, 0), (-40, -2, 0), (-7, -1, 0), (-5, -3, 0), (-5, -2, 1), (-2, -1, 1)]
     for ig, eg, mult5 in gaps:
         X, Y = [], []
         for k in range(97):
             xl = int(rng.choice([12, 13, 40, 150, 700, 1999, 2000, 2001, int(rng.integers(12, 3001))]))
             if mult5:
-                yl = int(rng.choice([15, 100, 150, 160, 5 * int(rng.integers(3, 33))]))
+                yl = int(rng.choice([20, 100, 150, 160, 10 * int(rng.integers(2, 17))]))
             else:
                 yl = int(rng.choice([12, 31, 100, 149, 150, 151, 155, 160, int(rng.integers(12, 161))]))
             x = acgt[rng.integers(0, 4, xl)]

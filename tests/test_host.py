@@ -109,8 +109,8 @@ def test_emulated_packed_nw_mixed_shapes(emu, oracle):
         X, Y = [], []
         for k in range(11):
             xl = int(rng.choice([12, 13, 40, 150, 333, int(rng.integers(12, 600))]))
-            if mult5:       # every read length a multiple of NW_K: the LAST4 variant
-                yl = int(rng.choice([15, 100, 150, 160, 5 * int(rng.integers(3, 33))]))
+            if mult5:       # every read length a multiple of NW16_K: the static-last-column variant
+                yl = int(rng.choice([20, 100, 150, 160, 10 * int(rng.integers(2, 17))]))
             else:
                 yl = int(rng.choice([12, 31, 100, 149, 150, 160, int(rng.integers(12, 161))]))
             x = acgt[rng.integers(0, 4, xl)]
