@@ -3,6 +3,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <pthread.h>
+#include <unistd.h>
 #include "imsame_host.h"
 
 static inline int is_acgt(uint8_t c) { return c == 'A' || c == 'C' || c == 'G' || c == 'T'; }
@@ -54,19 +56,181 @@ int host_parse_fasta(const uint8_t *b, uint64_t nb, int want_brk, host_seqs *s) 
     return 0;
 }
 
-int host_load_fasta(const char *path, int want_brk, host_seqs *s) {
+/* ---- multi-threaded parse ------------------------------
+ * A '>' that begins a line always opens a record: a header ends at its first
+ * '\n', so the byte after any '\n' is never inside a header, and text before
+ * the first '>' is skipped anyway.  Cutting the image just before such '>'
+ * gives pieces that parse independently (each opens with a record, which
+ * resets the k-mer), so piece k produces exactly the bases, starts and reset
+ * positions the serial loop produces over that stretch.  Pieces parse into
+ * private buffers; the concatenation is a prefix sum + parallel copy. */
+typedef struct {
+    const uint8_t *b;
+    uint64_t lo, hi, nb;          /* [lo, hi) of the image of nb bytes       */
+    uint8_t  *seq;                /* private bases                           */
+    uint64_t *start, n, cap_n, len;
+    uint64_t *rst, nr, cap_r;     /* positions (piece-local) with a reset bit */
+    uint64_t base_off, rec_off;   /* filled after the prefix sum             */
+    host_seqs *dst;
+    int want_brk, err;
+} parse_piece;
+
+static int push_u64(uint64_t **a, uint64_t *n, uint64_t *cap, uint64_t v) {
+    if (*n == *cap) {
+        *cap = *cap ? 2 * *cap : 256;
+        uint64_t *p = realloc(*a, *cap * sizeof(uint64_t));
+        if (!p) return -1;
+        *a = p;
+    }
+    (*a)[(*n)++] = v;
+    return 0;
+}
+
+static void *parse_piece_run(void *arg) {
+    parse_piece *p = arg;
+    const uint8_t *b = p->b;
+    p->seq = malloc(p->hi - p->lo + 1);
+    if (!p->seq) { p->err = 1; return NULL; }
+    uint64_t i = p->lo, len = 0;
+    int reset = 0;
+    while (i < p->hi) {
+        const uint8_t *gt = memchr(b + i, '>', p->hi - i);
+        if (!gt) break;
+        i = (uint64_t)(gt - b);
+        if (i + 1 == p->nb) break;          /* '>' as the image's last byte */
+        if (push_u64(&p->start, &p->n, &p->cap_n, len)) { p->err = 1; return NULL; }
+        reset = 1;
+        const uint8_t *nl = memchr(b + i, '\n', p->hi - i);
+        i = nl ? (uint64_t)(nl - b) + 1 : p->hi;
+        for (; i < p->hi; ++i) {
+            uint8_t c = b[i];
+            if (c == '>') break;
+            if (c >= 'a' && c <= 'z') c -= 32;
+            if (is_acgt(c)) {
+                if (reset && p->want_brk && push_u64(&p->rst, &p->nr, &p->cap_r, len)) { p->err = 1; return NULL; }
+                reset = 0;
+                p->seq[len++] = c;
+            } else if (c != '\n') {
+                reset = 1;
+            }
+        }
+    }
+    p->len = len;
+    return NULL;
+}
+
+static void *copy_piece_run(void *arg) {
+    parse_piece *p = arg;
+    memcpy(p->dst->seq + p->base_off, p->seq, p->len);
+    for (uint64_t k = 0; k < p->n; ++k) p->dst->start[p->rec_off + k] = p->start[k] + p->base_off;
+    return NULL;
+}
+
+static void run_pieces(parse_piece *pc, int np, void *(*fn)(void *)) {
+    pthread_t th[HOST_MAX_THREADS];
+    int started[HOST_MAX_THREADS] = {0};
+    for (int k = 1; k < np; ++k) started[k] = pthread_create(&th[k], NULL, fn, &pc[k]) == 0;
+    fn(&pc[0]);
+    for (int k = 1; k < np; ++k) {
+        if (started[k]) pthread_join(th[k], NULL);
+        else fn(&pc[k]);
+    }
+}
+
+int host_parse_fasta_mt(const uint8_t *b, uint64_t nb, int want_brk, int nthreads, uint64_t min_piece,
+                        host_seqs *s) {
+    if (nthreads > HOST_MAX_THREADS) nthreads = HOST_MAX_THREADS;
+    if (min_piece == 0) min_piece = 1u << 22;
+    uint64_t np_want = nb / min_piece;
+    if (nthreads <= 1 || np_want < 2) return host_parse_fasta(b, nb, want_brk, s);
+    if (np_want > (uint64_t)nthreads) np_want = (uint64_t)nthreads;
+    parse_piece pc[HOST_MAX_THREADS];
+    memset(pc, 0, sizeof pc);
+    /* cut points: first "\n>" at or after k*nb/np (cut before the '>') */
+    uint64_t cut[HOST_MAX_THREADS + 1];
+    int np = 0;
+    cut[0] = 0;
+    for (uint64_t k = 1; k < np_want; ++k) {
+        uint64_t x = k * nb / np_want;
+        if (x <= cut[np]) x = cut[np] + 1;
+        uint64_t c = nb;
+        while (x < nb) {
+            const uint8_t *gt = memchr(b + x, '>', nb - x);
+            if (!gt) break;
+            const uint64_t g = (uint64_t)(gt - b);
+            if (g > 0 && b[g - 1] == '\n') { c = g; break; }
+            x = g + 1;
+        }
+        if (c >= nb) break;
+        cut[++np] = c;
+    }
+    cut[++np] = nb;
+    for (int k = 0; k < np; ++k)
+        pc[k] = (parse_piece){.b = b, .lo = cut[k], .hi = cut[k + 1], .nb = nb, .want_brk = want_brk};
+    run_pieces(pc, np, parse_piece_run);
+    int err = 0;
+    uint64_t len = 0, n = 0;
+    for (int k = 0; k < np; ++k) {
+        err |= pc[k].err;
+        pc[k].base_off = len;
+        pc[k].rec_off = n;
+        len += pc[k].len;
+        n += pc[k].n;
+    }
+    memset(s, 0, sizeof *s);
+    if (!err) {
+        s->seq = malloc(len + 1);
+        s->start = malloc((n + 1) * sizeof(uint64_t));
+        if (want_brk) s->brk = calloc(len / 8 + 2, 1);
+        err = !s->seq || !s->start || (want_brk && !s->brk);
+    }
+    if (!err) {
+        for (int k = 0; k < np; ++k) pc[k].dst = s;
+        run_pieces(pc, np, copy_piece_run);
+        if (want_brk)
+            for (int k = 0; k < np; ++k)
+                for (uint64_t r = 0; r < pc[k].nr; ++r) {
+                    const uint64_t q = pc[k].rst[r] + pc[k].base_off;
+                    s->brk[q >> 3] |= (uint8_t)(1u << (q & 7));
+                }
+        s->start[n] = len;
+        s->n = n;
+        s->len = len;
+    }
+    for (int k = 0; k < np; ++k) { free(pc[k].seq); free(pc[k].start); free(pc[k].rst); }
+    if (err) { host_free_seqs(s); return -1; }
+    return 0;
+}
+
+int host_read_file(const char *path, uint8_t **buf, uint64_t *len) {
     FILE *f = fopen(path, "rb");
     if (!f) return -1;
     fseeko(f, 0, SEEK_END);
     const uint64_t sz = (uint64_t)ftello(f);
     fseeko(f, 0, SEEK_SET);
-    uint8_t *buf = malloc(sz + 1);
-    if (!buf) { fclose(f); return -1; }
-    const uint64_t got = fread(buf, 1, sz, f);
+    *buf = malloc(sz + 1);
+    if (!*buf) { fclose(f); return -1; }
+    *len = fread(*buf, 1, sz, f);
     fclose(f);
-    const int rc = host_parse_fasta(buf, got, want_brk, s);
+    return 0;
+}
+
+int host_load_fasta(const char *path, int want_brk, host_seqs *s) {
+    uint8_t *buf;
+    uint64_t n;
+    if (host_read_file(path, &buf, &n)) return -1;
+    const int rc = host_parse_fasta_mt(buf, n, want_brk, host_threads(), 0, s);
     free(buf);
     return rc;
+}
+
+int host_threads(void) {
+    const char *e = getenv("IMSAME_HOST_THREADS");
+    long t = e ? strtol(e, NULL, 10) : sysconf(_SC_NPROCESSORS_ONLN);
+    if (t > 16 && !e) t = 16;               /* GPU boxes show the whole machine's CPUs */
+    if (t < 1) t = 1;
+    if (t > HOST_MAX_THREADS) t = HOST_MAX_THREADS;
+    return (int)t;
 }
 
 void host_free_seqs(host_seqs *s) {

@@ -20,6 +20,15 @@ int  host_parse_fasta(const uint8_t *b, uint64_t nb, int want_brk, host_seqs *s)
 int  host_load_fasta(const char *path, int want_brk, host_seqs *s);
 void host_free_seqs(host_seqs *s);
 
+/* Same result as host_parse_fasta, parsed by up to nthreads threads over
+ * pieces of at least min_piece bytes (0 = 4 MiB) cut before line-initial
+ * '>' (SURVEY 8(f) row 2).  host_load_fasta uses it with host_threads(). */
+#define HOST_MAX_THREADS 64
+int  host_parse_fasta_mt(const uint8_t *b, uint64_t nb, int want_brk, int nthreads, uint64_t min_piece,
+                         host_seqs *s);
+int  host_threads(void);        /* IMSAME_HOST_THREADS, else online CPUs capped at 16 */
+int  host_read_file(const char *path, uint8_t **buf, uint64_t *len);
+
 /* backtrackingNW's strings (alignmentFunctions.c:493-560) rebuilt from a
  * device path, then build_alignment's 60-column text (:230-271).
  * Returns the identities counted by the text loop. */

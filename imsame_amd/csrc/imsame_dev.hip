@@ -234,6 +234,11 @@ extern "C" const char *imsame_strerror(int code) {
     return "unknown error";
 }
 
+extern "C" int imsame_dev_count(void) {
+    int n = 0;
+    return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+}
+
 extern "C" int imsame_dev_open(int device, imsame_ctx **out) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) return IMSAME_E_HIP;

@@ -109,7 +109,13 @@ typedef struct imsame_stats {
 
 typedef struct imsame_ctx imsame_ctx;
 
-/* Open device `device` (HIP ordinal).  Fails with IMSAME_E_HIP if no GPU. */
+/* Number of visible HIP devices (0 without a GPU).  The reference has no
+ * device notion; the all-vs-all driver uses it to pick its shard count. */
+int  imsame_dev_count(void);
+
+/* Open device `device` (HIP ordinal).  Fails with IMSAME_E_HIP if no GPU.
+ * Several contexts may be opened on one device (each owns its own stream
+ * and buffers). */
 int  imsame_dev_open(int device, imsame_ctx **out);
 void imsame_dev_close(imsame_ctx *ctx);
 const char *imsame_strerror(int code);

@@ -98,3 +98,34 @@ def to_fasta(seq, starts, prefix, width=80):
 def write_fasta(path, seq, starts, prefix, width=80):
     with open(path, "wb") as f:
         f.write(to_fasta(seq, starts, prefix, width))
+
+
+
+
+def make_genome_pool(n_genomes, genome_bp, seed):
+    """C4's shared pool: n iid uniform genomes."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    return [ACGT[rng.integers(0, 4, genome_bp, dtype=np.uint8)] for _ in range(n_genomes)]
+
+
+def make_metagenome_arr(pool, abundance, n, L, seed, sub=0.01, ins=0.0005, dele=0.0005, rc_frac=0.5):
+    """n reads of length L drawn from the pool's genomes with the given
+    abundance vector, Illumina-like errors, a fraction from the reverse
+    strand.  Returns (seq uint8[n*L], starts uint64[n])."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    ab = np.asarray(abundance, dtype=np.float64)
+    who = rng.choice(len(pool), size=n, p=ab / ab.sum())
+    out = np.empty((n, L), np.uint8)
+    for g in range(len(pool)):
+        rows = np.flatnonzero(who == g)
+        if not len(rows):
+            continue
+        s, _ = make_reads_arr(pool[g], len(rows), L, int(rng.integers(1 << 62)), sub, ins, dele, frac_true=1.0)
+        s = s.reshape(len(rows), L)
+        flip = rng.random(len(rows)) < rc_frac
+        s[flip] = s[flip][:, ::-1]
+        lut = np.zeros(256, np.uint8)
+        lut[np.frombuffer(b"ACGT", np.uint8)] = np.frombuffer(b"TGCA", np.uint8)
+        s[flip] = lut[s[flip]]
+        out[rows] = s
+    return out.reshape(-1), np.arange(0, n * L, L, dtype=np.uint64)
