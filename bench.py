@@ -30,6 +30,26 @@ METRIC = "reads aligned/sec (node), 1M×150bp vs 50Mbp ref, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md, chip-level parameters
 
 
+# BASELINE.json configs, per GPU (SURVEY 8(d) canonical inputs).  c2 is the
+# metric's configuration and the default; c3 is configs[2]'s per-GPU shard
+# (10M reads / 8 GPUs vs 500 Mbp); c5 is configs[4] (ONT-like 10 kbp reads,
+# raised MAX_READ_SIZE, reads capped per GPU by --reads).
+CONFIGS = {
+    "c2": dict(reads=1_000_000, read_len=150, ref_bp=50_000_000, record_bp=2_000, ont=False, max_rs=None,
+               cpu_sample=40_000, seeds=(42, 43),
+               workload="C2: 1M x 150 bp Illumina-like reads per GPU vs 50 Mbp synthetic reference "
+                        "(2 kbp records), BASELINE.json configs[1]"),
+    "c3": dict(reads=1_250_000, read_len=150, ref_bp=500_000_000, record_bp=2_000, ont=False, max_rs=None,
+               cpu_sample=4_000, seeds=(43, 44),
+               workload="C3 per-GPU shard: 1.25M x 150 bp reads per GPU (10M over 8) vs 500 Mbp synthetic "
+                        "reference (2 kbp records), BASELINE.json configs[2]"),
+    "c5": dict(reads=100_000, read_len=10_000, ref_bp=50_000_000, record_bp=2_000, ont=True, max_rs=10_001,
+               cpu_sample=0, seeds=(42, 48),
+               workload="C5: 10 kbp ONT-like reads (5% sub, 2.5% ins, 2.5% del) vs 50 Mbp synthetic reference, "
+                        "MAX_READ_SIZE raised to 10001, BASELINE.json configs[4]"),
+}
+
+
 def nw_kernel_name(read_len, record_bp, igap=-5, egap=-2):
     """The NW kernel imsame_dev.hip:plan_nw picks for this shape (mirror of
     nw16_kernel.hip:nw16_fits for the default gap parameters)."""
@@ -45,15 +65,23 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--reads", type=int, default=1_000_000, help="reads per GPU")
-    ap.add_argument("--read-len", type=int, default=150)
-    ap.add_argument("--ref-bp", type=int, default=50_000_000)
-    ap.add_argument("--record-bp", type=int, default=2_000)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="c2",
+                    help="BASELINE.json workload (c2 = the metric's config; c3/c5 are stress runs)")
+    ap.add_argument("--reads", type=int, default=None, help="reads per GPU (default: the config's)")
+    ap.add_argument("--read-len", type=int, default=None)
+    ap.add_argument("--ref-bp", type=int, default=None)
+    ap.add_argument("--record-bp", type=int, default=None)
     ap.add_argument("--n-threads", type=int, default=16, help="reference -n_threads semantics")
-    ap.add_argument("--cpu-sample", type=int, default=40_000, help="reads in the CPU baseline sample (0: skip)")
+    ap.add_argument("--cpu-sample", type=int, default=None,
+                    help="reads in the CPU baseline sample (0: skip; default: the config's)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "nw_traffic.json"))
-    return ap.parse_args()
+    a = ap.parse_args()
+    cfg = CONFIGS[a.config]
+    for k in ("reads", "read_len", "ref_bp", "record_bp", "cpu_sample"):
+        if getattr(a, k) is None:
+            setattr(a, k, cfg[k])
+    return a
 
 
 def main():
@@ -71,14 +99,16 @@ def main():
     from tests import synth
 
     # synthetic C2 inputs: the reference is replicated, each rank has its own reads
-    ref, rst = synth.make_reference_arr(a.ref_bp, a.record_bp, seed=42)
-    q, qs = synth.make_reads_arr(ref, a.reads, a.read_len, seed=43 + 1000 * rank)
+    cfg = CONFIGS[a.config]
+    ref, rst = synth.make_reference_arr(a.ref_bp, a.record_bp, seed=cfg["seeds"][0])
+    gen = synth.make_long_reads_arr if cfg["ont"] else synth.make_reads_arr
+    q, qs = gen(ref, a.reads, a.read_len, seed=cfg["seeds"][1] + 1000 * rank)
     dev = imsame_amd.Device(local)
     t0 = time.time()
     dev.index(ref, rst)
     t_index = time.time() - t0
     dev.set_query(q, qs)                               # H2D once: inputs resident in HBM
-    params = dev.params()
+    params = dev.params(max_read_size=cfg["max_rs"]) if cfg["max_rs"] else dev.params()
 
     def step():
         return dev.align(0, a.reads, n_threads=a.n_threads, params=params)
@@ -117,7 +147,8 @@ def main():
     seq_bytes = n_nw * (a.record_bp + a.read_len)
     alg_bytes = 2 * cells + seq_bytes
     achieved = alg_bytes / (nw_ms / 1e3) / 1e9 if nw_ms else 0.0
-    kernel = nw_kernel_name(a.read_len, a.record_bp)
+    kernel = nw_kernel_name(a.read_len, a.record_bp) if not stats[-1]["nw_launches"] or a.read_len <= 160 \
+        else "nw_kernel"
     traffic = None
     if os.path.exists(a.traffic_json):
         try:
@@ -135,15 +166,14 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_sample > 0:
-        cpu = cpu_baseline(dev, ref, rst, q, qs, a)
+        cpu = cpu_baseline(dev, ref, rst, q, qs, a, params)
 
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "reads/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "int32", "data": "synthetic",
-            "config": {"workload": "C2: 1M x 150 bp Illumina-like reads per GPU vs 50 Mbp synthetic reference "
-                                   "(2 kbp records), BASELINE.json configs[1]",
+            "config": {"workload": cfg["workload"],
                        "reads_per_gpu": a.reads, "read_len": a.read_len, "ref_bp": a.ref_bp,
                        "record_bp": a.record_bp, "n_threads_semantic": a.n_threads,
                        "parallelism": f"dp{world} (read shards, replicated index)"},
@@ -161,7 +191,7 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(dev, ref, rst, q, qs, a):
+def cpu_baseline(dev, ref, rst, q, qs, a, params):
     """The oracle (clean-room CPU restatement, 'port') on the host cores, on a
     bounded sample: the first cpu_sample reads of the rank-0 shard taken as a
     query of their own, -n_threads cpu_threads, alignment phase only (index
@@ -172,11 +202,12 @@ def cpu_baseline(dev, ref, rst, q, qs, a):
     o = Oracle.load()
     n = min(a.cpu_sample, len(qs))
     qv = q[:int(qs[n])] if n < len(qs) else q
-    rc, exp, _ = o.align(ref, rst, qv, qs[:n], None, a.cpu_threads)
+    po = o.params(max_read_size=params.max_read_size)
+    rc, exp, _ = o.align(ref, rst, qv, qs[:n], po, a.cpu_threads)
     o.lib.or_last_align_seconds.restype = C.c_double
     secs = o.lib.or_last_align_seconds()
     dev.set_query(qv, qs[:n])
-    got, _, _ = dev.align(0, n, n_threads=a.cpu_threads)
+    got, _, _ = dev.align(0, n, n_threads=a.cpu_threads, params=params)
     same = int(np.all([exp[f] == got[f] for f in PARITY_FIELDS], axis=0).sum())
     return {"value": round(n / secs, 1), "unit": "reads/s", "cores": a.cpu_threads, "kind": "port",
             "sample": f"first {n} reads of the rank-0 shard as their own query, oracle/imsame_oracle.c "

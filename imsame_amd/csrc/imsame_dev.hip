@@ -425,6 +425,19 @@ static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, 
     const uint32_t cpw = pl->pk ? 2 * pl->GPW : pl->GPW;            // candidates per wave pull
     const uint64_t waves_needed = (ncand + cpw - 1) / cpw;
     pl->blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)c->ncu * per_cu, (waves_needed + wpb - 1) / wpb));
+    // Traceback arena: one slot per resident wave.  Long reads against long
+    // records (C5, 10 kbp x 12 kbp = 60 MB per slot) would ask for more than
+    // the card holds at full residency; the kernel pulls candidates from a
+    // queue, so fewer blocks finish the same work.  Budget: half of what is
+    // free (counting the arena already held), at most 64 GB.
+    const uint64_t per_block = (uint64_t)wpb * (pl->tb_dw * 4 + 3ull * pl->xcap * 4);
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = 0;
+    const uint64_t held = c->tb.cap + c->bnd.cap;
+    const uint64_t budget = std::min<uint64_t>(64ull << 30, (fr + held) / 2);
+    const uint64_t fit = budget / per_block;
+    if (fit < 1) return IMSAME_E_OOM;
+    if (pl->blocks > fit) pl->blocks = (unsigned)fit;
     return 0;
 }
 
@@ -578,7 +591,7 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
         for (int k = 0; k < 2; ++k) {
             if (!cls[k].n) continue;
             NwPlan pl;
-            plan_nw(c, cls[k].ylim, xcap, cls[k].n, p, c->q_len_mult, &pl);
+            if ((rc = plan_nw(c, cls[k].ylim, xcap, cls[k].n, p, c->q_len_mult, &pl))) return rc;
             double ms = 0;
             rc = launch_nw(c, pl, cls[k].cr, cls[k].cs, cls[k].n, cls[k].o, p->igap, p->egap, p, ymax, xcap,
                            (uint32_t *)(ctr + cls[k].work), c->db.as<uint8_t>(), c->db_start.as<uint64_t>(),
@@ -684,7 +697,7 @@ extern "C" int imsame_dev_nw_pairs(imsame_ctx *c, const uint8_t *xs, const uint6
     NwPlan pl;
     bool ymult = true;
     for (uint64_t k = 0; k < npairs; ++k) ymult = ymult && (y_start[k + 1] - y_start[k]) % NW16_K == 0;
-    plan_nw(c, ymax, xmax, (uint32_t)npairs, p, ymult, &pl);
+    if ((rc = plan_nw(c, ymax, xmax, (uint32_t)npairs, p, ymult, &pl))) return rc;
     double ms = 0;
     rc = launch_nw(c, pl, dc.as<uint32_t>(), dc.as<uint32_t>(), (uint32_t)npairs, dout.as<imsame_read_result>(),
                    p->igap, p->egap, p, ymax, xmax, (uint32_t *)(ctr + C_WORK), dx.as<uint8_t>(), dxs.as<uint64_t>(),

@@ -100,40 +100,77 @@ typedef struct {
 
 static int brk_at(const or_seqs *d, uint64_t b) { return d->brk ? (d->brk[b >> 3] >> (b & 7)) & 1 : 0; }
 
-static int kmer_ok(const or_seqs *d, uint64_t p, uint64_t rec_start) {   /* k-mer ending at base p */
-    if (p + 1 < rec_start + K) return 0;
-    for (uint64_t b = p + 2 - K; b <= p; b++)
-        if (brk_at(d, b)) return 0;
-    return 1;
-}
-
 static uint32_t kmer_code(const uint8_t *s) {
     uint32_t c = 0;
     for (int k = 0; k < K; k++) c = (c << 2) | (uint32_t)base_code(s[k]);
     return c;
 }
 
+/* Count and scatter run in parallel over disjoint bucket ranges: every
+ * thread reads the whole code array in order but only touches its own
+ * buckets, so each bucket is still filled in descending position. */
+typedef struct { const or_seqs *d; const uint32_t *code; or_index *ix; uint32_t lo, hi; int pass; } ix_part;
+
+static void *ix_part_run(void *arg) {
+    ix_part *t = arg;
+    const or_seqs *d = t->d;
+    if (t->pass == 0) {
+        for (uint64_t p = 0; p < d->len; p++) {
+            const uint32_t c = t->code[p];
+            if (c >= t->lo && c < t->hi) t->ix->off[c + 1]++;
+        }
+    } else {
+        uint64_t *fill = t->ix->off;            /* off[c] advances to the bucket end */
+        for (uint64_t rec = d->n; rec-- > 0;)
+            for (uint64_t p = d->start[rec + 1]; p-- > d->start[rec];) {
+                const uint32_t c = t->code[p];
+                if (c < t->lo || c >= t->hi) continue;
+                t->ix->pos[fill[c]] = (uint32_t)(p + 1);   /* pos = last base + 1 (IMSAME.c:247) */
+                t->ix->sid[fill[c]] = (uint32_t)rec;       /* s_id = current record (:249)     */
+                fill[c]++;
+            }
+    }
+    return NULL;
+}
+
 static void or_build_index(const or_seqs *d, or_index *ix) {
+    /* one pass computes every position's k-mer code (~0: no valid k-mer ends
+     * there) with a rolling code; a k-mer ending at p is valid when the K
+     * bases p-K+1..p lie in one record and no break flag sits on p-K+2..p
+     * -- i.e. the run of bases since the last record start/break is at
+     * least K long. */
+    const uint32_t mask = (uint32_t)((1ull << (2 * K)) - 1);
+    uint32_t *code = malloc((d->len + 1) * sizeof(uint32_t));
     ix->off = calloc(NB + 1, sizeof(uint64_t));
-    uint64_t total = 0, rec, p;
-    for (rec = 0; rec < d->n; rec++)
-        for (p = d->start[rec]; p < d->start[rec + 1]; p++)
-            if (kmer_ok(d, p, d->start[rec])) { ix->off[kmer_code(d->seq + p + 1 - K) + 1]++; total++; }
-    for (uint64_t b = 0; b < NB; b++) ix->off[b + 1] += ix->off[b];
-    uint64_t *fill = malloc(NB * sizeof(uint64_t));
-    memcpy(fill, ix->off, NB * sizeof(uint64_t));
-    ix->pos = malloc((total + 1) * sizeof(uint32_t));
-    ix->sid = malloc((total + 1) * sizeof(uint32_t));
-    for (rec = d->n; rec-- > 0;) {
-        for (p = d->start[rec + 1]; p-- > d->start[rec];) {
-            if (!kmer_ok(d, p, d->start[rec])) continue;
-            uint32_t c = kmer_code(d->seq + p + 1 - K);
-            ix->pos[fill[c]] = (uint32_t)(p + 1);       /* pos = last base + 1 (IMSAME.c:247) */
-            ix->sid[fill[c]] = (uint32_t)rec;           /* s_id = current record (:249)     */
-            fill[c]++;
+    uint64_t total = 0;
+    for (uint64_t rec = 0; rec < d->n; rec++) {
+        uint32_t c = 0, run = 0;
+        for (uint64_t p = d->start[rec]; p < d->start[rec + 1]; p++) {
+            run = (p == d->start[rec] || brk_at(d, p)) ? 1 : run + 1;
+            c = ((c << 2) | (uint32_t)base_code(d->seq[p])) & mask;
+            code[p] = (run >= K) ? c : ~0u;
+            total += run >= K;
         }
     }
-    free(fill);
+    const int T = d->len > (1u << 22) ? 8 : 1;
+    ix_part part[8];
+    pthread_t th[8];
+    for (int pass = 0; pass < 2; pass++) {
+        if (pass == 1) {
+            for (uint64_t b = 0; b < NB; b++) ix->off[b + 1] += ix->off[b];
+            ix->pos = malloc((total + 1) * sizeof(uint32_t));
+            ix->sid = malloc((total + 1) * sizeof(uint32_t));
+        }
+        for (int t = 0; t < T; t++) {
+            part[t] = (ix_part){ d, code, ix, (uint32_t)((uint64_t)NB * t / T), (uint32_t)((uint64_t)NB * (t + 1) / T), pass };
+            pthread_create(&th[t], NULL, ix_part_run, &part[t]);
+        }
+        for (int t = 0; t < T; t++) pthread_join(th[t], NULL);
+    }
+    /* the scatter advanced off[c] to the end of bucket c = off[c+1]: shift back */
+    for (uint64_t b = NB; b > 0; b--) ix->off[b] = ix->off[b - 1];
+    ix->off[0] = 0;
+    free(code);
 }
 
 static void or_free_index(or_index *ix) { free(ix->off); free(ix->pos); free(ix->sid); }
@@ -348,8 +385,16 @@ typedef struct {
     uint64_t n_nw;
 } or_chunk;
 
+/* Test-speed option, off by default: skip the NW of a (read, record) pair
+ * already rejected for this read.  Results are identical (NW is pure,
+ * SURVEY Appendix A Q18); the reference recomputes, which makes long-read
+ * (C5) cases with hundreds of e-value passes per read take minutes. */
+static int g_memo_rejected;
+void or_set_memo_rejected(int on) { g_memo_rejected = on; }
+
 static void *scan_chunk(void *arg) {
     or_chunk *ch = arg;
+    uint64_t memo_read = ~0ull, nmemo = 0, capmemo = 0, *memo = NULL;
     const or_seqs *db = ch->db, *q = ch->q;
     const imsame_params *prm = ch->prm;
     nw_work w; memset(&w, 0, sizeof w);
@@ -377,7 +422,14 @@ static void *scan_chunk(void *arg) {
                 if (xl > prm->max_read_size || yl > prm->max_read_size) {
                     ch->status = IMSAME_E_READ_TOO_LONG; ch->err_read = r; ch->err_dbseq = s;
                     work_free(&w);
+                    free(memo);
                     return NULL;
+                }
+                if (g_memo_rejected) {
+                    if (memo_read != r) { memo_read = r; nmemo = 0; }
+                    uint64_t k = 0;
+                    while (k < nmemo && memo[k] != s) k++;
+                    if (k < nmemo) continue;
                 }
                 or_nw_out o;
                 nw_full(db->seq + db->start[s], xl, q->seq + q->start[r], yl, prm->igap, prm->egap, &w, &o);
@@ -398,6 +450,12 @@ static void *scan_chunk(void *arg) {
                         ch->texts[r] = t;
                     }
                     done = 1;
+                } else if (g_memo_rejected) {
+                    if (nmemo == capmemo) {
+                        capmemo = capmemo ? 2 * capmemo : 16;
+                        memo = realloc(memo, capmemo * sizeof *memo);
+                    }
+                    memo[nmemo++] = s;
                 }
             }
             if (!done) run--;
@@ -410,6 +468,7 @@ static void *scan_chunk(void *arg) {
         p++;
     }
     work_free(&w);
+    free(memo);
     return NULL;
 }
 

@@ -54,6 +54,9 @@ int or_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_start, uint6
 
 /* Reverse complement of a FASTA byte image (reverseComplement.c semantics). */
 int or_revcomp(const uint8_t *in, uint64_t in_len, uint8_t *out, uint64_t out_cap, uint64_t *out_len);
+/* test-speed option: skip re-running NW for (read, record) pairs already
+ * rejected for the read (identical results) */
+void or_set_memo_rejected(int on);
 
 void or_params_default(imsame_params *p);
 

@@ -73,6 +73,27 @@ def make_reads_arr(ref_seq, n, L, seed, sub=0.01, ins=0.0005, dele=0.0005, frac_
     return reads.reshape(-1), starts
 
 
+def make_long_reads_arr(ref_seq, n, L, seed, sub=0.05, ins=0.025, dele=0.025, frac_true=0.9, chunk=1000):
+    """C5's ONT-like long reads (5 % substitutions, 2.5 %
+    insertions, 2.5 % deletions), generated `chunk` reads at a time so
+    100k x 10 kbp stays within a few hundred MB of scratch.  Returns
+    (seq uint8[n*L], starts uint64[n])."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    pad = int(L * dele * 1.5) + 64                    # deletions consume source bases
+    out = np.empty((n, L), dtype=np.uint8)
+    for c0 in range(0, n, chunk):
+        m = min(chunk, n - c0)
+        is_true = rng.random(m) < frac_true
+        blk = ACGT[rng.integers(0, 4, (m, L), dtype=np.uint8)]
+        nt = int(is_true.sum())
+        if nt:
+            off = rng.integers(0, len(ref_seq) - (L + pad), nt)
+            idx = off[:, None] + np.arange(L + pad)[None, :]
+            blk[is_true] = _mutate_rows(rng, ref_seq[idx], L, sub, ins, dele)
+        out[c0:c0 + m] = blk
+    return out.reshape(-1), np.arange(0, n * L, L, dtype=np.uint64)
+
+
 def make_reads(ref_records, n, L, seed, sub=0.01, ins=0.0005, dele=0.0005, frac_true=0.9):
     cat = np.frombuffer("".join(ref_records).encode(), dtype=np.uint8)
     seq, starts = make_reads_arr(cat, n, L, seed, sub, ins, dele, frac_true)

@@ -235,3 +235,63 @@ def test_full_c2_reference_properties(dev, oracle):
     n = 1500
     rc, exp, _ = oracle.align(ref, rst, q[:int(qs[n])], qs[:n], None, 1)
     assert not _cmp(res[:n - 1], exp[:n - 1]), _cmp(res[:n - 1], exp[:n - 1])
+
+
+@pytest.fixture
+def oracle_memo(oracle):
+    """The oracle with its test-speed memo of rejected (read, record) pairs
+    (identical results): the reference re-runs NW for
+    every e-value-passing hit, hundreds per 10 kbp read."""
+    oracle.lib.or_set_memo_rejected(1)
+    yield oracle
+    oracle.lib.or_set_memo_rejected(0)
+
+
+@pytest.mark.timeout(300)
+def test_c3_reference_500mbp(dev, oracle_memo):
+    """BASELINE configs[2] per-GPU shard: 1.25M x 150 bp reads (10M / 8) vs
+    the 500 Mbp reference (250k records, 4 GB of CSR entries): oracle parity
+    on a prefix, path self-consistency and the accepted fraction on all."""
+    ref, rst = synth.make_reference_arr(500_000_000, 2_000, seed=43)
+    q, qs = synth.make_reads_arr(ref, 1_250_000, 150, seed=44)
+    dev.index(ref, rst)
+    dev.set_query(q, qs)
+    res, paths, st = dev.align(n_threads=1, want_paths=True)
+    acc = res["status"] == 1
+    assert acc.mean() > 0.85, acc.mean()
+    for k in np.flatnonzero(acc)[:1000]:
+        r = res[k]
+        s = int(r["db_seq"])
+        X = ref[int(rst[s]):int(rst[s + 1]) if s + 1 < len(rst) else len(ref)]
+        Y = q[int(qs[k]):int(qs[k]) + int(r["ylen"])]
+        _, ident = render(X.tobytes(), Y.tobytes(), r, paths[r["path_off"]:r["path_off"] + r["path_len"]])
+        assert ident == r["identities"]
+    n = 1000
+    rc, exp, _ = oracle_memo.align(ref, rst, q[:int(qs[n])], qs[:n], None, 1)
+    assert rc == 0
+    assert not _cmp(res[:n - 1], exp[:n - 1]), _cmp(res[:n - 1], exp[:n - 1])
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("rec_bp,cap", [(2_000, 10_001), (12_000, 12_001)], ids=["c5_2kbp_records", "c5_12kbp_records"])
+def test_c5_ont_long_reads_raised_cap(dev, oracle_memo, rec_bp, cap):
+    """BASELINE configs[4] shape: 10 kbp ONT-like reads (5 % sub, 2.5 % ins,
+    2.5 % del) with the raised MAX_READ_SIZE (SURVEY 8(c) iv).  Against the
+    C5 2 kbp records every candidate is rejected (coverage len/ylen < 0.5);
+    against 12 kbp records reads are accepted with 120M-cell matrices.  At
+    the stock cap the first e-value pass is the fatal size error."""
+    n = 16 if rec_bp == 2_000 else 10
+    ref, rst = synth.make_reference_arr(rec_bp * 300, rec_bp, seed=48)
+    q, qs = synth.make_long_reads_arr(ref, n, 10_000, seed=49)
+    dev.index(ref, rst)
+    dev.set_query(q, qs)
+    res, _, st = dev.align(n_threads=8, params=dev.params(max_read_size=cap))
+    rc, exp, _ = oracle_memo.align(ref, rst, q, qs, oracle_memo.params(max_read_size=cap), 8)
+    assert rc == 0
+    assert not _cmp(res, exp), _cmp(res, exp)
+    assert st.n_nw > 0
+    if rec_bp > 10_000:
+        assert (res["status"] == 1).sum() >= n // 2
+    _, _, st3 = dev.align(n_threads=8, allow_too_long=True)
+    rc3, _, er3 = oracle_memo.align(ref, rst, q, qs, None, 8)
+    assert rc3 == abi.IMSAME_E_READ_TOO_LONG and st3.err_read == er3
