@@ -75,6 +75,8 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=None,
                     help="reads in the CPU baseline sample (0: skip; default: the config's)")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-kind", choices=("auto", "port", "reference"), default="auto",
+                    help="auto: the compiled reference (oracle/_ref/IMSAME) when present, else the port")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "nw_traffic.json"))
     a = ap.parse_args()
     cfg = CONFIGS[a.config]
@@ -209,10 +211,57 @@ def cpu_baseline(dev, ref, rst, q, qs, a, params):
     dev.set_query(qv, qs[:n])
     got, _, _ = dev.align(0, n, n_threads=a.cpu_threads, params=params)
     same = int(np.all([exp[f] == got[f] for f in PARITY_FIELDS], axis=0).sum())
-    return {"value": round(n / secs, 1), "unit": "reads/s", "cores": a.cpu_threads, "kind": "port",
+    port = {"value": round(n / secs, 1), "unit": "reads/s", "cores": a.cpu_threads, "kind": "port",
             "sample": f"first {n} reads of the rank-0 shard as their own query, oracle/imsame_oracle.c "
                       f"-n_threads {a.cpu_threads}, alignment-phase wall {secs:.2f} s",
             "sample_reads_identical_to_gpu": same, "sample_reads_compared": n}
+    ref_bin = os.path.join(REPO, "oracle", "_ref", "IMSAME")
+    if a.cpu_kind == "port" or (a.cpu_kind == "auto" and not os.access(ref_bin, os.X_OK)):
+        return port
+    r = run_reference(ref_bin, ref, rst, qv, qs[:n], a.cpu_threads)
+    gpu_acc = int((got["status"] == 1).sum())
+    return {"value": round(n / r["align_s"], 1), "unit": "reads/s", "cores": a.cpu_threads, "kind": "reference",
+            "sample": f"first {n} reads of the rank-0 shard as their own query vs the same database, "
+                      f"IMSAME compiled from the reference sources (oracle/Makefile ref, gcc -O3) -n_threads "
+                      f"{a.cpu_threads}; alignment phase = process wall {r['wall_s']:.2f} s minus its single-threaded "
+                      f"setup phases {r['setup_s']:.2f} s = {r['align_s']:.2f} s",
+            "reference_accepted": r["accepted"], "gpu_accepted": gpu_acc,
+            "port": port}
+
+
+def run_reference(ref_bin, ref, rst, q, qs, threads):
+    """Run the compiled reference on FASTA files of the sample (test
+    infrastructure: the CPU baseline only).  Its timing lines use clock() --
+    CPU time summed over threads -- so the alignment phase is the process's
+    wall time minus its three single-threaded setup phases (quick table,
+    database + hash table, query; IMSAME.c:102,295,407), for which clock()
+    equals wall time.  Process start-up and the heap teardown
+    after the last line stay in, so this slightly overstates the phase."""
+    import re
+    import subprocess
+    import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        dbf, qf = os.path.join(td, "db.fa"), os.path.join(td, "q.fa")
+        b = ref.tobytes()
+        ends = rst[1:].tolist() + [len(ref)]
+        with open(dbf, "wb") as f:
+            for i, (s0, s1) in enumerate(zip(rst.tolist(), ends)):
+                rec = b[s0:s1]
+                f.write(b">ref_%d\n" % i + b"\n".join(rec[j:j + 80] for j in range(0, len(rec), 80)) + b"\n")
+        b = q.tobytes()
+        qe = qs[1:].tolist() + [len(q)]
+        with open(qf, "wb") as f:
+            f.write(b"".join(b">read_%d\n" % i + b[s0:s1] + b"\n" for i, (s0, s1) in enumerate(zip(qs.tolist(), qe))))
+        t0 = time.monotonic()
+        p = subprocess.run([ref_bin, "-db", dbf, "-query", qf, "-n_threads", str(threads)],
+                           stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=600)
+        wall = time.monotonic() - t0
+    out = p.stdout.decode(errors="replace")
+    setup = [float(x) for x in re.findall(r"(?:Initialization took|building took|Took) ([0-9.eE+-]+) seconds", out)]
+    acc = re.search(r"\[INFO\] (\d+) reads \(", out)
+    if p.returncode != 0 or len(setup) != 3 or acc is None:
+        raise RuntimeError(f"reference run failed (rc {p.returncode}): {out[-500:]}")
+    return {"align_s": wall - sum(setup), "wall_s": wall, "setup_s": sum(setup), "accepted": int(acc.group(1))}
 
 
 if __name__ == "__main__":

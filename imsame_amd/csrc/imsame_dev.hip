@@ -44,50 +44,61 @@ __global__ void mark_record_starts(const uint64_t *st, uint64_t n, uint64_t L, u
     if (k < n && st[k] < L) atomicOr(&brk[st[k] >> 5], 1u << (st[k] & 31));
 }
 
+// Grid-stride loops: a dispatch holds < 2^32 work-items, a database may
+// hold more bases.
+#define GRID_STRIDE(p, n) \
+    for (uint64_t p = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; p < (n); p += (uint64_t)gridDim.x * blockDim.x)
+
 // code of the 12-mer ending at base p, or ~0 when a reset lies in (p-11, p]
 __global__ void kmer_code_kernel(const uint8_t *seq, uint64_t L, const uint32_t *brk, uint32_t *codes,
                                  uint32_t *cnt) {
-    uint64_t p = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (p >= L) return;
-    uint32_t code = 0xFFFFFFFFu;
-    if (p >= IMSAME_FIXED_K - 1) {
-        const uint64_t b0 = p - (IMSAME_FIXED_K - 2);           // bits p-10 .. p
-        const uint64_t w = b0 >> 5;
-        const uint64_t win = ((uint64_t)brk[w] | ((uint64_t)brk[w + 1] << 32)) >> (b0 & 31);
-        if ((win & ((1u << (IMSAME_FIXED_K - 1)) - 1)) == 0) {
-            code = 0;
+    GRID_STRIDE(p, L) {
+        uint32_t code = 0xFFFFFFFFu;
+        if (p >= IMSAME_FIXED_K - 1) {
+            const uint64_t b0 = p - (IMSAME_FIXED_K - 2);           // bits p-10 .. p
+            const uint64_t w = b0 >> 5;
+            const uint64_t win = ((uint64_t)brk[w] | ((uint64_t)brk[w + 1] << 32)) >> (b0 & 31);
+            if ((win & ((1u << (IMSAME_FIXED_K - 1)) - 1)) == 0) {
+                code = 0;
 #pragma unroll
-            for (int k = IMSAME_FIXED_K - 1; k >= 0; --k) code = (code << 2) | base2(seq[p - k]);
-            atomicAdd(&cnt[code], 1u);
+                for (int k = IMSAME_FIXED_K - 1; k >= 0; --k) code = (code << 2) | base2(seq[p - k]);
+                atomicAdd(&cnt[code], 1u);
+            }
         }
+        codes[p] = code;
     }
-    codes[p] = code;
 }
 
-__global__ void kmer_scatter(const uint32_t *codes, uint64_t L, const uint32_t *off, uint32_t *fill,
+// Entry = {pos - start[record], record}: 8 bytes whatever the database size
+// (positions past 2^32 need no wider entry; records stay < 2^32 bases).
+// The reference's pos (last base + 1, IMSAME.c:247) is start[record] + x.
+__global__ void kmer_scatter(const uint32_t *codes, uint64_t L, const uint64_t *off, uint32_t *fill,
                              const uint64_t *st, uint64_t n_db, uint2 *ent) {
-    uint64_t p = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (p >= L) return;
-    const uint32_t c = codes[p];
-    if (c == 0xFFFFFFFFu) return;
-    uint64_t lo = 0, hi = n_db;                 // last record with start <= p
-    while (hi - lo > 1) { uint64_t m = (lo + hi) >> 1; if (st[m] <= p) lo = m; else hi = m; }
-    const uint32_t slot = off[c] + atomicAdd(&fill[c], 1u);
-    ent[slot] = make_uint2((uint32_t)(p + 1), (uint32_t)lo);   // pos = last base + 1 (IMSAME.c:247)
+    GRID_STRIDE(p, L) {
+        const uint32_t c = codes[p];
+        if (c == 0xFFFFFFFFu) continue;
+        uint64_t lo = 0, hi = n_db;             // last record with start <= p
+        while (hi - lo > 1) { uint64_t m = (lo + hi) >> 1; if (st[m] <= p) lo = m; else hi = m; }
+        const uint64_t slot = off[c] + atomicAdd(&fill[c], 1u);
+        ent[slot] = make_uint2((uint32_t)(p + 1 - st[lo]), (uint32_t)lo);
+    }
 }
+
+// records are contiguous and ascending, so descending pos = descending (record, x)
+__device__ __forceinline__ uint64_t ent_key(uint2 v) { return ((uint64_t)v.y << 32) | v.x; }
 
 // buckets in DESCENDING pos = the reference's LIFO chain order (IMSAME.c:255-276)
-__global__ void segsort_small(const uint32_t *off, uint2 *ent, uint32_t *big, uint32_t *nbig) {
+__global__ void segsort_small(const uint64_t *off, uint2 *ent, uint32_t *big, uint32_t *nbig) {
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= NBUCKETS) return;
-    const uint32_t lo = off[b], n = off[b + 1] - lo;
+    const uint64_t lo = off[b], n = off[b + 1] - lo;
     if (n < 2) return;
     if (n > 32) { big[atomicAdd(nbig, 1u)] = b; return; }
     uint2 *e = ent + lo;
     for (uint32_t i = 1; i < n; ++i) {
         uint2 v = e[i];
         uint32_t j = i;
-        while (j > 0 && e[j - 1].x < v.x) { e[j] = e[j - 1]; --j; }
+        while (j > 0 && ent_key(e[j - 1]) < ent_key(v)) { e[j] = e[j - 1]; --j; }
         e[j] = v;
     }
 }
@@ -101,25 +112,30 @@ __device__ void bitonic_desc(uint2 *s, uint32_t np) {
                 const uint32_t l = i ^ j;
                 if (l > i) {
                     const bool desc = (i & k) == 0;
-                    if ((s[i].x < s[l].x) == desc) { uint2 t = s[i]; s[i] = s[l]; s[l] = t; }
+                    if ((ent_key(s[i]) < ent_key(s[l])) == desc) { uint2 t = s[i]; s[i] = s[l]; s[l] = t; }
                 }
             }
             __syncthreads();
         }
 }
 
-__global__ void segsort_big(const uint32_t *off, uint2 *ent, const uint32_t *big) {
+// block-stride over the listed buckets: past ~1 Gbase nearly every bucket
+// is listed, and hbig blocks x 256 would overflow a dispatch's 2^32 items
+__global__ void segsort_big(const uint64_t *off, uint2 *ent, const uint32_t *big, uint32_t nbig) {
     __shared__ uint2 s[4096];
-    const uint32_t b = big[blockIdx.x];
-    const uint32_t lo = off[b], n = off[b + 1] - lo;
-    uint32_t np = 1;
-    while (np < n) np <<= 1;
-    if (np > 4096) return;                      // handled by segsort_huge
-    uint2 *e = ent + lo;
-    for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) s[i] = i < n ? e[i] : make_uint2(0u, 0u);
-    __syncthreads();
-    bitonic_desc(s, np);
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) e[i] = s[i];
+    for (uint32_t k = blockIdx.x; k < nbig; k += gridDim.x) {
+        const uint32_t b = big[k];
+        const uint64_t lo = off[b], n = off[b + 1] - lo;
+        uint32_t np = 1;
+        while (np < n) np <<= 1;
+        if (np > 4096) continue;                // handled by segsort_huge (uniform per block)
+        uint2 *e = ent + lo;
+        for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) s[i] = i < n ? e[i] : make_uint2(0u, 0u);
+        __syncthreads();
+        bitonic_desc(s, np);
+        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) e[i] = s[i];
+        __syncthreads();                        // s is reused by the next bucket
+    }
 }
 
 __global__ void segsort_huge(uint2 *e, uint32_t n, uint2 *scratch, uint32_t np) {
@@ -129,15 +145,16 @@ __global__ void segsort_huge(uint2 *e, uint32_t n, uint2 *scratch, uint32_t np) 
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) e[i] = scratch[i];
 }
 
-// exclusive scan of n u32 (1024 elements per block; recursive over block sums)
-__global__ void scan_blocks(const uint32_t *in, uint32_t *out, uint32_t *bsum, uint64_t n) {
-    __shared__ uint32_t s[1024];
+// exclusive scan of n values (1024 elements per block; recursive over block sums)
+template <class TI, class TO>
+__global__ void scan_blocks(const TI *in, TO *out, TO *bsum, uint64_t n) {
+    __shared__ TO s[1024];
     const uint64_t i = blockIdx.x * 1024ull + threadIdx.x;
-    const uint32_t v = i < n ? in[i] : 0;
+    const TO v = i < n ? (TO)in[i] : (TO)0;
     s[threadIdx.x] = v;
     __syncthreads();
     for (int o = 1; o < 1024; o <<= 1) {
-        const uint32_t t = threadIdx.x >= (uint32_t)o ? s[threadIdx.x - o] : 0;
+        const TO t = threadIdx.x >= (uint32_t)o ? s[threadIdx.x - o] : (TO)0;
         __syncthreads();
         s[threadIdx.x] += t;
         __syncthreads();
@@ -145,7 +162,8 @@ __global__ void scan_blocks(const uint32_t *in, uint32_t *out, uint32_t *bsum, u
     if (i < n) out[i] = s[threadIdx.x] - v;
     if (threadIdx.x == 1023) bsum[blockIdx.x] = s[1023];
 }
-__global__ void scan_add(uint32_t *out, const uint32_t *bpre, uint64_t n) {
+template <class T>
+__global__ void scan_add(T *out, const T *bpre, uint64_t n) {
     const uint64_t i = blockIdx.x * 1024ull + threadIdx.x;
     if (i < n) out[i] += bpre[blockIdx.x];
 }
@@ -274,17 +292,21 @@ extern "C" void imsame_dev_close(imsame_ctx *c) {
 
 static unsigned nblk(uint64_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
 
-// exclusive scan out[0..n) of in[0..n) (u32, wraps past 2^32: callers size for it)
-static int dev_scan(hipStream_t s, const uint32_t *in, uint32_t *out, uint64_t n) {
+// grid for a grid-stride kernel (a dispatch holds < 2^32 work-items)
+static unsigned gsblk(uint64_t n, unsigned b) { return (unsigned)std::min<uint64_t>((n + b - 1) / b, 1u << 20); }
+
+// exclusive scan out[0..n) of in[0..n) (TO wraps past its range: callers size for it)
+template <class TI, class TO>
+static int dev_scan(hipStream_t s, const TI *in, TO *out, uint64_t n) {
     if (n == 0) return 0;
     const uint64_t nb = (n + 1023) / 1024;
     DBuf bs, bp;
-    if (bs.ensure(nb * 4 + 16) || bp.ensure(nb * 4 + 16)) return IMSAME_E_OOM;
-    scan_blocks<<<(unsigned)nb, 1024, 0, s>>>(in, out, bs.as<uint32_t>(), n);
+    if (bs.ensure(nb * sizeof(TO) + 16) || bp.ensure(nb * sizeof(TO) + 16)) return IMSAME_E_OOM;
+    scan_blocks<TI, TO><<<(unsigned)nb, 1024, 0, s>>>(in, out, bs.as<TO>(), n);
     if (nb > 1) {
-        int rc = dev_scan(s, bs.as<uint32_t>(), bp.as<uint32_t>(), nb);
+        int rc = dev_scan<TO, TO>(s, bs.as<TO>(), bp.as<TO>(), nb);
         if (rc) return rc;
-        scan_add<<<(unsigned)nb, 1024, 0, s>>>(out, bp.as<uint32_t>(), n);
+        scan_add<TO><<<(unsigned)nb, 1024, 0, s>>>(out, bp.as<TO>(), n);
     }
     HIPCHK(hipStreamSynchronize(s));     // the level buffers are freed on return
     return 0;
@@ -293,7 +315,7 @@ static int dev_scan(hipStream_t s, const uint32_t *in, uint32_t *out, uint64_t n
 extern "C" int imsame_dev_index(imsame_ctx *c, const uint8_t *db_seq, uint64_t db_len, const uint64_t *db_start,
                                 uint64_t n_db, const uint8_t *db_brk) {
     if (!c || (db_len && !db_seq) || (n_db && !db_start)) return IMSAME_E_ARG;
-    if (db_len >= 0xFFFFFFF0ull || n_db >= 0xFFFFFFF0ull) return IMSAME_E_ARG;   // u32 positions
+    if (n_db >= 0xFFFFFFF0ull) return IMSAME_E_ARG;              // u32 record ids
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     c->have_index = false;
@@ -301,11 +323,13 @@ extern "C" int imsame_dev_index(imsame_ctx *c, const uint8_t *db_seq, uint64_t d
     c->h_db_start.assign(db_start, db_start + n_db);
     c->h_db_start.push_back(db_len);
     c->max_rec = 0;
-    for (uint64_t k = 0; k < n_db; ++k)
-        c->max_rec = (uint32_t)std::max<uint64_t>(c->max_rec, c->h_db_start[k + 1] - c->h_db_start[k]);
+    uint64_t max_rec = 0;
+    for (uint64_t k = 0; k < n_db; ++k) max_rec = std::max<uint64_t>(max_rec, c->h_db_start[k + 1] - c->h_db_start[k]);
+    if (max_rec >= 0xFFFFFFF0ull) return IMSAME_E_ARG;           // record-relative u32 entry positions
+    c->max_rec = (uint32_t)max_rec;
     const uint64_t nw = db_len / 32 + 2;
     if (c->db.ensure(db_len + 64) || c->db_start.ensure((n_db + 1) * 8) || c->brk.ensure(nw * 4) ||
-        c->codes.ensure((db_len + 1) * 4) || c->off.ensure(((uint64_t)NBUCKETS + 1) * 4) ||
+        c->codes.ensure((db_len + 1) * 4) || c->off.ensure(((uint64_t)NBUCKETS + 1) * 8) ||
         c->fill.ensure((uint64_t)NBUCKETS * 4) || c->big.ensure((uint64_t)NBUCKETS * 4))
         return IMSAME_E_OOM;
     if (db_len) HIPCHK(hipMemcpyAsync(c->db.p, db_seq, db_len, hipMemcpyHostToDevice, s));
@@ -315,44 +339,46 @@ extern "C" int imsame_dev_index(imsame_ctx *c, const uint8_t *db_seq, uint64_t d
     if (n_db) mark_record_starts<<<nblk(n_db, 256), 256, 0, s>>>(c->db_start.as<uint64_t>(), n_db, db_len,
                                                                    c->brk.as<uint32_t>());
     HIPCHK(hipMemsetAsync(c->fill.p, 0, (uint64_t)NBUCKETS * 4, s));
-    if (db_len) kmer_code_kernel<<<nblk(db_len, 256), 256, 0, s>>>(c->db.as<uint8_t>(), db_len, c->brk.as<uint32_t>(),
+    if (db_len) kmer_code_kernel<<<gsblk(db_len, 256), 256, 0, s>>>(c->db.as<uint8_t>(), db_len, c->brk.as<uint32_t>(),
                                                                   c->codes.as<uint32_t>(), c->fill.as<uint32_t>());
     // exclusive scan of the counts -> off[0..NB], off[NB] = total
-    uint32_t total = 0;
+    uint64_t total = 0;
     {
         DBuf cnt;
         if (cnt.ensure(((uint64_t)NBUCKETS + 1) * 4)) return IMSAME_E_OOM;
         HIPCHK(hipMemsetAsync(cnt.p, 0, ((uint64_t)NBUCKETS + 1) * 4, s));
         HIPCHK(hipMemcpyAsync(cnt.p, c->fill.p, (uint64_t)NBUCKETS * 4, hipMemcpyDeviceToDevice, s));
-        int rc = dev_scan(s, cnt.as<uint32_t>(), c->off.as<uint32_t>(), (uint64_t)NBUCKETS + 1);
+        int rc = dev_scan<uint32_t, uint64_t>(s, cnt.as<uint32_t>(), c->off.as<uint64_t>(), (uint64_t)NBUCKETS + 1);
         if (rc) return rc;
-        HIPCHK(hipMemcpyAsync(&total, c->off.as<uint32_t>() + NBUCKETS, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(&total, c->off.as<uint64_t>() + NBUCKETS, 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         cnt.release();
     }
     c->n_ent = total;
-    if (c->ent.ensure(((uint64_t)total + 1) * 8)) return IMSAME_E_OOM;
+    if (c->ent.ensure((total + 1) * 8)) return IMSAME_E_OOM;
     HIPCHK(hipMemsetAsync(c->fill.p, 0, (uint64_t)NBUCKETS * 4, s));
-    if (db_len) kmer_scatter<<<nblk(db_len, 256), 256, 0, s>>>(c->codes.as<uint32_t>(), db_len, c->off.as<uint32_t>(),
+    if (db_len) kmer_scatter<<<gsblk(db_len, 256), 256, 0, s>>>(c->codes.as<uint32_t>(), db_len, c->off.as<uint64_t>(),
                                                               c->fill.as<uint32_t>(), c->db_start.as<uint64_t>(), n_db,
                                                               c->ent.as<uint2>());
     uint32_t *nbig = c->fill.as<uint32_t>();       // fill is free again: reuse as a counter
     HIPCHK(hipMemsetAsync(nbig, 0, 4, s));
-    segsort_small<<<nblk(NBUCKETS, 256), 256, 0, s>>>(c->off.as<uint32_t>(), c->ent.as<uint2>(),
+    segsort_small<<<nblk(NBUCKETS, 256), 256, 0, s>>>(c->off.as<uint64_t>(), c->ent.as<uint2>(),
                                                       c->big.as<uint32_t>(), nbig);
     uint32_t hbig = 0;
     HIPCHK(hipMemcpyAsync(&hbig, nbig, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     if (hbig) {
-        segsort_big<<<hbig, 256, 0, s>>>(c->off.as<uint32_t>(), c->ent.as<uint2>(), c->big.as<uint32_t>());
+        segsort_big<<<std::min<uint32_t>(hbig, 1u << 16), 256, 0, s>>>(c->off.as<uint64_t>(), c->ent.as<uint2>(),
+                                                                      c->big.as<uint32_t>(), hbig);
         // buckets beyond 4096 entries (repeats): one block each, padded global scratch
-        std::vector<uint32_t> bigs(hbig), offs(NBUCKETS + 1);
+        std::vector<uint32_t> bigs(hbig);
+        std::vector<uint64_t> offs(NBUCKETS + 1);
         HIPCHK(hipMemcpyAsync(bigs.data(), c->big.p, (uint64_t)hbig * 4, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipMemcpyAsync(offs.data(), c->off.p, ((uint64_t)NBUCKETS + 1) * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(offs.data(), c->off.p, ((uint64_t)NBUCKETS + 1) * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         DBuf scr;
         for (uint32_t b : bigs) {
-            const uint32_t nb = offs[b + 1] - offs[b];
+            const uint32_t nb = (uint32_t)(offs[b + 1] - offs[b]);
             uint32_t np = 1;
             while (np < nb) np <<= 1;
             if (np <= 4096) continue;
@@ -551,7 +577,7 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
         SeedLaunch S;
         S.db = c->db.as<uint8_t>(); S.db_start = c->db_start.as<uint64_t>(); S.n_db = c->n_db; S.db_len = c->db_len;
         S.q = c->q.as<uint8_t>(); S.q_start = c->q_start.as<uint64_t>(); S.n_q = c->n_q; S.q_len = c->q_len;
-        S.off = c->off.as<uint32_t>(); S.ent = c->ent.as<uint2>();
+        S.off = c->off.as<uint64_t>(); S.ent = c->ent.as<uint2>();
         S.active = act; S.n_active = nact;
         S.read_from = read_from;
         S.T = n_threads_semantic ? n_threads_semantic : 1;

@@ -19,7 +19,7 @@ __device__ __forceinline__ uint32_t base2(uint32_t c) { return ((c >> 1) ^ (c >>
 struct SeedLaunch {
     const uint8_t *db; const uint64_t *db_start; uint64_t n_db, db_len;
     const uint8_t *q;  const uint64_t *q_start;  uint64_t n_q, q_len;
-    const uint32_t *off; const uint2 *ent;        // CSR, each bucket in descending pos
+    const uint64_t *off; const uint2 *ent;        // CSR {pos - record start, record}, buckets in descending pos
     const uint32_t *active; uint32_t n_active;
     uint64_t read_from, rpt, T;
     uint64_t *cur_p; uint32_t *cur_h; uint32_t *memo; uint8_t *nmemo; uint8_t *rstat;
@@ -165,8 +165,8 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint
         } else {
             code = ((code << 2) | base2(S.q[p])) & (NBUCKETS - 1);
         }
-        const uint32_t lo = S.off[code], hi = S.off[code + 1];
-        for (uint32_t e = lo + h; e < hi; ++e, ++h) {
+        const uint64_t lo = S.off[code], hi = S.off[code + 1];
+        for (uint64_t e = lo + h; e < hi; ++e, ++h) {
             const uint2 ent = S.ent[e];
             const uint32_t sid = ent.y;
             bool skip = false;
@@ -183,7 +183,7 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint
             const int64_t xs = (int64_t)S.db_start[sid];
             const int64_t xe = (sid == S.n_db - 1) ? (int64_t)S.db_len : (int64_t)S.db_start[sid + 1] - 1;
             ++hits;
-            const uint64_t raw = ungapped_raw(S.db, S.q, ent.x, (int64_t)p + 1, xs, xe, ys, ye,
+            const uint64_t raw = ungapped_raw(S.db, S.q, xs + ent.x, (int64_t)p + 1, xs, xe, ys, ye,
                                               (int64_t)S.db_len, (int64_t)S.q_len);
             if (mraw != ~0ull && raw >= mraw) {                      // e < min_e (:139)
                 const uint64_t xlen = S.db_start[sid + 1] - S.db_start[sid];
@@ -295,8 +295,8 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
         if (!done && pw < up_to) {
             const uint32_t need = spec - ne;
             const uint32_t code = kmer_code_at(S.q, pw);
-            const uint32_t wbase = S.off[code], hi = S.off[code + 1];
-            for (uint32_t e = wbase + (wl == 0 ? h : 0u); e < hi; ++e) {
+            const uint64_t wbase = S.off[code], hi = S.off[code + 1];
+            for (uint64_t e = wbase + (wl == 0 ? h : 0u); e < hi; ++e) {
                 const uint2 ent = S.ent[e];
                 const uint32_t sid = ent.y;
                 bool skip = emit_has(emit, ne, sid);
@@ -306,13 +306,13 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
                 ++ev;
                 const int64_t xs = (int64_t)S.db_start[sid];
                 const int64_t xe = (sid == S.n_db - 1) ? (int64_t)S.db_len : (int64_t)S.db_start[sid + 1] - 1;
-                const uint64_t raw = ungapped_raw(S.db, S.q, ent.x, (int64_t)pw + 1, xs, xe, ys, ye,
+                const uint64_t raw = ungapped_raw(S.db, S.q, xs + ent.x, (int64_t)pw + 1, xs, xe, ys, ye,
                                                   (int64_t)S.db_len, (int64_t)S.q_len);
                 if (mraw != ~0ull && raw >= mraw) {                      // e < min_e (:139)
                     const uint64_t xlen = S.db_start[sid + 1] - S.db_start[sid];
                     const bool bad = xlen > S.max_rs || ylen > S.max_rs;   // terror (:155) if reached
-                    lst[nl++] = make_uint2(sid, (e - wbase) | (bad ? 0x80000000u : 0u));
-                    last_rel = e - wbase;
+                    lst[nl++] = make_uint2(sid, (uint32_t)(e - wbase) | (bad ? 0x80000000u : 0u));
+                    last_rel = (uint32_t)(e - wbase);
                     if (bad || nl == need) { full = true; break; }
                 }
             }

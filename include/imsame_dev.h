@@ -127,7 +127,11 @@ const char *imsame_strerror(int code);
  *   db_start : n_db record starts (IMSAME.c:200)
  *   db_brk   : optional bitmap, bit p (LSB-first) = k-mer reset before base p
  *              (non-ACGT, non-'\n' byte: IMSAME.c:229-231); record starts are
- *              resets implicitly.  NULL = none besides record starts. */
+ *              resets implicitly.  NULL = none besides record starts.
+ * Sizes: db_len is u64 (databases past 4 Gbases index with 8-byte entries
+ * {pos - record start, record}); n_db and each record's length must be
+ * below 2^32 - 16 (IMSAME_E_ARG).  HBM: db_len x 5 B during the build,
+ * plus 8 B per k-mer and 128 MB of bucket offsets. */
 int imsame_dev_index(imsame_ctx *ctx, const uint8_t *db_seq, uint64_t db_len,
                      const uint64_t *db_start, uint64_t n_db, const uint8_t *db_brk);
 

@@ -20,6 +20,7 @@
 #include <string.h>
 #include <math.h>
 #include <pthread.h>
+#include <unistd.h>
 #include <time.h>
 #include <inttypes.h>
 #include "imsame_oracle.h"
@@ -95,7 +96,8 @@ static void or_free_seqs(or_seqs *s) {
  * descending position order. */
 typedef struct {
     uint64_t *off;       /* NB+1 */
-    uint32_t *pos, *sid;
+    uint64_t *pos;       /* reference pos (u64: databases past 4 Gbases) */
+    uint32_t *sid;
 } or_index;
 
 static int brk_at(const or_seqs *d, uint64_t b) { return d->brk ? (d->brk[b >> 3] >> (b & 7)) & 1 : 0; }
@@ -106,70 +108,77 @@ static uint32_t kmer_code(const uint8_t *s) {
     return c;
 }
 
-/* Count and scatter run in parallel over disjoint bucket ranges: every
- * thread reads the whole code array in order but only touches its own
- * buckets, so each bucket is still filled in descending position. */
-typedef struct { const or_seqs *d; const uint32_t *code; or_index *ix; uint32_t lo, hi; int pass; } ix_part;
+/* The index build splits the database by record ranges: thread t computes
+ * the rolling codes of its records and counts its k-mers per bucket; bucket
+ * c then gets, per thread, a fill cursor that leaves room for every later
+ * range's entries first (descending position = higher ranges first), and
+ * each thread scatters its own positions in descending order.  Every pass
+ * is O(len / T). */
+typedef struct { const or_seqs *d; uint32_t *code; uint64_t *cnt; or_index *ix; uint64_t lo, hi, total; int pass; } ix_part;
 
 static void *ix_part_run(void *arg) {
     ix_part *t = arg;
     const or_seqs *d = t->d;
     if (t->pass == 0) {
-        for (uint64_t p = 0; p < d->len; p++) {
-            const uint32_t c = t->code[p];
-            if (c >= t->lo && c < t->hi) t->ix->off[c + 1]++;
+        const uint32_t mask = (uint32_t)((1ull << (2 * K)) - 1);
+        for (uint64_t rec = t->lo; rec < t->hi; rec++) {
+            uint32_t c = 0, run = 0;
+            for (uint64_t p = d->start[rec]; p < d->start[rec + 1]; p++) {
+                run = (p == d->start[rec] || brk_at(d, p)) ? 1 : run + 1;
+                c = ((c << 2) | (uint32_t)base_code(d->seq[p])) & mask;
+                t->code[p] = (run >= K) ? c : ~0u;
+                if (run >= K) { t->cnt[c]++; t->total++; }
+            }
         }
     } else {
-        uint64_t *fill = t->ix->off;            /* off[c] advances to the bucket end */
-        for (uint64_t rec = d->n; rec-- > 0;)
+        uint64_t *fill = t->cnt;                 /* this range's cursor per bucket */
+        for (uint64_t rec = t->hi; rec-- > t->lo;)
             for (uint64_t p = d->start[rec + 1]; p-- > d->start[rec];) {
                 const uint32_t c = t->code[p];
-                if (c < t->lo || c >= t->hi) continue;
-                t->ix->pos[fill[c]] = (uint32_t)(p + 1);   /* pos = last base + 1 (IMSAME.c:247) */
-                t->ix->sid[fill[c]] = (uint32_t)rec;       /* s_id = current record (:249)     */
+                if (c == ~0u) continue;
+                t->ix->pos[fill[c]] = p + 1;             /* pos = last base + 1 (IMSAME.c:247) */
+                t->ix->sid[fill[c]] = (uint32_t)rec;     /* s_id = current record (:249)     */
                 fill[c]++;
             }
     }
     return NULL;
 }
 
+#define IX_THREADS 16
+
 static void or_build_index(const or_seqs *d, or_index *ix) {
-    /* one pass computes every position's k-mer code (~0: no valid k-mer ends
-     * there) with a rolling code; a k-mer ending at p is valid when the K
-     * bases p-K+1..p lie in one record and no break flag sits on p-K+2..p
-     * -- i.e. the run of bases since the last record start/break is at
-     * least K long. */
-    const uint32_t mask = (uint32_t)((1ull << (2 * K)) - 1);
+    /* a k-mer ending at p is valid when the K bases p-K+1..p lie in one
+     * record and no break flag sits on p-K+2..p -- i.e. the run of bases
+     * since the last record start/break is at least K long. */
     uint32_t *code = malloc((d->len + 1) * sizeof(uint32_t));
     ix->off = calloc(NB + 1, sizeof(uint64_t));
+    const long ncpu = sysconf(_SC_NPROCESSORS_ONLN);
+    int T = d->len > (1u << 22) ? (int)(ncpu < 1 ? 1 : ncpu > IX_THREADS ? IX_THREADS : ncpu) : 1;
+    if (d->n > 0 && (uint64_t)T > d->n) T = (int)d->n;
+    pthread_t th[IX_THREADS];
+    ix_part part[IX_THREADS];
     uint64_t total = 0;
-    for (uint64_t rec = 0; rec < d->n; rec++) {
-        uint32_t c = 0, run = 0;
-        for (uint64_t p = d->start[rec]; p < d->start[rec + 1]; p++) {
-            run = (p == d->start[rec] || brk_at(d, p)) ? 1 : run + 1;
-            c = ((c << 2) | (uint32_t)base_code(d->seq[p])) & mask;
-            code[p] = (run >= K) ? c : ~0u;
-            total += run >= K;
-        }
-    }
-    const int T = d->len > (1u << 22) ? 8 : 1;
-    ix_part part[8];
-    pthread_t th[8];
     for (int pass = 0; pass < 2; pass++) {
         if (pass == 1) {
-            for (uint64_t b = 0; b < NB; b++) ix->off[b + 1] += ix->off[b];
-            ix->pos = malloc((total + 1) * sizeof(uint32_t));
+            for (uint64_t c = 0; c < NB; c++) {
+                uint64_t n = 0;
+                for (int t = 0; t < T; t++) n += part[t].cnt[c];
+                ix->off[c + 1] = ix->off[c] + n;
+                uint64_t run = ix->off[c];
+                for (int t = T; t-- > 0;) { const uint64_t k = part[t].cnt[c]; part[t].cnt[c] = run; run += k; }
+            }
+            for (int t = 0; t < T; t++) total += part[t].total;
+            ix->pos = malloc((total + 1) * sizeof(uint64_t));
             ix->sid = malloc((total + 1) * sizeof(uint32_t));
         }
         for (int t = 0; t < T; t++) {
-            part[t] = (ix_part){ d, code, ix, (uint32_t)((uint64_t)NB * t / T), (uint32_t)((uint64_t)NB * (t + 1) / T), pass };
+            if (pass == 0) part[t] = (ix_part){ d, code, calloc(NB, sizeof(uint64_t)), ix, d->n * t / T, d->n * (t + 1) / T, 0, 0 };
+            part[t].pass = pass;
             pthread_create(&th[t], NULL, ix_part_run, &part[t]);
         }
         for (int t = 0; t < T; t++) pthread_join(th[t], NULL);
     }
-    /* the scatter advanced off[c] to the end of bucket c = off[c+1]: shift back */
-    for (uint64_t b = NB; b > 0; b--) ix->off[b] = ix->off[b - 1];
-    ix->off[0] = 0;
+    for (int t = 0; t < T; t++) free(part[t].cnt);
     free(code);
 }
 
@@ -529,9 +538,16 @@ int or_align(const uint8_t *dbs, uint64_t db_len, const uint64_t *db_start, uint
     for (uint64_t s = 0; s < n_db; s++)
         if (db.start[s] < db_len) db.brk[db.start[s] >> 3] |= (uint8_t)(1u << (db.start[s] & 7));
     or_index ix;
+    struct timespec t0, t1, t2;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
     or_build_index(&db, &ix);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
     uint64_t er = 0, es = 0;
     int st = run_chunks(&db, &q, &ix, prm, T, res, NULL, &er, &es, NULL, 0);
+    clock_gettime(CLOCK_MONOTONIC, &t2);
+    if (getenv("OR_TIMING"))
+        fprintf(stderr, "[oracle] index %.2f s, align %.2f s\n", (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec),
+                (t2.tv_sec - t1.tv_sec) + 1e-9 * (t2.tv_nsec - t1.tv_nsec));
     if (err_read) *err_read = er;
     or_free_index(&ix);
     free(db.start); free(q.start); free(db.brk);

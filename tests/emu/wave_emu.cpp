@@ -100,7 +100,7 @@ extern "C" int emu_nw_pairs(const uint8_t *xs, const uint64_t *x_start, const ui
 // host CSR with the device index's semantics (imsame_dev.hip: kmer_code_kernel,
 // kmer_scatter, segsort): buckets in descending pos
 static void build_csr(const uint8_t *db, uint64_t L, const uint64_t *dbs, uint64_t n_db, const uint8_t *brk_in,
-                      std::vector<uint32_t> &off, std::vector<uint2> &ent) {
+                      std::vector<uint64_t> &off, std::vector<uint2> &ent) {
     std::vector<uint32_t> brk(L / 32 + 2, 0);
     if (brk_in) for (uint64_t b = 0; b < (L + 7) / 8; ++b) brk[b / 4] |= (uint32_t)brk_in[b] << (8 * (b % 4));
     for (uint64_t s = 0; s < n_db; ++s) if (dbs[s] < L) brk[dbs[s] >> 5] |= 1u << (dbs[s] & 31);
@@ -117,12 +117,12 @@ static void build_csr(const uint8_t *db, uint64_t L, const uint64_t *dbs, uint64
     }
     for (uint32_t b = 0; b < NBUCKETS; ++b) off[b + 1] += off[b];
     ent.assign(off[NBUCKETS] + 1, uint2{0, 0});
-    std::vector<uint32_t> fill(off.begin(), off.end() - 1);
+    std::vector<uint64_t> fill(off.begin(), off.end() - 1);
     for (uint64_t p = L; p-- > 0;) {          // descending positions
         if (code[p] == 0xFFFFFFFFu) continue;
         uint64_t lo = 0, hi = n_db;
         while (hi - lo > 1) { uint64_t m = (lo + hi) / 2; if (dbs[m] <= p) lo = m; else hi = m; }
-        ent[fill[code[p]]++] = uint2{(uint32_t)(p + 1), (uint32_t)lo};
+        ent[fill[code[p]]++] = uint2{(uint32_t)(p + 1 - dbs[lo]), (uint32_t)lo};
     }
 }
 
@@ -139,7 +139,7 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
     if (q_len) memcpy(qpad.data(), q, q_len);
     db = (const uint8_t *)dbpad.data();
     q = (const uint8_t *)qpad.data();
-    std::vector<uint32_t> off;
+    std::vector<uint64_t> off;
     std::vector<uint2> ent;
     build_csr(db, db_len, dbs.data(), n_db, db_brk, off, ent);
     uint32_t max_rec = 0, ymax = 0;

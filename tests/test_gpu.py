@@ -295,3 +295,32 @@ def test_c5_ont_long_reads_raised_cap(dev, oracle_memo, rec_bp, cap):
     _, _, st3 = dev.align(n_threads=8, allow_too_long=True)
     rc3, _, er3 = oracle_memo.align(ref, rst, q, qs, None, 8)
     assert rc3 == abi.IMSAME_E_READ_TOO_LONG and st3.err_read == er3
+
+
+@pytest.mark.timeout(600)
+def test_wide_database_past_4_gbases(oracle_memo):
+    """a 4.4 Gbase database (2.2M records of 2 kbp), past
+    the 2^32 positions a u32 index holds.  Reads come from the last 150 Mbp,
+    so their seeds, records and NW rows lie on both sides of 2^32.  Oracle
+    parity (u64 positions) on every read; path self-consistency."""
+    total = 4_400_000_000
+    ref, rst = synth.make_reference_arr(total, 2_000, seed=50)
+    tail = total - 150_000_000
+    q, qs = synth.make_reads_arr(ref[tail:], 1_500, 150, seed=51)
+    with Device(0) as d:
+        d.index(ref, rst)
+        d.set_query(q, qs)
+        res, paths, st = d.align(n_threads=1, want_paths=True)
+    acc = res["status"] == 1
+    assert acc.mean() > 0.85, acc.mean()
+    assert (rst[res["db_seq"][acc]] >= 2 ** 32).sum() > 500       # records past 2^32 found
+    for k in np.flatnonzero(acc)[:300]:
+        r = res[k]
+        s = int(r["db_seq"])
+        X = ref[int(rst[s]):int(rst[s + 1]) if s + 1 < len(rst) else len(ref)]
+        Y = q[int(qs[k]):int(qs[k]) + int(r["ylen"])]
+        _, ident = render(X.tobytes(), Y.tobytes(), r, paths[r["path_off"]:r["path_off"] + r["path_len"]])
+        assert ident == r["identities"]
+    rc, exp, _ = oracle_memo.align(ref, rst, q, qs, None, 1)
+    assert rc == 0
+    assert not _cmp(res, exp), _cmp(res, exp)
