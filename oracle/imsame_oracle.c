@@ -152,7 +152,8 @@ static void or_build_index(const or_seqs *d, or_index *ix) {
      * since the last record start/break is at least K long. */
     uint32_t *code = malloc((d->len + 1) * sizeof(uint32_t));
     ix->off = calloc(NB + 1, sizeof(uint64_t));
-    const long ncpu = sysconf(_SC_NPROCESSORS_ONLN);
+    const char *th_env = getenv("OR_INDEX_THREADS");     /* tests: force a thread count */
+    const long ncpu = th_env ? atol(th_env) : sysconf(_SC_NPROCESSORS_ONLN);
     int T = d->len > (1u << 22) ? (int)(ncpu < 1 ? 1 : ncpu > IX_THREADS ? IX_THREADS : ncpu) : 1;
     if (d->n > 0 && (uint64_t)T > d->n) T = (int)d->n;
     pthread_t th[IX_THREADS];
@@ -484,6 +485,9 @@ static void *scan_chunk(void *arg) {
 /* wall time of the last alignment phase (threads only, no loading/index) */
 static double g_align_seconds;
 double or_last_align_seconds(void) { return g_align_seconds; }
+/* NW calls of the last or_align (distinct pairs when the rejected-pair memo is on) */
+static uint64_t g_last_nw;
+uint64_t or_last_nw(void) { return g_last_nw; }
 
 /* Partition, IMSAME.c:414,430-452: rpt = floor(n/T); chunk i = [i*rpt,(i+1)*rpt),
  * the last chunk runs to n. */
@@ -543,7 +547,7 @@ int or_align(const uint8_t *dbs, uint64_t db_len, const uint64_t *db_start, uint
     or_build_index(&db, &ix);
     clock_gettime(CLOCK_MONOTONIC, &t1);
     uint64_t er = 0, es = 0;
-    int st = run_chunks(&db, &q, &ix, prm, T, res, NULL, &er, &es, NULL, 0);
+    int st = run_chunks(&db, &q, &ix, prm, T, res, NULL, &er, &es, &g_last_nw, 0);
     clock_gettime(CLOCK_MONOTONIC, &t2);
     if (getenv("OR_TIMING"))
         fprintf(stderr, "[oracle] index %.2f s, align %.2f s\n", (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec),

@@ -68,3 +68,39 @@ def test_revcomp_match_reference(oracle):
         data = open(os.path.join(d, n + ".in"), "rb").read()
         exp = open(os.path.join(d, n + ".out"), "rb").read()
         assert oracle.revcomp(data) == exp, n
+
+
+REF_BIN = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref", "IMSAME")
+
+
+@pytest.mark.skipif(not os.access(REF_BIN, os.X_OK), reason="oracle/_ref not built (needs /root/reference)")
+def test_bench_reference_baseline_leg(oracle):
+    """bench.py's CPU baseline runs the compiled reference on FASTA files of
+    the sample: its accepted count equals the oracle's on the same input and
+    the alignment-phase time it derives is positive and below the wall."""
+    import bench
+    from tests import synth
+    ref, rst = synth.make_reference_arr(2_000_000, 2_000, seed=5)
+    q, qs = synth.make_reads_arr(ref, 1_500, 150, seed=6)
+    r = bench.run_reference(REF_BIN, ref, rst, q, qs, 3)
+    rc, exp, _ = oracle.align(ref, rst, q, qs, None, 3)
+    assert rc == 0
+    assert r["accepted"] == int((exp["status"] == 1).sum())
+    assert 0 < r["align_s"] < r["wall_s"]
+
+
+def test_parallel_index_build_matches_serial(oracle, monkeypatch):
+    """The oracle's index build splits the database by record ranges above
+    4 Mbases (count, per-range cursors, descending scatter): every bucket must
+    keep the serial build's descending-position order, so per-read results
+    (which depend on the visiting order) are identical for 1 and 7 threads."""
+    from tests import synth
+    ref, rst = synth.make_reference_arr(6_000_000, 1_000, seed=8)
+    q, qs = synth.make_reads_arr(ref, 3_000, 150, seed=9)
+    out = {}
+    for t in ("1", "7"):
+        monkeypatch.setenv("OR_INDEX_THREADS", t)
+        rc, out[t], _ = oracle.align(ref, rst, q, qs, None, 2)
+        assert rc == 0
+    assert (out["1"]["status"] == 1).sum() > 2_500
+    assert np.array_equal(out["1"], out["7"])
