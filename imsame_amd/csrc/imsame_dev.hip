@@ -569,8 +569,6 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
     const uint32_t short_y = std::min<uint32_t>(ycap, NW_W / 2);
     uint32_t nact = n;
     uint32_t *act = c->act0.as<uint32_t>(), *nxt = c->act1.as<uint32_t>();
-    uint64_t nw_ms_launch_sum = 0;
-    (void)nw_ms_launch_sum;
     while (nact) {
         st.rounds++;
         HIPCHK(hipMemsetAsync(ctr + C_NCAND, 0, 3 * 8, s));     // NCAND, NCAND2, NNEXT
@@ -661,8 +659,7 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
     st.nw_cells = hc[C_CELLS];
     st.n_accepted = hc[C_NACC];
     st.nw_launch_ms = st.nw_launches ? st.ms_nw / st.nw_launches : 0;
-    st.nw_bytes = 2 * st.nw_cells;       // traceback floor; sequences added below
-    st.nw_bytes += 0;
+    st.nw_bytes = 2 * st.nw_cells;       // 2 B/cell traceback floor; bench.py adds xlen + ylen per NW
     int ret = IMSAME_OK;
     if (hc[C_ERR] != ~0ull) {
         st.err_read = hc[C_ERR] >> 32; st.err_dbseq = hc[C_ERR] & 0xFFFFFFFFull;

@@ -104,7 +104,7 @@ typedef struct imsame_stats {
     double   ms_total;      /* wall time of imsame_dev_align          */
     double   nw_launch_ms;  /* average NW kernel launch duration      */
     uint64_t nw_launches;
-    uint64_t nw_bytes;      /* algorithmic bytes moved by NW launches */
+    uint64_t nw_bytes;      /* 2 B per NW cell (traceback floor) */
 } imsame_stats;
 
 typedef struct imsame_ctx imsame_ctx;
