@@ -554,7 +554,7 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
     // speculation: round 1 emits one candidate per read (most reads accept
     // it); later rounds emit up to SPEC_MAX, bounded by the candidate buffers
     const char *spec_env = getenv("IMSAME_SPEC");
-    const uint32_t spec_later = spec_env ? (uint32_t)std::max(1, std::min(SPEC_MAX, atoi(spec_env))) : 4u;
+    const uint32_t spec_later = spec_env ? (uint32_t)std::max(1, std::min(SPEC_MAX, atoi(spec_env))) : (uint32_t)SPEC_MAX;
     const char *bud_env = getenv("IMSAME_SEED_BUDGET");
     const uint32_t budget1 = bud_env ? (uint32_t)std::max(0, atoi(bud_env)) : SEED_BUDGET1;
     uint64_t *ctr = c->ctr.as<uint64_t>();

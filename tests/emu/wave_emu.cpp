@@ -156,7 +156,7 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
     std::vector<uint32_t> cur_h(n), memo((size_t)n * MEMO), act(n), nxt(n), cr(n), cs(n), cr2(n), cs2(n);
     std::vector<uint32_t> cbase(n), ccnt(n), perr(n);
     const char *spec_env = getenv("IMSAME_SPEC");
-    const uint32_t spec_later = spec_env ? (uint32_t)std::max(1, std::min(SPEC_MAX, atoi(spec_env))) : 4u;
+    const uint32_t spec_later = spec_env ? (uint32_t)std::max(1, std::min(SPEC_MAX, atoi(spec_env))) : (uint32_t)SPEC_MAX;
     const char *bud_env = getenv("IMSAME_SEED_BUDGET");
     const uint32_t budget1 = bud_env ? (uint32_t)std::max(0, atoi(bud_env)) : SEED_BUDGET1;
     std::vector<uint8_t> nmemo(n), rstat(n);

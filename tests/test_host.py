@@ -205,14 +205,18 @@ def test_emulated_pipeline_matches_oracle(emu, oracle, name, flags, monkeypatch)
             assert st.err_read == er
 
 
-@pytest.mark.parametrize("budget,lanes", [("1", "1"), ("3", "1"), ("0", "4"), ("3", "4"), ("1", "16"), ("0", "16")])
-def test_emulated_pipeline_seed_budget(emu, oracle, budget, lanes, monkeypatch):
+@pytest.mark.parametrize("budget,lanes,spec", [("1", "1", "8"), ("3", "1", "1"), ("0", "4", "8"), ("3", "4", "2"),
+                                               ("1", "16", "8"), ("0", "16", "1")])
+def test_emulated_pipeline_seed_budget(emu, oracle, budget, lanes, spec, monkeypatch):
     """Reads that pause on the per-round hit budget resume at the same hit,
-    and the grouped scan (L lanes per read, seed_kernel.hip:seed_group) merges
-    its windows in visiting order: results equal the oracle's for every
-    budget (0 = none) and group size."""
+    the grouped scan (L lanes per read, seed_kernel.hip:seed_group) merges
+    its windows in visiting order, and speculative candidates after a
+    rejection (up to `spec` per read and round) keep the first accepted one
+    in visiting order: results equal the oracle's for every budget (0 =
+    none), group size and speculation width."""
     monkeypatch.setenv("IMSAME_SEED_BUDGET", budget)
     monkeypatch.setenv("IMSAME_SEED_L", lanes)
+    monkeypatch.setenv("IMSAME_SPEC", spec)
     rounds = 0
     for name in ("borrowed", "reads_vs_reads", "toolong"):
         case = G.e2e_case(name)
