@@ -60,6 +60,8 @@ def lib():
         L.imsame_dev_set_query.argtypes = [vp, vp, u64, vp, u64]
         L.imsame_dev_align.argtypes = [vp, u64, u64, u64, C.POINTER(Params), vp, vp, u64, C.POINTER(u64),
                                        C.POINTER(Stats)]
+        L.imsame_dev_align_sliced.argtypes = [vp, vp, u64, vp, u64, vp, u64, u64, u64, u64, C.POINTER(Params),
+                                              vp, vp, u64, C.POINTER(u64), C.POINTER(u64), C.POINTER(Stats)]
         L.imsame_dev_nw_pairs.argtypes = [vp, vp, vp, vp, vp, u64, C.POINTER(Params), vp, vp, u64,
                                           C.POINTER(u64), C.POINTER(C.c_double)]
         L.imsame_dev_revcomp.argtypes = [vp, vp, u64, vp, u64, C.POINTER(u64)]
@@ -182,6 +184,35 @@ class Device:
         if rc and not (rc == abi.IMSAME_E_READ_TOO_LONG and allow_too_long):
             raise ImsameError(rc, "imsame_dev_align")
         return res, paths[:used.value], st
+
+    def align_sliced(self, db_seq, db_starts, slice_bases, db_brk=None, read_from=0, read_to=None, n_threads=4,
+                     params=None, want_paths=False, paths_cap=None):
+        """align() against db_seq indexed and searched in slices of at most
+        slice_bases bases, one slice's index in HBM at a time
+        (imsame_dev_align_sliced).  Returns (res, paths, stats, n_slices)."""
+        db_seq, db_starts = _arr(db_seq, np.uint8), _arr(db_starts, np.uint64)
+        brk = None if db_brk is None else _arr(db_brk, np.uint8)
+        read_to = self.n_q if read_to is None else read_to
+        p = params if params is not None else self.params()
+        p.want_paths = 1 if want_paths else 0
+        n = read_to - read_from
+        res = np.zeros(n, dtype=RESULT_DTYPE)
+        cap = (paths_cap if paths_cap is not None else 8 * n + 1024) if want_paths else 0
+        st, used, ns = Stats(), C.c_uint64(), C.c_uint64()
+        while True:
+            paths = np.zeros(max(cap, 1), dtype=np.uint32)
+            rc = lib().imsame_dev_align_sliced(self._h, db_seq.ctypes.data, len(db_seq), db_starts.ctypes.data,
+                                               len(db_starts), None if brk is None else brk.ctypes.data,
+                                               slice_bases, read_from, read_to, n_threads, C.byref(p),
+                                               res.ctypes.data, paths.ctypes.data if want_paths else None, cap,
+                                               C.byref(used), C.byref(ns), C.byref(st))
+            if rc == abi.IMSAME_E_PATHS:
+                cap = int(max(used.value, cap) * 2) + 1024
+                continue
+            break
+        if rc:
+            raise ImsameError(rc, "imsame_dev_align_sliced")
+        return res, paths[:used.value], st, ns.value
 
     def nw_pairs(self, X, Y, params=None, want_paths=False):
         """Unit-level NW + backtrack + acceptance of explicit pairs

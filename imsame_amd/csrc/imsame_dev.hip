@@ -219,6 +219,11 @@ struct imsame_ctx {
     DBuf tb, bnd, paths;
     // revcomp
     DBuf rc_in, rc_out, rc_a, rc_b, rc_c;
+    // database slices (imsame_dev_align_sliced): the e-value's L_DB is the
+    // whole database's length, and each read scans windows below its cap
+    uint64_t ev_db_len = 0;          // 0: db_len
+    bool use_wcap = false;
+    DBuf wcap, wout;
 };
 
 // counters block layout (u64 slots)
@@ -282,7 +287,7 @@ extern "C" void imsame_dev_close(imsame_ctx *c) {
                     &c->q_start, &c->res, &c->cur_p, &c->cur_h, &c->memo, &c->nmemo, &c->rstat, &c->act0,
                     &c->act1, &c->cread, &c->csid, &c->cread2, &c->csid2, &c->cout, &c->cout2, &c->ctr,
                     &c->minraw, &c->minlen, &c->minident, &c->tb, &c->bnd, &c->paths, &c->rc_in, &c->rc_out,
-                    &c->rc_a, &c->rc_b, &c->rc_c, &c->cbase, &c->ccnt, &c->perr};
+                    &c->rc_a, &c->rc_b, &c->rc_c, &c->cbase, &c->ccnt, &c->perr, &c->wcap, &c->wout};
     for (DBuf *b : bufs) b->release();
     (void)hipEventDestroy(c->ev0);
     (void)hipEventDestroy(c->ev1);
@@ -417,7 +422,7 @@ extern "C" int imsame_dev_set_query(imsame_ctx *c, const uint8_t *q_seq, uint64_
 static int build_tables(imsame_ctx *c, const imsame_params *p, uint32_t ymax, uint32_t xmax) {
     std::vector<uint64_t> mr;
     std::vector<uint32_t> ml, mi;
-    imsame_build_tables(p, c->db_len, ymax, xmax, mr, ml, mi);
+    imsame_build_tables(p, c->ev_db_len ? c->ev_db_len : c->db_len, ymax, xmax, mr, ml, mi);
     if (c->minraw.ensure(mr.size() * 8) || c->minlen.ensure(ml.size() * 4) || c->minident.ensure(mi.size() * 4))
         return IMSAME_E_OOM;
     HIPCHK(hipMemcpyAsync(c->minraw.p, mr.data(), mr.size() * 8, hipMemcpyHostToDevice, c->stream));
@@ -591,6 +596,7 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
         S.cread = c->cread.as<uint32_t>(); S.csid = c->csid.as<uint32_t>(); S.ncand = (uint32_t *)(ctr + C_NCAND);
         S.cread2 = c->cread2.as<uint32_t>(); S.csid2 = c->csid2.as<uint32_t>(); S.ncand2 = (uint32_t *)(ctr + C_NCAND2);
         S.err = (unsigned long long *)(ctr + C_ERR); S.nhits = (unsigned long long *)(ctr + C_HITS);
+        S.wcap = c->use_wcap ? c->wcap.as<uint64_t>() : nullptr;
         const char *l_env = getenv(st.rounds == 1 && getenv("IMSAME_SEED_L1") ? "IMSAME_SEED_L1" : "IMSAME_SEED_L");
         const int L = l_env ? atoi(l_env) : seed_lanes(nact);
         const size_t slds = 256 * SEED_LDS_PER_LANE;
@@ -681,6 +687,129 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
 
 // Unit-level entry: NW + backtrack + acceptance for explicit (X_k, Y_k) pairs
 // (build_alignment, alignmentFunctions.c:210-274), default-or-given params.
+// ---------------------------------------------------------------------------
+// Database slices (memory-capped multi-pass index).
+// A bucket lists its hits in descending position, so cutting the database
+// into record ranges from the TOP down splits every bucket into consecutive
+// runs: slice 0 (highest records) first.  The reference's visiting order is
+// then (window, slice, rank in slice), and the first accepted pair of the
+// whole database is the minimum over slices of each slice's first accepted
+// pair under that key.  Passes run slice 0, 1, ...; after a read accepts at
+// window w, later slices (whose hits in window w come after) scan windows
+// < w only.  Results equal one pass over the whole database; each pass holds
+// only its slice's index in HBM.
+// ---------------------------------------------------------------------------
+extern "C" int imsame_dev_align_sliced(imsame_ctx *c, const uint8_t *db_seq, uint64_t db_len,
+                                       const uint64_t *db_start, uint64_t n_db, const uint8_t *db_brk,
+                                       uint64_t slice_bases, uint64_t read_from, uint64_t read_to,
+                                       uint64_t n_threads_semantic, const imsame_params *p, imsame_read_result *res,
+                                       uint32_t *paths, uint64_t paths_cap, uint64_t *paths_used,
+                                       uint64_t *n_slices, imsame_stats *stats) {
+    const double t_start = now_ms();
+    if (!c || !p || (!res && read_to > read_from) || (n_db && !db_start) || (db_len && !db_seq)) return IMSAME_E_ARG;
+    if (!c->have_query) return IMSAME_E_STATE;
+    if (read_to > c->n_q || read_from > read_to || n_db == 0 || slice_bases == 0) return IMSAME_E_ARG;
+    if (p->want_paths && !paths) return IMSAME_E_ARG;
+    // the size error aborts the reference at its first e-value pass in visiting
+    // order; slices would see such hits out of order, so the sliced path takes
+    // only inputs where it cannot fire
+    auto rec_end = [&](uint64_t k) { return k + 1 < n_db ? db_start[k + 1] : db_len; };
+    uint64_t max_rec = 0, ymax = 0;
+    for (uint64_t k = 0; k < n_db; ++k) max_rec = std::max<uint64_t>(max_rec, rec_end(k) - db_start[k]);
+    for (uint64_t r = read_from; r < read_to; ++r)
+        ymax = std::max<uint64_t>(ymax, c->h_q_start[r + 1] - c->h_q_start[r]);
+    if (max_rec > p->max_read_size || ymax > p->max_read_size) return IMSAME_E_ARG;
+    // slices: record ranges [lo, hi), top down, each <= slice_bases (>= 1 record)
+    std::vector<std::pair<uint64_t, uint64_t>> sl;
+    for (uint64_t hi = n_db; hi > 0;) {
+        uint64_t lo = hi - 1;
+        while (lo > 0 && rec_end(hi - 1) - db_start[lo - 1] <= slice_bases) --lo;
+        sl.push_back({lo, hi});
+        hi = lo;
+    }
+    if (n_slices) *n_slices = sl.size();
+    const uint32_t n = (uint32_t)(read_to - read_from);
+    imsame_stats tot;
+    memset(&tot, 0, sizeof tot);
+    tot.n_reads = n;
+    tot.err_read = ~0ull;
+    if (paths_used) *paths_used = 0;
+    HIPCHK(hipSetDevice(c->device));
+    if (c->wcap.ensure((uint64_t)n * 8 + 8) || c->wout.ensure((uint64_t)n * 8 + 8)) return IMSAME_E_OOM;
+    HIPCHK(hipMemsetAsync(c->wcap.p, 0xFF, (uint64_t)n * 8, c->stream));
+    std::vector<uint64_t> cap(n, ~0ull), wout(n);
+    std::vector<imsame_read_result> tmp(n);
+    std::vector<uint64_t> st_rebased;
+    std::vector<uint8_t> brk;
+    uint64_t used = 0;
+    int ret = IMSAME_OK;
+    for (size_t k = 0; k < sl.size() && ret == IMSAME_OK; ++k) {
+        const uint64_t lo = sl[k].first, hi = sl[k].second;
+        const uint64_t base = lo ? db_start[lo] : 0, len = rec_end(hi - 1) - base;
+        st_rebased.resize(hi - lo);
+        for (uint64_t r = lo; r < hi; ++r) st_rebased[r - lo] = db_start[r] - base;
+        const uint8_t *bk = nullptr;
+        if (db_brk && len) {                              // bits [base, base + len) of the bitmap
+            brk.assign((len + 7) / 8, 0);
+            const uint64_t b0 = base >> 3, sh = base & 7, nsrc = (db_len + 7) / 8;
+            for (uint64_t i = 0; i < brk.size(); ++i) {
+                const uint32_t a = b0 + i < nsrc ? db_brk[b0 + i] : 0, b = b0 + i + 1 < nsrc ? db_brk[b0 + i + 1] : 0;
+                brk[i] = (uint8_t)(sh ? ((a >> sh) | (b << (8 - sh))) : a);
+            }
+            bk = brk.data();
+        }
+        int rc = imsame_dev_index(c, db_seq + base, len, st_rebased.data(), hi - lo, bk);
+        if (rc) return rc;
+        c->ev_db_len = db_len;                            // the e-value's L_DB: the whole database
+        c->use_wcap = true;
+        imsame_stats st;
+        uint64_t pu = 0;
+        rc = imsame_dev_align(c, read_from, read_to, n_threads_semantic, p, tmp.data(),
+                              p->want_paths ? paths + used : nullptr, p->want_paths ? paths_cap - used : 0, &pu, &st);
+        c->ev_db_len = 0;
+        if (rc == IMSAME_OK && n) {
+            // window of each accepted hit (same launch shape as the pass)
+            SeedLaunch S;
+            memset(&S, 0, sizeof S);
+            S.db = c->db.as<uint8_t>(); S.db_start = c->db_start.as<uint64_t>(); S.n_db = c->n_db; S.db_len = c->db_len;
+            S.q = c->q.as<uint8_t>(); S.q_start = c->q_start.as<uint64_t>(); S.n_q = c->n_q; S.q_len = c->q_len;
+            S.off = c->off.as<uint64_t>(); S.ent = c->ent.as<uint2>();
+            S.read_from = read_from;
+            S.T = n_threads_semantic ? n_threads_semantic : 1;
+            S.rpt = (uint64_t)floorl((long double)c->n_q / (long double)S.T);     // IMSAME.c:414
+            S.minraw = c->minraw.as<uint64_t>(); S.n_minraw = (uint32_t)ymax + 1;
+            S.wcap = c->wcap.as<uint64_t>();
+            accept_window_kernel<<<nblk(n, 256), 256, 0, c->stream>>>(S, c->res.as<imsame_read_result>(), n,
+                                                                     c->wout.as<uint64_t>());
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipMemcpyAsync(wout.data(), c->wout.p, (uint64_t)n * 8, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+        }
+        c->use_wcap = false;
+        if (rc) { ret = rc; break; }
+        tot.n_nw += st.n_nw; tot.nw_cells += st.nw_cells; tot.n_hits += st.n_hits; tot.rounds += st.rounds;
+        tot.ms_seed += st.ms_seed; tot.ms_nw += st.ms_nw; tot.nw_launches += st.nw_launches; tot.nw_bytes += st.nw_bytes;
+        for (uint32_t r = 0; r < n; ++r) {
+            if (k == 0) res[r] = tmp[r];                  // not found (ylen) unless a slice accepts
+            if (tmp[r].status != 1) continue;
+            if (wout[r] >= cap[r]) return IMSAME_E_STATE;  // cannot happen: the pass scanned below the cap
+            res[r] = tmp[r];
+            res[r].db_seq += lo;
+            res[r].path_off += (uint32_t)used;
+            cap[r] = wout[r];
+        }
+        used += pu;
+        HIPCHK(hipMemcpyAsync(c->wcap.p, cap.data(), (uint64_t)n * 8, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
+    if (paths_used) *paths_used = used;
+    for (uint32_t r = 0; r < n; ++r) tot.n_accepted += res[r].status == 1;
+    tot.nw_launch_ms = tot.nw_launches ? tot.ms_nw / tot.nw_launches : 0;
+    tot.ms_total = now_ms() - t_start;
+    if (stats) *stats = tot;
+    return ret;
+}
+
 extern "C" int imsame_dev_nw_pairs(imsame_ctx *c, const uint8_t *xs, const uint64_t *x_start, const uint8_t *ys,
                                    const uint64_t *y_start, uint64_t npairs, const imsame_params *p,
                                    imsame_read_result *res, uint32_t *paths, uint64_t paths_cap, uint64_t *paths_used,

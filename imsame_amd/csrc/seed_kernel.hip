@@ -30,6 +30,8 @@ struct SeedLaunch {
     uint32_t *next, *nnext;                // reads that paused on the budget (next round's active list)
     uint32_t *cbase, *ccnt;                // per read: first slot and count of this round's candidates
     uint32_t *perr;                        // per read: 1 + record of a pending size error, 0 = none
+    const uint64_t *wcap;                  // per read: scan windows p < wcap[k] only (NULL: no cap;
+                                           // database slices, imsame_dev_align_sliced)
     uint32_t *cread, *csid, *ncand;        // class 0: ylen <= short_ylen
     uint32_t *cread2, *csid2, *ncand2;     // class 1: longer reads
     unsigned long long *err;               // min (read << 32 | record)
@@ -131,7 +133,8 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint
     const uint64_t from_c = (S.rpt == 0) ? 0 : min(r / S.rpt, S.T - 1) * S.rpt;
     const bool head = S.q_start[from_c] == rs;
     const uint64_t p0 = rs - (head ? 0 : 1);
-    const uint64_t up_to = (r + 1 < S.n_q) ? (re ? re - 1 : 0) : S.q_len;    // :93
+    uint64_t up_to = (r + 1 < S.n_q) ? (re ? re - 1 : 0) : S.q_len;          // :93
+    if (S.wcap) up_to = min(up_to, S.wcap[k]);
     uint64_t p = S.cur_p[k];
     uint32_t h = S.cur_h[k];
     if (p == ~0ull) { p = p0 + IMSAME_FIXED_K - 1; h = 0; }
@@ -274,6 +277,7 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
         const bool head = S.q_start[from_c] == rs;
         const uint64_t p0 = rs - (head ? 0 : 1);
         up_to = (r + 1 < S.n_q) ? (re ? re - 1 : 0) : S.q_len;                     // :93
+        if (S.wcap) up_to = min(up_to, S.wcap[k]);
         p = S.cur_p[k]; h = S.cur_h[k];
         if (p == ~0ull) { p = p0 + IMSAME_FIXED_K - 1; h = 0; }
         nm = S.nmemo[k];
@@ -382,6 +386,40 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
     S.cbase[k] = o; S.ccnt[k] = ne;
 }
 
+// Database slices (imsame_dev_align_sliced): the window of each accepted
+// read's hit.  The accepted record s is the first whose NW accepted, and NW
+// is pure (Q18), so its hit is the FIRST e-value-passing hit of s in
+// visiting order: rescan the read's windows for it (read-start logic as
+// seed_one; usually the first window).
+__device__ __forceinline__ void accept_window_one(const SeedLaunch &S, const imsame_read_result *res, uint32_t k,
+                                                  uint64_t *wout) {
+    if (res[k].status != 1) return;
+    const uint64_t r = S.read_from + k;
+    const uint64_t rs = S.q_start[r], re = S.q_start[r + 1], ylen = re - rs;
+    const uint64_t from_c = (S.rpt == 0) ? 0 : min(r / S.rpt, S.T - 1) * S.rpt;
+    const bool head = S.q_start[from_c] == rs;
+    const uint64_t p0 = rs - (head ? 0 : 1);
+    uint64_t up_to = (r + 1 < S.n_q) ? (re ? re - 1 : 0) : S.q_len;
+    if (S.wcap) up_to = min(up_to, S.wcap[k]);
+    const uint64_t mraw = ylen < S.n_minraw ? S.minraw[ylen] : ~0ull;
+    const int64_t ys = (int64_t)rs, ye = (r == S.n_q - 1) ? (int64_t)S.q_len : (int64_t)re - 1;
+    const uint32_t sid = (uint32_t)res[k].db_seq;
+    const int64_t xs = (int64_t)S.db_start[sid];
+    const int64_t xe = (sid == S.n_db - 1) ? (int64_t)S.db_len : (int64_t)S.db_start[sid + 1] - 1;
+    uint64_t w = ~0ull;
+    for (uint64_t p = p0 + IMSAME_FIXED_K - 1; p < up_to && w == ~0ull; ++p) {
+        const uint32_t code = kmer_code_at(S.q, p);
+        for (uint64_t e = S.off[code]; e < S.off[code + 1]; ++e) {
+            const uint2 ent = S.ent[e];
+            if (ent.y != sid) continue;
+            const uint64_t raw = ungapped_raw(S.db, S.q, xs + ent.x, (int64_t)p + 1, xs, xe, ys, ye,
+                                              (int64_t)S.db_len, (int64_t)S.q_len);
+            if (mraw != ~0ull && raw >= mraw) { w = p; break; }
+        }
+    }
+    wout[k] = w;
+}
+
 struct UpdLaunch {
     const uint32_t *cread, *csid; uint32_t n;
     const imsame_read_result *out;
@@ -445,6 +483,10 @@ __device__ __forceinline__ void init_one(const InitLaunch &I, uint32_t k) {
 }
 
 #ifndef IMSAME_WAVE_EMU
+__global__ void accept_window_kernel(const SeedLaunch S, const imsame_read_result *res, uint32_t n, uint64_t *wout) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n) accept_window_one(S, res, k, wout);
+}
 template <int L>
 __global__ __launch_bounds__(256) void seed_group_kernel(SeedLaunch S) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];

@@ -152,6 +152,24 @@ int imsame_dev_align(imsame_ctx *ctx, uint64_t read_from, uint64_t read_to,
                      imsame_read_result *res, uint32_t *paths, uint64_t paths_cap,
                      uint64_t *paths_used, imsame_stats *stats);
 
+/* imsame_dev_align against a database whose index is built and searched in
+ * slices of at most slice_bases bases (whole records; a record longer than
+ * that is a slice of its own), one slice's index in HBM at a time: the
+ * memory-capped multi-pass form of IMSAME.c:232-281 + the worker.  Results
+ * (db_seq global) equal imsame_dev_align over the whole database (the
+ * e-value uses the whole db_len).  Slices run from the highest records down
+ * (a bucket's LIFO order, IMSAME.c:255-276); a read accepted at window w
+ * scans only windows < w of later slices.  Restriction: every record and
+ * read must fit max_read_size (the reference's size abort is not sliced):
+ * IMSAME_E_ARG otherwise.  Needs a loaded query; leaves the last slice's
+ * index loaded.  n_slices (may be NULL) receives the slice count. */
+int imsame_dev_align_sliced(imsame_ctx *ctx, const uint8_t *db_seq, uint64_t db_len,
+                            const uint64_t *db_start, uint64_t n_db, const uint8_t *db_brk,
+                            uint64_t slice_bases, uint64_t read_from, uint64_t read_to,
+                            uint64_t n_threads_semantic, const imsame_params *prm,
+                            imsame_read_result *res, uint32_t *paths, uint64_t paths_cap,
+                            uint64_t *paths_used, uint64_t *n_slices, imsame_stats *stats);
+
 /* Unit-level entry replacing build_alignment (alignmentFunctions.c:210-274:
  * NW + backtrackingNW + identities) plus the acceptance test (:163) for
  * explicit pairs: X_k = xs[x_start[k] .. x_start[k+1]) (database record,

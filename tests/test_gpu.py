@@ -324,3 +324,64 @@ def test_wide_database_past_4_gbases(oracle_memo):
     rc, exp, _ = oracle_memo.align(ref, rst, q, qs, None, 1)
     assert rc == 0
     assert not _cmp(res, exp), _cmp(res, exp)
+
+
+@pytest.mark.parametrize("name", G.e2e_cases())
+def test_sliced_database_matches_oracle_e2e(dev, oracle, name):
+    """imsame_dev_align_sliced with every record a slice of its own (the
+    finest cut) on the golden end-to-end cases: k-mer reset bitmaps shifted
+    into each slice, the whole database's L_DB in the e-value, every
+    -n_threads.  Cases that reach the size abort are refused (IMSAME_E_ARG)."""
+    case = G.e2e_case(name)
+    db, dbs, brk = fasta.load(case["db"], True)
+    q, qs, _ = fasta.load(case["query"])
+    dev.set_query(q, qs)
+    rec_len = np.diff(np.append(dbs, len(db)).astype(np.int64))
+    read_len = np.diff(np.append(qs, len(q)).astype(np.int64))
+    for T in [int(t) for t in case["meta"]["runs"]]:
+        p = _params_for(dev, case)
+        po = _params_for(oracle, case)
+        if max(rec_len.max(initial=0), read_len.max(initial=0)) > p.max_read_size:
+            with pytest.raises(abi_error()) as e:
+                dev.align_sliced(db, dbs, 1, brk, n_threads=T, params=p)
+            assert e.value.code == abi.IMSAME_E_ARG
+            continue
+        rc, ref, er = oracle.align(db, dbs, q, qs, po, T, brk)
+        assert rc == 0
+        res, _, _, ns = dev.align_sliced(db, dbs, 1, brk, n_threads=T, params=p)
+        assert ns == len(dbs)
+        assert not _cmp(res, ref), _cmp(res, ref)
+
+
+def abi_error():
+    from imsame_amd import ImsameError
+    return ImsameError
+
+
+@pytest.mark.parametrize("slice_bases", [1_000_000, 301_000])
+def test_sliced_database_matches_whole(dev, oracle, slice_bases):
+    """Memory-capped multi-pass index: a 4 Mbp database
+    searched in slices gives the whole-database results bit for bit (oracle
+    and single-index device pass), with paths that render to the same
+    identities, for -n_threads 1 and 5."""
+    ref, rst = synth.make_reference_arr(4_000_000, 2_000, seed=21)
+    q, qs = synth.make_reads_arr(ref, 4_000, 150, seed=22)
+    dev.index(ref, rst)
+    dev.set_query(q, qs)
+    wholes = {T: dev.align(n_threads=T)[0] for T in (1, 5)}     # before the slices replace the index
+    for T in (1, 5):
+        whole = wholes[T]
+        res, paths, st, ns = dev.align_sliced(ref, rst, slice_bases, n_threads=T, want_paths=True)
+        assert ns == -(-4_000_000 // (slice_bases - slice_bases % 2_000))
+        assert not _cmp(res, whole), _cmp(res, whole)
+        rc, exp, _ = oracle.align(ref, rst, q, qs, None, T)
+        assert rc == 0 and not _cmp(res, exp), _cmp(res, exp)
+        acc = np.flatnonzero(res["status"] == 1)
+        assert len(acc) > 3_400 and st.n_accepted == len(acc)
+        for k in acc[:300]:
+            r = res[k]
+            s = int(r["db_seq"])
+            X = ref[int(rst[s]):int(rst[s]) + 2_000]
+            Y = q[int(qs[k]):int(qs[k]) + int(r["ylen"])]
+            _, ident = render(X.tobytes(), Y.tobytes(), r, paths[r["path_off"]:r["path_off"] + r["path_len"]])
+            assert ident == r["identities"]
