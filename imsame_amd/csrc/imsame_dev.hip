@@ -699,6 +699,53 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
 // < w only.  Results equal one pass over the whole database; each pass holds
 // only its slice's index in HBM.
 // ---------------------------------------------------------------------------
+// imsame_dev_align on the loaded index with the e-value's L_DB set to the
+// whole database (the index holds one slice of it), per-read window caps and
+// the window of each accepted hit: the building block of database slices
+// (below) and of database shards across GPUs (min of (window, shard) keys).
+extern "C" int imsame_dev_align_windows(imsame_ctx *c, uint64_t read_from, uint64_t read_to,
+                                        uint64_t n_threads_semantic, const imsame_params *p, uint64_t ev_db_len,
+                                        const uint64_t *win_cap, imsame_read_result *res, uint64_t *win,
+                                        uint32_t *paths, uint64_t paths_cap, uint64_t *paths_used,
+                                        imsame_stats *stats) {
+    if (!c || !p || (read_to > read_from && (!res || !win))) return IMSAME_E_ARG;
+    if (!c->have_index || !c->have_query) return IMSAME_E_STATE;
+    if (read_to > c->n_q || read_from > read_to) return IMSAME_E_ARG;
+    HIPCHK(hipSetDevice(c->device));
+    const uint32_t n = (uint32_t)(read_to - read_from);
+    if (c->wcap.ensure((uint64_t)n * 8 + 8) || c->wout.ensure((uint64_t)n * 8 + 8)) return IMSAME_E_OOM;
+    if (win_cap) HIPCHK(hipMemcpyAsync(c->wcap.p, win_cap, (uint64_t)n * 8, hipMemcpyHostToDevice, c->stream));
+    else         HIPCHK(hipMemsetAsync(c->wcap.p, 0xFF, (uint64_t)n * 8, c->stream));
+    HIPCHK(hipMemsetAsync(c->wout.p, 0xFF, (uint64_t)n * 8, c->stream));
+    uint64_t ymax = 0;
+    for (uint64_t r = read_from; r < read_to; ++r)
+        ymax = std::max<uint64_t>(ymax, c->h_q_start[r + 1] - c->h_q_start[r]);
+    c->ev_db_len = ev_db_len;
+    c->use_wcap = true;
+    int rc = imsame_dev_align(c, read_from, read_to, n_threads_semantic, p, res, paths, paths_cap, paths_used, stats);
+    c->ev_db_len = 0;
+    c->use_wcap = false;
+    if (n && (rc == IMSAME_OK || rc == IMSAME_E_READ_TOO_LONG)) {
+        // window of each accepted hit (same read-start logic and cap as the pass)
+        SeedLaunch S;
+        memset(&S, 0, sizeof S);
+        S.db = c->db.as<uint8_t>(); S.db_start = c->db_start.as<uint64_t>(); S.n_db = c->n_db; S.db_len = c->db_len;
+        S.q = c->q.as<uint8_t>(); S.q_start = c->q_start.as<uint64_t>(); S.n_q = c->n_q; S.q_len = c->q_len;
+        S.off = c->off.as<uint64_t>(); S.ent = c->ent.as<uint2>();
+        S.read_from = read_from;
+        S.T = n_threads_semantic ? n_threads_semantic : 1;
+        S.rpt = (uint64_t)floorl((long double)c->n_q / (long double)S.T);     // IMSAME.c:414
+        S.minraw = c->minraw.as<uint64_t>(); S.n_minraw = (uint32_t)ymax + 1;
+        S.wcap = c->wcap.as<uint64_t>();
+        accept_window_kernel<<<nblk(n, 256), 256, 0, c->stream>>>(S, c->res.as<imsame_read_result>(), n,
+                                                                 c->wout.as<uint64_t>());
+        HIPCHK(hipGetLastError());
+    }
+    if (n) HIPCHK(hipMemcpyAsync(win, c->wout.p, (uint64_t)n * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return rc;
+}
+
 extern "C" int imsame_dev_align_sliced(imsame_ctx *c, const uint8_t *db_seq, uint64_t db_len,
                                        const uint64_t *db_start, uint64_t n_db, const uint8_t *db_brk,
                                        uint64_t slice_bases, uint64_t read_from, uint64_t read_to,
@@ -735,8 +782,6 @@ extern "C" int imsame_dev_align_sliced(imsame_ctx *c, const uint8_t *db_seq, uin
     tot.err_read = ~0ull;
     if (paths_used) *paths_used = 0;
     HIPCHK(hipSetDevice(c->device));
-    if (c->wcap.ensure((uint64_t)n * 8 + 8) || c->wout.ensure((uint64_t)n * 8 + 8)) return IMSAME_E_OOM;
-    HIPCHK(hipMemsetAsync(c->wcap.p, 0xFF, (uint64_t)n * 8, c->stream));
     std::vector<uint64_t> cap(n, ~0ull), wout(n);
     std::vector<imsame_read_result> tmp(n);
     std::vector<uint64_t> st_rebased;
@@ -760,32 +805,11 @@ extern "C" int imsame_dev_align_sliced(imsame_ctx *c, const uint8_t *db_seq, uin
         }
         int rc = imsame_dev_index(c, db_seq + base, len, st_rebased.data(), hi - lo, bk);
         if (rc) return rc;
-        c->ev_db_len = db_len;                            // the e-value's L_DB: the whole database
-        c->use_wcap = true;
         imsame_stats st;
         uint64_t pu = 0;
-        rc = imsame_dev_align(c, read_from, read_to, n_threads_semantic, p, tmp.data(),
-                              p->want_paths ? paths + used : nullptr, p->want_paths ? paths_cap - used : 0, &pu, &st);
-        c->ev_db_len = 0;
-        if (rc == IMSAME_OK && n) {
-            // window of each accepted hit (same launch shape as the pass)
-            SeedLaunch S;
-            memset(&S, 0, sizeof S);
-            S.db = c->db.as<uint8_t>(); S.db_start = c->db_start.as<uint64_t>(); S.n_db = c->n_db; S.db_len = c->db_len;
-            S.q = c->q.as<uint8_t>(); S.q_start = c->q_start.as<uint64_t>(); S.n_q = c->n_q; S.q_len = c->q_len;
-            S.off = c->off.as<uint64_t>(); S.ent = c->ent.as<uint2>();
-            S.read_from = read_from;
-            S.T = n_threads_semantic ? n_threads_semantic : 1;
-            S.rpt = (uint64_t)floorl((long double)c->n_q / (long double)S.T);     // IMSAME.c:414
-            S.minraw = c->minraw.as<uint64_t>(); S.n_minraw = (uint32_t)ymax + 1;
-            S.wcap = c->wcap.as<uint64_t>();
-            accept_window_kernel<<<nblk(n, 256), 256, 0, c->stream>>>(S, c->res.as<imsame_read_result>(), n,
-                                                                     c->wout.as<uint64_t>());
-            HIPCHK(hipGetLastError());
-            HIPCHK(hipMemcpyAsync(wout.data(), c->wout.p, (uint64_t)n * 8, hipMemcpyDeviceToHost, c->stream));
-            HIPCHK(hipStreamSynchronize(c->stream));
-        }
-        c->use_wcap = false;
+        rc = imsame_dev_align_windows(c, read_from, read_to, n_threads_semantic, p, db_len, cap.data(), tmp.data(),
+                                      wout.data(), p->want_paths ? paths + used : nullptr,
+                                      p->want_paths ? paths_cap - used : 0, &pu, &st);
         if (rc) { ret = rc; break; }
         tot.n_nw += st.n_nw; tot.nw_cells += st.nw_cells; tot.n_hits += st.n_hits; tot.rounds += st.rounds;
         tot.ms_seed += st.ms_seed; tot.ms_nw += st.ms_nw; tot.nw_launches += st.nw_launches; tot.nw_bytes += st.nw_bytes;
@@ -799,8 +823,6 @@ extern "C" int imsame_dev_align_sliced(imsame_ctx *c, const uint8_t *db_seq, uin
             cap[r] = wout[r];
         }
         used += pu;
-        HIPCHK(hipMemcpyAsync(c->wcap.p, cap.data(), (uint64_t)n * 8, hipMemcpyHostToDevice, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
     }
     if (paths_used) *paths_used = used;
     for (uint32_t r = 0; r < n; ++r) tot.n_accepted += res[r].status == 1;

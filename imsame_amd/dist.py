@@ -39,3 +39,71 @@ def align_sharded(align_fn, n_reads, rank, world, n_threads):
     acc = int(np.count_nonzero(res["status"] == 1))
     tot = all_reduce([acc, b - a])
     return res, (a, b), [int(tot[0]), int(tot[1])]
+
+
+# ---------------------------------------------------------------------------
+# Database shards (SURVEY 8(f) row 4 across GPUs): each rank holds one slice
+# of the DATABASE (whole records; rank 0 the highest records, so a bucket's
+# hits run rank 0, 1, ... in the reference's LIFO order, IMSAME.c:255-276)
+# and aligns every read against it with imsame_dev_align_windows.  The
+# reference's first accepted pair of a read is the accepted result with the
+# smallest (window, rank) key: one min all-reduce of the keys, then one sum
+# all-reduce of the winning 64-byte result rows.  The exchange is real data
+# (16 B + 64 B per read) -- this is the path's one collective step.
+# ---------------------------------------------------------------------------
+NO_KEY = np.iinfo(np.int64).max
+
+
+def db_shard_records(db_starts, db_len, rank, world):
+    """Record range [lo, hi) of database shard `rank`: contiguous, top down
+    (rank 0 = the highest records), cut at record starts near equal bases."""
+    st = np.asarray(db_starts, dtype=np.uint64)
+    n = len(st)
+    # cut c (0 < c < world) at the first record starting at or after c/world of the bases
+    cuts = [int(np.searchsorted(st, (db_len * c) // world)) for c in range(1, world)]
+    edges = [0] + cuts + [n]                        # bottom-up record edges
+    k = world - 1 - rank                            # rank 0 takes the top range
+    return edges[k], edges[k + 1]
+
+
+def shard_keys(res, win, rank, world):
+    """Per-read key of this shard's result: window * world + rank if accepted."""
+    acc = res["status"] == 1
+    w = np.asarray(win, dtype=np.uint64)
+    return np.where(acc, (w.astype(np.int64) * world + rank), NO_KEY).astype(np.int64)
+
+
+def merge_shard_results(parts):
+    """Host merge of shard results [(res, win, rec_lo)] listed rank 0 first:
+    per read, the accepted row with the smallest (window, rank); reads no
+    shard accepted keep rank 0's row.  db_seq becomes global."""
+    world = len(parts)
+    keys = np.stack([shard_keys(r, w, k, world) for k, (r, w, _) in enumerate(parts)])
+    best = keys.argmin(axis=0)
+    out = parts[0][0].copy()
+    for k, (r, _, lo) in enumerate(parts):
+        m = (best == k) & (keys[k] != NO_KEY)
+        out[m] = r[m]
+        out["db_seq"][m] += lo
+    return out
+
+
+def merge_db_sharded(res, win, rec_lo, rank, world):
+    """merge_shard_results over torch.distributed ranks (RCCL "nccl" on
+    GPUs, gloo on CPU): min all-reduce of the keys, sum all-reduce of the
+    winning rows (64 B each, so exactly one rank contributes a row)."""
+    import torch
+    import torch.distributed as dist
+    dev = _device_for_backend()
+    key = shard_keys(res, win, rank, world)
+    kmin = torch.from_numpy(key.copy()).to(dev)
+    dist.all_reduce(kmin, op=dist.ReduceOp.MIN)
+    kmin = kmin.cpu().numpy()
+    mine = (kmin == key) & (key != NO_KEY)
+    rows = res.copy()
+    rows["db_seq"] += np.where(mine, rec_lo, 0).astype(rows["db_seq"].dtype)
+    contrib = mine | ((kmin == NO_KEY) & (rank == 0))
+    rows[~contrib] = np.zeros(1, dtype=rows.dtype)
+    words = torch.from_numpy(rows.view(np.int64).copy()).to(dev)
+    dist.all_reduce(words, op=dist.ReduceOp.SUM)
+    return words.cpu().numpy().view(res.dtype).reshape(res.shape)

@@ -152,6 +152,22 @@ int imsame_dev_align(imsame_ctx *ctx, uint64_t read_from, uint64_t read_to,
                      imsame_read_result *res, uint32_t *paths, uint64_t paths_cap,
                      uint64_t *paths_used, imsame_stats *stats);
 
+/* imsame_dev_align on the loaded index when it holds ONE SLICE (whole
+ * records) of a larger database: ev_db_len is the whole database's length
+ * for the e-value (0 = the loaded index's), win_cap[k] (host, may be NULL)
+ * limits read read_from+k to windows p < win_cap[k] (p = query position of
+ * the k-mer's last base, the reference's curr_pos), and win[k] (host, out)
+ * receives the window of each accepted read's hit (~0 if none).  res[k].db_seq
+ * is slice-local.  For a database cut into slices s = 0, 1, ... from its
+ * highest records down, the reference's first accepted pair is, per read,
+ * the accepted result with the smallest (win, s): slices on one GPU
+ * (imsame_dev_align_sliced) or shards across GPUs (a min all-reduce). */
+int imsame_dev_align_windows(imsame_ctx *ctx, uint64_t read_from, uint64_t read_to,
+                             uint64_t n_threads_semantic, const imsame_params *prm, uint64_t ev_db_len,
+                             const uint64_t *win_cap, imsame_read_result *res, uint64_t *win,
+                             uint32_t *paths, uint64_t paths_cap, uint64_t *paths_used,
+                             imsame_stats *stats);
+
 /* imsame_dev_align against a database whose index is built and searched in
  * slices of at most slice_bases bases (whole records; a record longer than
  * that is a slice of its own), one slice's index in HBM at a time: the

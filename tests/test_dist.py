@@ -59,3 +59,65 @@ def test_two_rank_shards_equal_single_run(tmp_path, oracle, T):
     acc = int((exp["status"] == 1).sum())
     for r in range(world):
         assert list(np.load(tmp_path / f"t{r}.npy")) == [acc, len(qs)]
+
+
+def _fake_parts(world, n=300, seed=3):
+    """Per-shard results as imsame_dev_align_windows returns them (random
+    accepts, windows in a small range so (window) ties across shards occur)."""
+    from imsame_amd.abi import RESULT_DTYPE
+    rng = np.random.default_rng(seed)
+    ylen = rng.integers(50, 200, n)
+    parts = []
+    for k in range(world):
+        r = np.zeros(n, dtype=RESULT_DTYPE)
+        r["ylen"] = ylen
+        acc = rng.random(n) < 0.4
+        r["status"][acc] = 1
+        for f in ("db_seq", "score", "bx", "by", "length", "identities", "head_x"):
+            r[f][acc] = rng.integers(1, 1000, int(acc.sum()))
+        win = np.where(acc, rng.integers(11, 20, n), np.iinfo(np.uint64).max).astype(np.uint64)
+        parts.append((r, win, 1000 * (world - 1 - k)))          # rank 0 holds the top records
+    return parts
+
+
+def test_db_shard_merge_rule():
+    """Smallest (window, shard) wins; a window tie goes to the higher records
+    (lower rank: earlier in the LIFO bucket); unaccepted reads keep shard 0's
+    row; db_seq becomes global."""
+    from imsame_amd.dist import merge_shard_results, db_shard_records
+    parts = _fake_parts(3)
+    out = merge_shard_results(parts)
+    for i in range(len(out)):
+        cands = [(int(w[i]), k) for k, (r, w, _) in enumerate(parts) if r["status"][i] == 1]
+        if not cands:
+            assert out[i] == parts[0][0][i]
+            continue
+        w, k = min(cands)
+        exp = parts[k][0][i].copy()
+        exp["db_seq"] += parts[k][2]
+        assert out[i] == exp
+    st = np.arange(0, 10_000, 100, dtype=np.uint64)
+    rngs = [db_shard_records(st, 10_000, r, 4) for r in range(4)]
+    assert rngs[0][1] == 100 and rngs[-1][0] == 0                  # rank 0 = top records
+    assert all(rngs[r][0] == rngs[r + 1][1] for r in range(3))
+
+
+def _merge_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+    from imsame_amd.dist import merge_db_sharded
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    r, w, lo = _fake_parts(world)[rank]
+    np.save(os.path.join(out_dir, f"m{rank}.npy"), merge_db_sharded(r, w, lo, rank, world))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_db_shard_merge_over_gloo(tmp_path):
+    """The collective form (min all-reduce of keys, sum all-reduce of the
+    winning rows) equals the host merge on every rank."""
+    from imsame_amd.dist import merge_shard_results
+    world = 2
+    mp.spawn(_merge_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    exp = merge_shard_results(_fake_parts(world))
+    for r in range(world):
+        assert np.array_equal(np.load(tmp_path / f"m{r}.npy"), exp)

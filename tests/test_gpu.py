@@ -385,3 +385,29 @@ def test_sliced_database_matches_whole(dev, oracle, slice_bases):
             Y = q[int(qs[k]):int(qs[k]) + int(r["ylen"])]
             _, ident = render(X.tobytes(), Y.tobytes(), r, paths[r["path_off"]:r["path_off"] + r["path_len"]])
             assert ident == r["identities"]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_db_shards_min_merge_matches_whole(dev, oracle, world):
+    """Database shards (one per GPU in a multi-GPU run, here one after the
+    other on one device): each shard's index + imsame_dev_align_windows with
+    the whole database's L_DB and no caps, merged by the smallest (window,
+    shard) key (imsame_amd.dist) -- bit-exact vs the whole-database oracle."""
+    from imsame_amd.dist import db_shard_records, merge_shard_results
+    ref, rst = synth.make_reference_arr(3_000_000, 2_000, seed=31)
+    q, qs = synth.make_reads_arr(ref, 3_000, 150, seed=32)
+    dev.set_query(q, qs)
+    for T in (1, 4):
+        parts = []
+        for rank in range(world):
+            lo, hi = db_shard_records(rst, len(ref), rank, world)
+            base = int(rst[lo])
+            end = int(rst[hi]) if hi < len(rst) else len(ref)
+            dev.index(ref[base:end], rst[lo:hi] - np.uint64(base))
+            res, win, _ = dev.align_windows(len(ref), n_threads=T)
+            assert (win[res["status"] == 1] != np.iinfo(np.uint64).max).all()
+            parts.append((res, win, lo))
+        got = merge_shard_results(parts)
+        rc, exp, _ = oracle.align(ref, rst, q, qs, None, T)
+        assert rc == 0 and not _cmp(got, exp), _cmp(got, exp)
+        assert (got["status"] == 1).sum() > 2_500
