@@ -77,6 +77,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-kind", choices=("auto", "port", "reference"), default="auto",
                     help="auto: the compiled reference (oracle/_ref/IMSAME) when present, else the port")
+    ap.add_argument("--slice-bases", type=int, default=0,
+                    help="search the database in slices of at most this many bases, one slice's index in HBM "
+                         "at a time (imsame_dev_align_sliced; the index rebuilds are inside the timed step)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "nw_traffic.json"))
     a = ap.parse_args()
     cfg = CONFIGS[a.config]
@@ -112,7 +115,14 @@ def main():
     dev.set_query(q, qs)                               # H2D once: inputs resident in HBM
     params = dev.params(max_read_size=cfg["max_rs"]) if cfg["max_rs"] else dev.params()
 
+    n_slices = 1
+
     def step():
+        nonlocal n_slices
+        if a.slice_bases:
+            res, paths, st, n_slices = dev.align_sliced(ref, rst, a.slice_bases, n_threads=a.n_threads,
+                                                        params=params)
+            return res, paths, st
         return dev.align(0, a.reads, n_threads=a.n_threads, params=params)
 
     def barrier():
@@ -168,6 +178,8 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_sample > 0:
+        if a.slice_bases:
+            dev.index(ref, rst)                     # the sample is checked against the whole index
         cpu = cpu_baseline(dev, ref, rst, q, qs, a, params)
 
     if rank == 0:
@@ -175,7 +187,8 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "reads/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "int32", "data": "synthetic",
-            "config": {"workload": cfg["workload"],
+            "config": {"workload": cfg["workload"] + (f"; database searched in {n_slices} slices of <= "
+                                                       f"{a.slice_bases} bases" if a.slice_bases else ""),
                        "reads_per_gpu": a.reads, "read_len": a.read_len, "ref_bp": a.ref_bp,
                        "record_bp": a.record_bp, "n_threads_semantic": a.n_threads,
                        "parallelism": f"dp{world} (read shards, replicated index)"},

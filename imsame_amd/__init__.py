@@ -60,7 +60,7 @@ def lib():
         L.imsame_dev_set_query.argtypes = [vp, vp, u64, vp, u64]
         L.imsame_dev_align.argtypes = [vp, u64, u64, u64, C.POINTER(Params), vp, vp, u64, C.POINTER(u64),
                                        C.POINTER(Stats)]
-        L.imsame_dev_align_windows.argtypes = [vp, u64, u64, u64, C.POINTER(Params), u64, vp, vp, vp, vp, u64,
+        L.imsame_dev_align_windows.argtypes = [vp, u64, u64, u64, C.POINTER(Params), u64, vp, vp, vp, vp, vp, u64,
                                                C.POINTER(u64), C.POINTER(Stats)]
         L.imsame_dev_align_sliced.argtypes = [vp, vp, u64, vp, u64, vp, u64, u64, u64, u64, C.POINTER(Params),
                                               vp, vp, u64, C.POINTER(u64), C.POINTER(u64), C.POINTER(Stats)]
@@ -188,7 +188,7 @@ class Device:
         return res, paths[:used.value], st
 
     def align_windows(self, ev_db_len, win_cap=None, read_from=0, read_to=None, n_threads=4, params=None,
-                      allow_too_long=False):
+                      allow_too_long=False, win_start=None):
         """align() on the loaded index as ONE SLICE of a database of
         ev_db_len bases: per-read window caps in, accept windows out
         (imsame_dev_align_windows).  Returns (res, win, stats); db_seq is
@@ -200,8 +200,10 @@ class Device:
         res = np.zeros(n, dtype=RESULT_DTYPE)
         win = np.zeros(n, dtype=np.uint64)
         cap = None if win_cap is None else _arr(win_cap, np.uint64)
+        ws = None if win_start is None else _arr(win_start, np.uint64)
         st, used = Stats(), C.c_uint64()
         rc = lib().imsame_dev_align_windows(self._h, read_from, read_to, n_threads, C.byref(p), ev_db_len,
+                                            None if ws is None else ws.ctypes.data,
                                             None if cap is None else cap.ctypes.data, res.ctypes.data,
                                             win.ctypes.data, None, 0, C.byref(used), C.byref(st))
         if rc and not (rc == abi.IMSAME_E_READ_TOO_LONG and allow_too_long):

@@ -222,8 +222,8 @@ struct imsame_ctx {
     // database slices (imsame_dev_align_sliced): the e-value's L_DB is the
     // whole database's length, and each read scans windows below its cap
     uint64_t ev_db_len = 0;          // 0: db_len
-    bool use_wcap = false;
-    DBuf wcap, wout;
+    bool use_wcap = false, use_wstart = false;
+    DBuf wcap, wout, wstart;
 };
 
 // counters block layout (u64 slots)
@@ -287,7 +287,7 @@ extern "C" void imsame_dev_close(imsame_ctx *c) {
                     &c->q_start, &c->res, &c->cur_p, &c->cur_h, &c->memo, &c->nmemo, &c->rstat, &c->act0,
                     &c->act1, &c->cread, &c->csid, &c->cread2, &c->csid2, &c->cout, &c->cout2, &c->ctr,
                     &c->minraw, &c->minlen, &c->minident, &c->tb, &c->bnd, &c->paths, &c->rc_in, &c->rc_out,
-                    &c->rc_a, &c->rc_b, &c->rc_c, &c->cbase, &c->ccnt, &c->perr, &c->wcap, &c->wout};
+                    &c->rc_a, &c->rc_b, &c->rc_c, &c->cbase, &c->ccnt, &c->perr, &c->wcap, &c->wout, &c->wstart};
     for (DBuf *b : bufs) b->release();
     (void)hipEventDestroy(c->ev0);
     (void)hipEventDestroy(c->ev1);
@@ -597,6 +597,7 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
         S.cread2 = c->cread2.as<uint32_t>(); S.csid2 = c->csid2.as<uint32_t>(); S.ncand2 = (uint32_t *)(ctr + C_NCAND2);
         S.err = (unsigned long long *)(ctr + C_ERR); S.nhits = (unsigned long long *)(ctr + C_HITS);
         S.wcap = c->use_wcap ? c->wcap.as<uint64_t>() : nullptr;
+        S.wstart = c->use_wstart ? c->wstart.as<uint64_t>() : nullptr;
         const char *l_env = getenv(st.rounds == 1 && getenv("IMSAME_SEED_L1") ? "IMSAME_SEED_L1" : "IMSAME_SEED_L");
         const int L = l_env ? atoi(l_env) : seed_lanes(nact);
         const size_t slds = 256 * SEED_LDS_PER_LANE;
@@ -705,7 +706,8 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
 // (below) and of database shards across GPUs (min of (window, shard) keys).
 extern "C" int imsame_dev_align_windows(imsame_ctx *c, uint64_t read_from, uint64_t read_to,
                                         uint64_t n_threads_semantic, const imsame_params *p, uint64_t ev_db_len,
-                                        const uint64_t *win_cap, imsame_read_result *res, uint64_t *win,
+                                        const uint64_t *win_start, const uint64_t *win_cap,
+                                        imsame_read_result *res, uint64_t *win,
                                         uint32_t *paths, uint64_t paths_cap, uint64_t *paths_used,
                                         imsame_stats *stats) {
     if (!c || !p || (read_to > read_from && (!res || !win))) return IMSAME_E_ARG;
@@ -713,7 +715,10 @@ extern "C" int imsame_dev_align_windows(imsame_ctx *c, uint64_t read_from, uint6
     if (read_to > c->n_q || read_from > read_to) return IMSAME_E_ARG;
     HIPCHK(hipSetDevice(c->device));
     const uint32_t n = (uint32_t)(read_to - read_from);
-    if (c->wcap.ensure((uint64_t)n * 8 + 8) || c->wout.ensure((uint64_t)n * 8 + 8)) return IMSAME_E_OOM;
+    if (c->wcap.ensure((uint64_t)n * 8 + 8) || c->wout.ensure((uint64_t)n * 8 + 8) ||
+        (win_start && c->wstart.ensure((uint64_t)n * 8 + 8)))
+        return IMSAME_E_OOM;
+    if (win_start) HIPCHK(hipMemcpyAsync(c->wstart.p, win_start, (uint64_t)n * 8, hipMemcpyHostToDevice, c->stream));
     if (win_cap) HIPCHK(hipMemcpyAsync(c->wcap.p, win_cap, (uint64_t)n * 8, hipMemcpyHostToDevice, c->stream));
     else         HIPCHK(hipMemsetAsync(c->wcap.p, 0xFF, (uint64_t)n * 8, c->stream));
     HIPCHK(hipMemsetAsync(c->wout.p, 0xFF, (uint64_t)n * 8, c->stream));
@@ -722,9 +727,10 @@ extern "C" int imsame_dev_align_windows(imsame_ctx *c, uint64_t read_from, uint6
         ymax = std::max<uint64_t>(ymax, c->h_q_start[r + 1] - c->h_q_start[r]);
     c->ev_db_len = ev_db_len;
     c->use_wcap = true;
+    c->use_wstart = win_start != nullptr;
     int rc = imsame_dev_align(c, read_from, read_to, n_threads_semantic, p, res, paths, paths_cap, paths_used, stats);
     c->ev_db_len = 0;
-    c->use_wcap = false;
+    c->use_wcap = c->use_wstart = false;
     if (n && (rc == IMSAME_OK || rc == IMSAME_E_READ_TOO_LONG)) {
         // window of each accepted hit (same read-start logic and cap as the pass)
         SeedLaunch S;
@@ -782,47 +788,69 @@ extern "C" int imsame_dev_align_sliced(imsame_ctx *c, const uint8_t *db_seq, uin
     tot.err_read = ~0ull;
     if (paths_used) *paths_used = 0;
     HIPCHK(hipSetDevice(c->device));
-    std::vector<uint64_t> cap(n, ~0ull), wout(n);
+    // Two phases.  A: every slice, windows below a band of BAND windows per
+    // read -- most reads accept at their first windows, and the smallest
+    // (window, slice) key found there is final since every key below the band
+    // was examined.  B: the reads A left, from the band on, slice by slice
+    // under the caps.  (Without A, slices not holding a read's record would
+    // be scanned over all windows before a cap exists.)
+    const uint64_t BAND = 8;
+    std::vector<uint64_t> cap(n), wstart(n), wout(n);
+    for (uint32_t r = 0; r < n; ++r) cap[r] = c->h_q_start[read_from + r] + IMSAME_FIXED_K - 1 + BAND;
     std::vector<imsame_read_result> tmp(n);
     std::vector<uint64_t> st_rebased;
     std::vector<uint8_t> brk;
     uint64_t used = 0;
     int ret = IMSAME_OK;
-    for (size_t k = 0; k < sl.size() && ret == IMSAME_OK; ++k) {
-        const uint64_t lo = sl[k].first, hi = sl[k].second;
-        const uint64_t base = lo ? db_start[lo] : 0, len = rec_end(hi - 1) - base;
-        st_rebased.resize(hi - lo);
-        for (uint64_t r = lo; r < hi; ++r) st_rebased[r - lo] = db_start[r] - base;
-        const uint8_t *bk = nullptr;
-        if (db_brk && len) {                              // bits [base, base + len) of the bitmap
-            brk.assign((len + 7) / 8, 0);
-            const uint64_t b0 = base >> 3, sh = base & 7, nsrc = (db_len + 7) / 8;
-            for (uint64_t i = 0; i < brk.size(); ++i) {
-                const uint32_t a = b0 + i < nsrc ? db_brk[b0 + i] : 0, b = b0 + i + 1 < nsrc ? db_brk[b0 + i + 1] : 0;
-                brk[i] = (uint8_t)(sh ? ((a >> sh) | (b << (8 - sh))) : a);
+    for (int phase = 0; phase < 2 && ret == IMSAME_OK; ++phase) {
+        if (phase == 1) {
+            uint64_t left = 0;
+            for (uint32_t r = 0; r < n; ++r) {
+                const bool done = res[r].status == 1;
+                wstart[r] = cap[r];
+                cap[r] = done ? 0 : ~0ull;                // accepted in A: final, not scanned again
+                left += !done;
             }
-            bk = brk.data();
+            if (!left) break;
         }
-        int rc = imsame_dev_index(c, db_seq + base, len, st_rebased.data(), hi - lo, bk);
-        if (rc) return rc;
-        imsame_stats st;
-        uint64_t pu = 0;
-        rc = imsame_dev_align_windows(c, read_from, read_to, n_threads_semantic, p, db_len, cap.data(), tmp.data(),
-                                      wout.data(), p->want_paths ? paths + used : nullptr,
-                                      p->want_paths ? paths_cap - used : 0, &pu, &st);
-        if (rc) { ret = rc; break; }
-        tot.n_nw += st.n_nw; tot.nw_cells += st.nw_cells; tot.n_hits += st.n_hits; tot.rounds += st.rounds;
-        tot.ms_seed += st.ms_seed; tot.ms_nw += st.ms_nw; tot.nw_launches += st.nw_launches; tot.nw_bytes += st.nw_bytes;
-        for (uint32_t r = 0; r < n; ++r) {
-            if (k == 0) res[r] = tmp[r];                  // not found (ylen) unless a slice accepts
-            if (tmp[r].status != 1) continue;
-            if (wout[r] >= cap[r]) return IMSAME_E_STATE;  // cannot happen: the pass scanned below the cap
-            res[r] = tmp[r];
-            res[r].db_seq += lo;
-            res[r].path_off += (uint32_t)used;
-            cap[r] = wout[r];
+        for (size_t k = 0; k < sl.size() && ret == IMSAME_OK; ++k) {
+            const uint64_t lo = sl[k].first, hi = sl[k].second;
+            const uint64_t base = lo ? db_start[lo] : 0, len = rec_end(hi - 1) - base;
+            st_rebased.resize(hi - lo);
+            for (uint64_t r = lo; r < hi; ++r) st_rebased[r - lo] = db_start[r] - base;
+            const uint8_t *bk = nullptr;
+            if (db_brk && len) {                          // bits [base, base + len) of the bitmap
+                brk.assign((len + 7) / 8, 0);
+                const uint64_t b0 = base >> 3, sh = base & 7, nsrc = (db_len + 7) / 8;
+                for (uint64_t i = 0; i < brk.size(); ++i) {
+                    const uint32_t a = b0 + i < nsrc ? db_brk[b0 + i] : 0, b = b0 + i + 1 < nsrc ? db_brk[b0 + i + 1] : 0;
+                    brk[i] = (uint8_t)(sh ? ((a >> sh) | (b << (8 - sh))) : a);
+                }
+                bk = brk.data();
+            }
+            int rc = imsame_dev_index(c, db_seq + base, len, st_rebased.data(), hi - lo, bk);
+            if (rc) return rc;
+            imsame_stats st;
+            uint64_t pu = 0;
+            rc = imsame_dev_align_windows(c, read_from, read_to, n_threads_semantic, p, db_len,
+                                          phase ? wstart.data() : nullptr, cap.data(), tmp.data(), wout.data(),
+                                          p->want_paths ? paths + used : nullptr, p->want_paths ? paths_cap - used : 0,
+                                          &pu, &st);
+            if (rc) { ret = rc; break; }
+            tot.n_nw += st.n_nw; tot.nw_cells += st.nw_cells; tot.n_hits += st.n_hits; tot.rounds += st.rounds;
+            tot.ms_seed += st.ms_seed; tot.ms_nw += st.ms_nw; tot.nw_launches += st.nw_launches;
+            tot.nw_bytes += st.nw_bytes;
+            for (uint32_t r = 0; r < n; ++r) {
+                if (phase == 0 && k == 0) res[r] = tmp[r];  // not found (ylen) unless a slice accepts
+                if (tmp[r].status != 1) continue;
+                if (wout[r] >= cap[r]) return IMSAME_E_STATE;   // cannot happen: the pass scanned below the cap
+                res[r] = tmp[r];
+                res[r].db_seq += lo;
+                res[r].path_off += (uint32_t)used;
+                cap[r] = wout[r];
+            }
+            used += pu;
         }
-        used += pu;
     }
     if (paths_used) *paths_used = used;
     for (uint32_t r = 0; r < n; ++r) tot.n_accepted += res[r].status == 1;

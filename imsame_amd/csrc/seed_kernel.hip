@@ -32,6 +32,7 @@ struct SeedLaunch {
     uint32_t *perr;                        // per read: 1 + record of a pending size error, 0 = none
     const uint64_t *wcap;                  // per read: scan windows p < wcap[k] only (NULL: no cap;
                                            // database slices, imsame_dev_align_sliced)
+    const uint64_t *wstart;                // per read: first window scanned >= wstart[k] (NULL: none)
     uint32_t *cread, *csid, *ncand;        // class 0: ylen <= short_ylen
     uint32_t *cread2, *csid2, *ncand2;     // class 1: longer reads
     unsigned long long *err;               // min (read << 32 | record)
@@ -137,7 +138,7 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint
     if (S.wcap) up_to = min(up_to, S.wcap[k]);
     uint64_t p = S.cur_p[k];
     uint32_t h = S.cur_h[k];
-    if (p == ~0ull) { p = p0 + IMSAME_FIXED_K - 1; h = 0; }
+    if (p == ~0ull) { p = p0 + IMSAME_FIXED_K - 1; h = 0; if (S.wstart) p = max(p, S.wstart[k]); }
     const uint32_t nm = S.nmemo[k];
     uint32_t memo[MEMO];
 #pragma unroll
@@ -279,7 +280,7 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
         up_to = (r + 1 < S.n_q) ? (re ? re - 1 : 0) : S.q_len;                     // :93
         if (S.wcap) up_to = min(up_to, S.wcap[k]);
         p = S.cur_p[k]; h = S.cur_h[k];
-        if (p == ~0ull) { p = p0 + IMSAME_FIXED_K - 1; h = 0; }
+        if (p == ~0ull) { p = p0 + IMSAME_FIXED_K - 1; h = 0; if (S.wstart) p = max(p, S.wstart[k]); }
         nm = S.nmemo[k];
         spec = nm ? S.spec : 1u;
         budget = S.budget ? S.budget : 0xFFFFFFFFu;

@@ -156,7 +156,8 @@ int imsame_dev_align(imsame_ctx *ctx, uint64_t read_from, uint64_t read_to,
  * records) of a larger database: ev_db_len is the whole database's length
  * for the e-value (0 = the loaded index's), win_cap[k] (host, may be NULL)
  * limits read read_from+k to windows p < win_cap[k] (p = query position of
- * the k-mer's last base, the reference's curr_pos), and win[k] (host, out)
+ * the k-mer's last base, the reference's curr_pos), win_start[k] (host, may
+ * be NULL) makes its scan begin at window max(first, win_start[k]), and win[k] (host, out)
  * receives the window of each accepted read's hit (~0 if none).  res[k].db_seq
  * is slice-local.  For a database cut into slices s = 0, 1, ... from its
  * highest records down, the reference's first accepted pair is, per read,
@@ -164,7 +165,8 @@ int imsame_dev_align(imsame_ctx *ctx, uint64_t read_from, uint64_t read_to,
  * (imsame_dev_align_sliced) or shards across GPUs (a min all-reduce). */
 int imsame_dev_align_windows(imsame_ctx *ctx, uint64_t read_from, uint64_t read_to,
                              uint64_t n_threads_semantic, const imsame_params *prm, uint64_t ev_db_len,
-                             const uint64_t *win_cap, imsame_read_result *res, uint64_t *win,
+                             const uint64_t *win_start, const uint64_t *win_cap,
+                             imsame_read_result *res, uint64_t *win,
                              uint32_t *paths, uint64_t paths_cap, uint64_t *paths_used,
                              imsame_stats *stats);
 
@@ -175,7 +177,9 @@ int imsame_dev_align_windows(imsame_ctx *ctx, uint64_t read_from, uint64_t read_
  * (db_seq global) equal imsame_dev_align over the whole database (the
  * e-value uses the whole db_len).  Slices run from the highest records down
  * (a bucket's LIFO order, IMSAME.c:255-276); a read accepted at window w
- * scans only windows < w of later slices.  Restriction: every record and
+ * scans only windows < w of later slices.  Two phases: every slice over each
+ * read's first windows (where most reads accept, and where the smallest key
+ * is final), then the rest for reads still open.  Restriction: every record and
  * read must fit max_read_size (the reference's size abort is not sliced):
  * IMSAME_E_ARG otherwise.  Needs a loaded query; leaves the last slice's
  * index loaded.  n_slices (may be NULL) receives the slice count. */

@@ -175,7 +175,7 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
         SeedLaunch S;
         S.db = db; S.db_start = dbs.data(); S.n_db = n_db; S.db_len = db_len;
         S.q = q; S.q_start = qs.data(); S.n_q = n_q; S.q_len = q_len;
-        S.off = off.data(); S.ent = ent.data(); S.wcap = nullptr;
+        S.off = off.data(); S.ent = ent.data(); S.wcap = nullptr; S.wstart = nullptr;
         S.active = act.data(); S.n_active = nact;
         S.read_from = read_from; S.T = T ? T : 1;
         S.rpt = (uint64_t)floorl((long double)n_q / (long double)S.T);
