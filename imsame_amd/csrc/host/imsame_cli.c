@@ -50,6 +50,7 @@ static void usage(void) {
     printf("           --help      Shows help for program usage\n");
     printf("           -device     [Integer: HIP device] (default 0)\n");
     printf("           -max_read_size [Integer] (default 3000)\n");
+    printf("           -slice_bases [Integer: index the database in slices of at most this many bases]\n");
     exit(1);
 }
 
@@ -59,6 +60,7 @@ int main(int argc, char **argv) {
     imsame_params_default(&prm);
     uint64_t T = 4;                                   /* IMSAME.c:49 */
     int device = 0;
+    uint64_t slice_bases = 0;                        /* 0: one index (the reference's) */
     /* init_args, IMSAME.c:520-578 (same strcmp scan over every argv slot) */
     for (int a = 0; a < argc; a++) {
         if (!strcmp(argv[a], "--help")) usage();
@@ -83,6 +85,7 @@ int main(int argc, char **argv) {
         if (!strcmp(argv[a], "-n_threads")) T = (uint64_t)atoi(argv[a + 1]);
         if (!strcmp(argv[a], "-device")) device = atoi(argv[a + 1]);
         if (!strcmp(argv[a], "-max_read_size")) prm.max_read_size = strtoull(argv[a + 1], NULL, 10);
+        if (!strcmp(argv[a], "-slice_bases")) slice_bases = strtoull(argv[a + 1], NULL, 10);
     }
     if (!qpath || !dpath) terror("A query and database is required");
     FILE *out = NULL;
@@ -99,7 +102,7 @@ int main(int argc, char **argv) {
     t0 = now_s();
     host_seqs db, q;
     if (host_load_fasta(dpath, 1, &db)) terror("Could not open database file");
-    rc = imsame_dev_index(ctx, db.seq, db.len, db.start, db.n, db.brk);
+    rc = slice_bases ? IMSAME_OK : imsame_dev_index(ctx, db.seq, db.len, db.start, db.n, db.brk);
     if (rc) terror(imsame_strerror(rc));
     printf("[INFO] Database loaded and of length %" PRIu64 ". Hash table building took %e seconds\n", db.len,
            now_s() - t0);
@@ -126,11 +129,15 @@ int main(int argc, char **argv) {
     prm.want_paths = out ? 1 : 0;
     imsame_stats st;
     for (;;) {
-        rc = imsame_dev_align(ctx, 0, q.n, T, &prm, res, paths, cap, &used, &st);
+        rc = slice_bases ? imsame_dev_align_sliced(ctx, db.seq, db.len, db.start, db.n, db.brk, slice_bases, 0, q.n,
+                                                   T, &prm, res, paths, cap, &used, NULL, &st)
+                         : imsame_dev_align(ctx, 0, q.n, T, &prm, res, paths, cap, &used, &st);
         if (rc != IMSAME_E_PATHS) break;
-        cap = used + used / 4 + 1024;                 /* arena too small: grow and redo */
+        cap = used + used / 4 + 1024 > 2 * cap ? used + used / 4 + 1024 : 2 * cap;   /* too small: grow, redo */
         paths = realloc(paths, cap * sizeof(uint32_t));
     }
+    if (rc == IMSAME_E_ARG && slice_bases)
+        terror("-slice_bases needs every record and read within -max_read_size");
     if (rc && rc != IMSAME_E_READ_TOO_LONG) terror(imsame_strerror(rc));
     const uint64_t stop = (rc == IMSAME_E_READ_TOO_LONG) ? st.err_read : q.n;
     uint64_t acc = 0;

@@ -411,3 +411,26 @@ def test_db_shards_min_merge_matches_whole(dev, oracle, world):
         rc, exp, _ = oracle.align(ref, rst, q, qs, None, T)
         assert rc == 0 and not _cmp(got, exp), _cmp(got, exp)
         assert (got["status"] == 1).sum() > 2_500
+
+
+@pytest.mark.parametrize("name", G.e2e_cases())
+def test_cli_sliced_matches_reference_golden(name):
+    """The CLI with -slice_bases (database indexed 3 kbp at a time) writes the
+    reference's .align bytes and [INFO] lines; inputs where the size abort
+    could fire are refused with a message instead."""
+    case = G.e2e_case(name)
+    db, dbs, _ = fasta.load(case["db"], True)
+    q, qs, _ = fasta.load(case["query"])
+    big = max(np.diff(np.append(dbs, len(db)).astype(np.int64)).max(initial=0),
+              np.diff(np.append(qs, len(q)).astype(np.int64)).max(initial=0)) > 3000
+    for T in case["meta"]["runs"]:
+        with tempfile.TemporaryDirectory() as td:
+            outp = os.path.join(td, "o.align")
+            p = subprocess.run([CLI, "-query", case["query"], "-db", case["db"], "-out", outp, "-n_threads", T,
+                                "-slice_bases", "3000", *case["meta"]["extra"]],
+                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=300)
+            if big:
+                assert p.returncode != 0 and b"-slice_bases" in p.stdout
+                continue
+            blob = open(outp, "rb").read() if os.path.exists(outp) else b""
+            G.check_cli_against_golden(case, int(T), p.returncode, p.stdout, blob)
