@@ -102,6 +102,7 @@ int main(int argc, char **argv) {
     t0 = now_s();
     host_seqs db, q;
     if (host_load_fasta(dpath, 1, &db)) terror("Could not open database file");
+    if (db.n == 0) slice_bases = 0;                  /* nothing to slice */
     rc = slice_bases ? IMSAME_OK : imsame_dev_index(ctx, db.seq, db.len, db.start, db.n, db.brk);
     if (rc) terror(imsame_strerror(rc));
     printf("[INFO] Database loaded and of length %" PRIu64 ". Hash table building took %e seconds\n", db.len,
