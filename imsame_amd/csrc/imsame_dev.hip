@@ -598,6 +598,8 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
         S.err = (unsigned long long *)(ctr + C_ERR); S.nhits = (unsigned long long *)(ctr + C_HITS);
         S.wcap = c->use_wcap ? c->wcap.as<uint64_t>() : nullptr;
         S.wstart = c->use_wstart ? c->wstart.as<uint64_t>() : nullptr;
+        S.minlen = c->minlen.as<uint32_t>(); S.n_minlen = ymax + 1;
+        S.minident = c->minident.as<uint32_t>(); S.n_minident = xcap + ymax + 2;
         const char *l_env = getenv(st.rounds == 1 && getenv("IMSAME_SEED_L1") ? "IMSAME_SEED_L1" : "IMSAME_SEED_L");
         const int L = l_env ? atoi(l_env) : seed_lanes(nact);
         const size_t slds = 256 * SEED_LDS_PER_LANE;

@@ -33,6 +33,8 @@ struct SeedLaunch {
     const uint64_t *wcap;                  // per read: scan windows p < wcap[k] only (NULL: no cap;
                                            // database slices, imsame_dev_align_sliced)
     const uint64_t *wstart;                // per read: first window scanned >= wstart[k] (NULL: none)
+    const uint32_t *minlen, *minident;     // acceptance tables of the launch (NULL: no a-priori rejection)
+    uint32_t n_minlen, n_minident;
     uint32_t *cread, *csid, *ncand;        // class 0: ylen <= short_ylen
     uint32_t *cread2, *csid2, *ncand2;     // class 1: longer reads
     unsigned long long *err;               // min (read << 32 | record)
@@ -123,6 +125,22 @@ __device__ __forceinline__ uint64_t ungapped_raw(const uint8_t *__restrict__ db,
     return (uint64_t)idents * IMSAME_POINT - (t_len - idents) * IMSAME_POINT;
 }
 
+// NW(record, read) cannot be accepted, whatever its path: acceptance
+// (alignmentFunctions.c:163) needs len >= minlen[ylen] and identities >=
+// minident[len], minident is nondecreasing in len, and identities <=
+// min(xlen, ylen) (build_alignment counts equal X/Y characters, each X and Y
+// base at most once, :254-258).  Such a hit is rejected without running NW --
+// the reference runs it and rejects it (C5: 10 kbp reads vs 2 kbp records).
+__device__ __forceinline__ bool nw_cannot_accept(const SeedLaunch &S, uint64_t xlen, uint64_t ylen) {
+    if (!S.minlen || ylen >= S.n_minlen) return false;
+    uint32_t l0 = S.minlen[ylen];
+    if (l0 == 0xFFFFFFFFu) return true;
+    l0 = l0 ? l0 : 1u;                                    // minident[0] never passes
+    if (l0 >= S.n_minident) return true;                  // longer than any path
+    const uint32_t mi = S.minident[l0];
+    return mi == 0xFFFFFFFFu || (uint64_t)mi > (xlen < ylen ? xlen : ylen);
+}
+
 __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint64_t &hits) {
     const uint64_t r = S.active[idx], k = r - S.read_from;
     const uint64_t rs = S.q_start[r], re = S.q_start[r + 1];
@@ -196,6 +214,7 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint
                     stop = true;
                     break;
                 }
+                if (nw_cannot_accept(S, xlen, ylen)) continue;       // NW would reject it
                 emit[ne++] = sid;
                 if (ne == spec) {
                     S.cur_p[k] = p; S.cur_h[k] = h + 1;              // resume after this hit
@@ -316,6 +335,7 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
                 if (mraw != ~0ull && raw >= mraw) {                      // e < min_e (:139)
                     const uint64_t xlen = S.db_start[sid + 1] - S.db_start[sid];
                     const bool bad = xlen > S.max_rs || ylen > S.max_rs;   // terror (:155) if reached
+                    if (!bad && nw_cannot_accept(S, xlen, ylen)) continue; // NW would reject it
                     lst[nl++] = make_uint2(sid, (uint32_t)(e - wbase) | (bad ? 0x80000000u : 0u));
                     last_rel = (uint32_t)(e - wbase);
                     if (bad || nl == need) { full = true; break; }

@@ -289,7 +289,9 @@ def test_c5_ont_long_reads_raised_cap(dev, oracle_memo, rec_bp, cap):
     rc, exp, _ = oracle_memo.align(ref, rst, q, qs, oracle_memo.params(max_read_size=cap), 8)
     assert rc == 0
     assert not _cmp(res, exp), _cmp(res, exp)
-    assert st.n_nw > 0
+    # 2 kbp records cannot give the 2500 identities a 10 kbp read needs: every
+    # candidate is rejected a priori (seed_kernel.hip:nw_cannot_accept)
+    assert (st.n_nw > 0) == (rec_bp > 10_000)
     if rec_bp > 10_000:
         assert (res["status"] == 1).sum() >= n // 2
     _, _, st3 = dev.align(n_threads=8, allow_too_long=True)

@@ -260,3 +260,20 @@ def test_thresholds_match_long_double_tests(emu, oracle):
             assert (num >= mc) == (num / den >= 0.5)
             if num <= den:
                 assert (num >= mi) == bool(oracle.lib.or_ident_ok(num, den, C.byref(p)))
+
+
+@pytest.mark.parametrize("rec_bp,expect_nw", [(300, False), (400, True)])
+def test_emulated_a_priori_rejection(emu, oracle, rec_bp, expect_nw):
+    """seed_kernel.hip:nw_cannot_accept -- with 1500 bp reads, acceptance
+    needs >= 0.5 * 0.5 * 1500 = 375 identities, more than a 300 bp record can
+    give, so every e-value-passing hit is rejected without NW (the oracle runs
+    and rejects each); at 400 bp records NW runs.  Results equal the oracle's."""
+    from tests import synth
+    ref, rst = synth.make_reference_arr(60_000, rec_bp, seed=13)
+    q, qs = synth.make_reads_arr(ref, 40, 1_500, seed=14)
+    rc1, r1, _ = oracle.align(ref, rst, q, qs, oracle.params(), 3)
+    rc2, r2, _, st = emu.align(ref, rst, q, qs, oracle.params(), 3)
+    assert rc1 == rc2 == 0
+    for f in PARITY_FIELDS:
+        assert np.array_equal(r1[f], r2[f]), f
+    assert (st.n_nw > 0) == expect_nw
