@@ -269,8 +269,8 @@ def test_emulated_a_priori_rejection(emu, oracle, rec_bp, expect_nw):
     give, so every e-value-passing hit is rejected without NW (the oracle runs
     and rejects each); at 400 bp records NW runs.  Results equal the oracle's."""
     from tests import synth
-    ref, rst = synth.make_reference_arr(60_000, rec_bp, seed=13)
-    q, qs = synth.make_reads_arr(ref, 40, 1_500, seed=14)
+    ref, rst = synth.make_reference_arr(24_000, rec_bp, seed=13)
+    q, qs = synth.make_reads_arr(ref, 6, 1_500, seed=14)
     rc1, r1, _ = oracle.align(ref, rst, q, qs, oracle.params(), 3)
     rc2, r2, _, st = emu.align(ref, rst, q, qs, oracle.params(), 3)
     assert rc1 == rc2 == 0
