@@ -58,6 +58,11 @@ def lib():
         L.imsame_dev_close.argtypes = [vp]
         L.imsame_dev_index.argtypes = [vp, vp, u64, vp, u64, vp]
         L.imsame_dev_set_query.argtypes = [vp, vp, u64, vp, u64]
+        L.imsame_dev_set_query_range.argtypes = [vp, vp, u64, vp, u64, u64, u64]
+        L.imsame_dev_fetch_paths.argtypes = [vp, vp, u64, C.POINTER(u64)]
+        L.imsame_host_alloc.restype = vp
+        L.imsame_host_alloc.argtypes = [u64]
+        L.imsame_host_free.argtypes = [vp]
         L.imsame_dev_align.argtypes = [vp, u64, u64, u64, C.POINTER(Params), vp, vp, u64, C.POINTER(u64),
                                        C.POINTER(Stats)]
         L.imsame_dev_align_windows.argtypes = [vp, u64, u64, u64, C.POINTER(Params), u64, vp, vp, vp, vp, vp, u64,
@@ -108,6 +113,30 @@ def _arr(a, dt):
     return np.ascontiguousarray(a, dtype=dt)
 
 
+class PinnedArray:
+    """numpy view of page-locked host memory (imsame_host_alloc): faster
+    H2D copies of query shards than pageable memory."""
+
+    def __init__(self, n, dtype=np.uint8):
+        self.nbytes = max(int(n) * np.dtype(dtype).itemsize, 1)
+        self._p = lib().imsame_host_alloc(self.nbytes)
+        if not self._p:
+            raise ImsameError(abi.IMSAME_E_OOM, "imsame_host_alloc")
+        self.array = np.ctypeslib.as_array((C.c_uint8 * self.nbytes).from_address(self._p)).view(dtype)[:n]
+
+    def free(self):
+        if getattr(self, "_p", None):
+            self.array = None
+            lib().imsame_host_free(self._p)
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
 class Device:
     """One HIP device context (imsame_ctx)."""
 
@@ -119,6 +148,7 @@ class Device:
             raise ImsameError(rc, f"imsame_dev_open({device})")
         self._h = h
         self._keep = []
+        self.q_range = (0, 0)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -155,18 +185,35 @@ class Device:
         if rc:
             raise ImsameError(rc, "imsame_dev_index")
 
-    def set_query(self, q_seq, q_starts):
+    def set_query(self, q_seq, q_starts, read_from=None, read_to=None):
+        """Upload the query; with read_from/read_to only that shard's reads
+        go to HBM (imsame_dev_set_query_range; chunk heads stay the whole
+        query's)."""
         q_seq, q_starts = _arr(q_seq, np.uint8), _arr(q_starts, np.uint64)
-        rc = lib().imsame_dev_set_query(self._h, q_seq.ctypes.data, len(q_seq), q_starts.ctypes.data,
-                                        len(q_starts))
+        a = 0 if read_from is None else read_from
+        b = len(q_starts) if read_to is None else read_to
+        rc = lib().imsame_dev_set_query_range(self._h, q_seq.ctypes.data, len(q_seq), q_starts.ctypes.data,
+                                              len(q_starts), a, b)
         if rc:
-            raise ImsameError(rc, "imsame_dev_set_query")
+            raise ImsameError(rc, "imsame_dev_set_query_range")
         self.n_q = len(q_starts)
+        self.q_range = (a, b)
 
-    def align(self, read_from=0, read_to=None, n_threads=4, params=None, want_paths=False, paths_cap=None,
+    def fetch_paths(self, cap):
+        """Paths of the last align call (after IMSAME_E_PATHS)."""
+        paths = np.zeros(max(cap, 1), dtype=np.uint32)
+        used = C.c_uint64()
+        rc = lib().imsame_dev_fetch_paths(self._h, paths.ctypes.data, cap, C.byref(used))
+        if rc:
+            raise ImsameError(rc, "imsame_dev_fetch_paths")
+        return paths[:used.value]
+
+    def align(self, read_from=None, read_to=None, n_threads=4, params=None, want_paths=False, paths_cap=None,
               allow_too_long=False):
-        """Per-read results (numpy RESULT_DTYPE) for reads [read_from, read_to)."""
-        read_to = self.n_q if read_to is None else read_to
+        """Per-read results (numpy RESULT_DTYPE) for reads [read_from, read_to)
+        (default: the uploaded range)."""
+        read_from = self.q_range[0] if read_from is None else read_from
+        read_to = self.q_range[1] if read_to is None else read_to
         p = params if params is not None else self.params()
         p.want_paths = 1 if want_paths else 0
         n = read_to - read_from
@@ -174,26 +221,24 @@ class Device:
         cap = (paths_cap if paths_cap is not None else 8 * n + 1024) if want_paths else 0
         st = Stats()
         used = C.c_uint64()
-        while True:
-            paths = np.zeros(max(cap, 1), dtype=np.uint32)
-            rc = lib().imsame_dev_align(self._h, read_from, read_to, n_threads, C.byref(p), res.ctypes.data,
-                                        paths.ctypes.data if want_paths else None, cap, C.byref(used),
-                                        C.byref(st))
-            if rc == abi.IMSAME_E_PATHS:
-                cap = int(used.value * 1.25) + 1024
-                continue
-            break
+        paths = np.zeros(max(cap, 1), dtype=np.uint32)
+        rc = lib().imsame_dev_align(self._h, read_from, read_to, n_threads, C.byref(p), res.ctypes.data,
+                                    paths.ctypes.data if want_paths else None, cap, C.byref(used), C.byref(st))
+        if rc == abi.IMSAME_E_PATHS:              # results complete; the paths wait on the device
+            paths = self.fetch_paths(used.value)
+            rc = 0
         if rc and not (rc == abi.IMSAME_E_READ_TOO_LONG and allow_too_long):
             raise ImsameError(rc, "imsame_dev_align")
         return res, paths[:used.value], st
 
-    def align_windows(self, ev_db_len, win_cap=None, read_from=0, read_to=None, n_threads=4, params=None,
+    def align_windows(self, ev_db_len, win_cap=None, read_from=None, read_to=None, n_threads=4, params=None,
                       allow_too_long=False, win_start=None):
         """align() on the loaded index as ONE SLICE of a database of
         ev_db_len bases: per-read window caps in, accept windows out
         (imsame_dev_align_windows).  Returns (res, win, stats); db_seq is
         slice-local."""
-        read_to = self.n_q if read_to is None else read_to
+        read_from = self.q_range[0] if read_from is None else read_from
+        read_to = self.q_range[1] if read_to is None else read_to
         p = params if params is not None else self.params()
         p.want_paths = 0
         n = read_to - read_from
@@ -210,31 +255,30 @@ class Device:
             raise ImsameError(rc, "imsame_dev_align_windows")
         return res, win, st
 
-    def align_sliced(self, db_seq, db_starts, slice_bases, db_brk=None, read_from=0, read_to=None, n_threads=4,
+    def align_sliced(self, db_seq, db_starts, slice_bases, db_brk=None, read_from=None, read_to=None, n_threads=4,
                      params=None, want_paths=False, paths_cap=None):
         """align() against db_seq indexed and searched in slices of at most
         slice_bases bases, one slice's index in HBM at a time
         (imsame_dev_align_sliced).  Returns (res, paths, stats, n_slices)."""
         db_seq, db_starts = _arr(db_seq, np.uint8), _arr(db_starts, np.uint64)
         brk = None if db_brk is None else _arr(db_brk, np.uint8)
-        read_to = self.n_q if read_to is None else read_to
+        read_from = self.q_range[0] if read_from is None else read_from
+        read_to = self.q_range[1] if read_to is None else read_to
         p = params if params is not None else self.params()
         p.want_paths = 1 if want_paths else 0
         n = read_to - read_from
         res = np.zeros(n, dtype=RESULT_DTYPE)
         cap = (paths_cap if paths_cap is not None else 8 * n + 1024) if want_paths else 0
         st, used, ns = Stats(), C.c_uint64(), C.c_uint64()
-        while True:
-            paths = np.zeros(max(cap, 1), dtype=np.uint32)
-            rc = lib().imsame_dev_align_sliced(self._h, db_seq.ctypes.data, len(db_seq), db_starts.ctypes.data,
-                                               len(db_starts), None if brk is None else brk.ctypes.data,
-                                               slice_bases, read_from, read_to, n_threads, C.byref(p),
-                                               res.ctypes.data, paths.ctypes.data if want_paths else None, cap,
-                                               C.byref(used), C.byref(ns), C.byref(st))
-            if rc == abi.IMSAME_E_PATHS:
-                cap = int(max(used.value, cap) * 2) + 1024
-                continue
-            break
+        paths = np.zeros(max(cap, 1), dtype=np.uint32)
+        rc = lib().imsame_dev_align_sliced(self._h, db_seq.ctypes.data, len(db_seq), db_starts.ctypes.data,
+                                           len(db_starts), None if brk is None else brk.ctypes.data,
+                                           slice_bases, read_from, read_to, n_threads, C.byref(p),
+                                           res.ctypes.data, paths.ctypes.data if want_paths else None, cap,
+                                           C.byref(used), C.byref(ns), C.byref(st))
+        if rc == abi.IMSAME_E_PATHS:
+            paths = self.fetch_paths(used.value)
+            rc = 0
         if rc:
             raise ImsameError(rc, "imsame_dev_align_sliced")
         return res, paths[:used.value], st, ns.value

@@ -22,6 +22,7 @@ MAX_READ_SIZE = 3000
 ALIGN_LEN = 60
 
 MOVE_DIAG, MOVE_UP, MOVE_LEFT = 0, 1, 2
+LAUNCH_STATS = 16        # IMSAME_LAUNCH_STATS
 
 
 class Params(C.Structure):
@@ -71,10 +72,18 @@ class Stats(C.Structure):
         ("err_read", C.c_uint64), ("err_dbseq", C.c_uint64),
         ("ms_seed", C.c_double), ("ms_nw", C.c_double), ("ms_total", C.c_double),
         ("nw_launch_ms", C.c_double), ("nw_launches", C.c_uint64), ("nw_bytes", C.c_uint64),
+        ("launch_cand", C.c_uint64 * LAUNCH_STATS), ("launch_ms", C.c_double * LAUNCH_STATS),
+        ("n_rewalk", C.c_uint64),
     ]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        d = {}
+        for k, _ in self._fields_:
+            v = getattr(self, k)
+            d[k] = list(v) if k.startswith("launch_") else v
+        k = min(self.nw_launches, LAUNCH_STATS)
+        d["launch_cand"], d["launch_ms"] = d["launch_cand"][:k], d["launch_ms"][:k]
+        return d
 
 
 def default_params():

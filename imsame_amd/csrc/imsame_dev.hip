@@ -201,10 +201,13 @@ struct imsame_ctx {
     uint32_t max_rec = 0;
     std::vector<uint64_t> h_db_start;
     bool have_index = false;
-    // query
+    // query: reads [q_lo, q_hi) of a query of n_q reads / q_len bases are in
+    // HBM (imsame_dev_set_query_range); q holds bases [q_base, ...), q_start
+    // the starts of reads q_lo .. q_hi.  Kernels index both with GLOBAL read
+    // and base numbers through the biased views dev_q / dev_qs.
     DBuf q, q_start;
-    uint64_t n_q = 0, q_len = 0;
-    std::vector<uint64_t> h_q_start;
+    uint64_t n_q = 0, q_len = 0, q_lo = 0, q_hi = 0, q_base = 0, q_lo_first = 0;
+    std::vector<uint64_t> h_q_start;  // starts of reads q_lo .. q_hi
     bool have_query = false;
     bool q_len_mult = false;         // every read length is a multiple of NW16_K
     // per-read state
@@ -215,8 +218,13 @@ struct imsame_ctx {
     DBuf ctr;
     // tables
     DBuf minraw, minlen, minident;
-    // NW scratch
+    // NW scratch; the path arena of the last align (device, or host for the
+    // sliced form) until imsame_dev_fetch_paths
     DBuf tb, bnd, paths;
+    uint64_t paths_cap_dev = 0, paths_n = 0;
+    double paths_hint = 0;     // path entries per read of the last call
+    std::vector<uint32_t> paths_host;
+    bool paths_on_host = false;
     // revcomp
     DBuf rc_in, rc_out, rc_a, rc_b, rc_c;
     // database slices (imsame_dev_align_sliced): the e-value's L_DB is the
@@ -225,6 +233,16 @@ struct imsame_ctx {
     bool use_wcap = false, use_wstart = false;
     DBuf wcap, wout, wstart;
 };
+
+static inline uint64_t hqs(const imsame_ctx *c, uint64_t r) { return c->h_q_start[r - c->q_lo]; }
+// biased views: valid for the uploaded reads (and QPAD bases before them)
+static inline const uint8_t *dev_q(const imsame_ctx *c) { return (const uint8_t *)((uintptr_t)c->q.p - c->q_base); }
+static inline const uint64_t *dev_qs(const imsame_ctx *c) {
+    return (const uint64_t *)((uintptr_t)c->q_start.p - c->q_lo * sizeof(uint64_t));
+}
+// bases uploaded before a range's first read: the borrowed base (Q4) and the
+// 16-byte chunk loads of the ungapped extension reach back <= 18 bases
+#define QPAD 64
 
 // counters block layout (u64 slots)
 enum { C_NCAND = 0, C_NCAND2, C_NNEXT, C_WORK, C_WORK2, C_PATHS, C_FLAGS, C_ERR, C_HITS, C_CELLS, C_NACC, C_NSLOTS };
@@ -400,23 +418,49 @@ extern "C" int imsame_dev_index(imsame_ctx *c, const uint8_t *db_seq, uint64_t d
     return IMSAME_OK;
 }
 
-extern "C" int imsame_dev_set_query(imsame_ctx *c, const uint8_t *q_seq, uint64_t q_len, const uint64_t *q_start,
-                                    uint64_t n_q) {
-    if (!c || (q_len && !q_seq) || (n_q && !q_start)) return IMSAME_E_ARG;
+extern "C" int imsame_dev_set_query_range(imsame_ctx *c, const uint8_t *q_seq, uint64_t q_len,
+                                          const uint64_t *q_start, uint64_t n_q, uint64_t read_from,
+                                          uint64_t read_to) {
+    if (!c || (q_len && !q_seq) || (n_q && !q_start) || read_from > read_to || read_to > n_q) return IMSAME_E_ARG;
     if (n_q >= 0xFFFFFFF0ull) return IMSAME_E_ARG;
     HIPCHK(hipSetDevice(c->device));
     c->have_query = false;
-    c->n_q = n_q; c->q_len = q_len;
-    c->h_q_start.assign(q_start, q_start + n_q);
-    c->h_q_start.push_back(q_len);
+    auto qs = [&](uint64_t r) { return r < n_q ? q_start[r] : q_len; };
+    for (uint64_t r = read_from; r < read_to; ++r)
+        if (qs(r) > qs(r + 1) || qs(r + 1) > q_len) return IMSAME_E_ARG;       // starts ascend within the query
+    c->n_q = n_q; c->q_len = q_len; c->q_lo = read_from; c->q_hi = read_to;
+    c->h_q_start.resize(read_to - read_from + 1);
+    for (uint64_t r = read_from; r <= read_to; ++r) c->h_q_start[r - read_from] = qs(r);
+    // reads q_lo_first .. read_from-1 are empty (start where read_from starts)
+    uint64_t f = read_from;
+    while (f > 0 && qs(f - 1) == qs(read_from)) --f;
+    c->q_lo_first = f;
+    const uint64_t b0 = qs(read_from), b1 = qs(read_to);
+    c->q_base = b0 > QPAD ? b0 - QPAD : 0;
+    const uint64_t nb = b1 - c->q_base, ns = read_to - read_from + 1;
     c->q_len_mult = true;
-    for (uint64_t r = 0; r < n_q; ++r) c->q_len_mult = c->q_len_mult && (c->h_q_start[r + 1] - c->h_q_start[r]) % NW16_K == 0;
-    if (c->q.ensure(q_len + 64) || c->q_start.ensure((n_q + 1) * 8)) return IMSAME_E_OOM;
-    if (q_len) HIPCHK(hipMemcpyAsync(c->q.p, q_seq, q_len, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(c->q_start.p, c->h_q_start.data(), (n_q + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    for (uint64_t r = read_from; r < read_to; ++r) c->q_len_mult = c->q_len_mult && (qs(r + 1) - qs(r)) % NW16_K == 0;
+    if (c->q.ensure(nb + 64) || c->q_start.ensure(ns * 8)) return IMSAME_E_OOM;
+    if (nb) HIPCHK(hipMemcpyAsync(c->q.p, q_seq + c->q_base, nb, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemsetAsync((uint8_t *)c->q.p + nb, 0, 64, c->stream));
+    HIPCHK(hipMemcpyAsync(c->q_start.p, c->h_q_start.data(), ns * 8, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     c->have_query = true;
     return IMSAME_OK;
+}
+
+extern "C" int imsame_dev_set_query(imsame_ctx *c, const uint8_t *q_seq, uint64_t q_len, const uint64_t *q_start,
+                                    uint64_t n_q) {
+    return imsame_dev_set_query_range(c, q_seq, q_len, q_start, n_q, 0, n_q);
+}
+
+extern "C" void *imsame_host_alloc(uint64_t bytes) {
+    void *p = nullptr;
+    return hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) == hipSuccess ? p : nullptr;
+}
+
+extern "C" void imsame_host_free(void *p) {
+    if (p) (void)hipHostFree(p);
 }
 
 static int build_tables(imsame_ctx *c, const imsame_params *p, uint32_t ymax, uint32_t xmax) {
@@ -513,10 +557,83 @@ static int launch_nw(imsame_ctx *c, const NwPlan &pl, const uint32_t *cread, con
 
 static int paths_setup(imsame_ctx *c, const imsame_params *p, uint64_t paths_cap, uint32_t *cap32) {
     *cap32 = 0;
+    c->paths_cap_dev = 0;
     if (p->want_paths) {
         *cap32 = (uint32_t)std::min<uint64_t>(paths_cap, 0xFFFFFFF0u);
         if (c->paths.ensure((uint64_t)*cap32 * 4 + 16)) return IMSAME_E_OOM;
+        c->paths_cap_dev = *cap32;
     }
+    return 0;
+}
+
+// grow the device path arena to `need` entries, keeping entries [0, keep)
+static int paths_grow(imsame_ctx *c, uint64_t keep, uint64_t need) {
+    if (need > 0xFFFFFFF0ull) return IMSAME_E_OOM;                  // u32 path offsets
+    if (need <= c->paths_cap_dev) return 0;
+    DBuf nb;
+    if (nb.ensure(need * 4 + 16)) return IMSAME_E_OOM;
+    if (keep) HIPCHK(hipMemcpyAsync(nb.p, c->paths.p, keep * 4, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->paths.release();
+    c->paths.p = nb.p; c->paths.cap = nb.cap;
+    nb.p = nullptr; nb.cap = 0;
+    c->paths_cap_dev = need;
+    return 0;
+}
+
+// Accepted reads whose path did not fit the device arena (path_off ~0,
+// path_len = entries needed).  NW + backtracking is a pure function of
+// (record, read), so re-running exactly those pairs
+// with room for their paths gives the same rows plus the paths -- instead of
+// re-running the whole alignment.  Appends after entry *used.
+static int rewalk_lost(imsame_ctx *c, const imsame_params *p, uint64_t read_from, uint32_t n,
+                       imsame_read_result *res, uint32_t ymax, uint32_t xcap, uint32_t ycap, uint32_t short_y,
+                       uint64_t *used, imsame_stats *st) {
+    std::vector<uint32_t> rd[2], sid[2], kk[2];
+    uint64_t need = 0;
+    for (uint32_t k = 0; k < n; ++k) {
+        if (res[k].status != 1 || res[k].path_off != 0xFFFFFFFFu) continue;
+        const int cl = res[k].ylen <= short_y ? 0 : 1;
+        rd[cl].push_back((uint32_t)(read_from + k)); sid[cl].push_back((uint32_t)res[k].db_seq); kk[cl].push_back(k);
+        need += res[k].path_len;
+    }
+    if (rd[0].empty() && rd[1].empty()) return 0;      // only discarded speculative candidates lost theirs
+    const uint64_t base = *used, cap = base + need + 16;
+    int rc = paths_grow(c, base, cap);
+    if (rc) return rc;
+    hipStream_t s = c->stream;
+    uint64_t *ctr = c->ctr.as<uint64_t>();
+    const uint64_t zero = 0;
+    HIPCHK(hipMemcpyAsync(ctr + C_PATHS, &base, 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(ctr + C_FLAGS, &zero, 8, hipMemcpyHostToDevice, s));
+    for (int cl = 0; cl < 2; ++cl) {
+        const uint32_t m = (uint32_t)rd[cl].size();
+        if (!m) continue;
+        HIPCHK(hipMemcpyAsync(c->cread.p, rd[cl].data(), (uint64_t)m * 4, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(c->csid.p, sid[cl].data(), (uint64_t)m * 4, hipMemcpyHostToDevice, s));
+        NwPlan pl;
+        if ((rc = plan_nw(c, cl ? ycap : short_y, xcap, m, p, c->q_len_mult, &pl))) return rc;
+        double ms = 0;
+        rc = launch_nw(c, pl, c->cread.as<uint32_t>(), c->csid.as<uint32_t>(), m, c->cout.as<imsame_read_result>(),
+                       p->igap, p->egap, p, ymax, xcap, (uint32_t *)(ctr + C_WORK), c->db.as<uint8_t>(),
+                       c->db_start.as<uint64_t>(), dev_q(c), dev_qs(c), (uint32_t)cap, &ms);
+        if (rc) return rc;
+        std::vector<imsame_read_result> o(m);
+        HIPCHK(hipMemcpyAsync(o.data(), c->cout.p, (uint64_t)m * 64, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        for (uint32_t j = 0; j < m; ++j) {
+            imsame_read_result &r = res[kk[cl][j]];
+            if (o[j].status != 1 || o[j].path_off == 0xFFFFFFFFu || o[j].db_seq != r.db_seq || o[j].score != r.score ||
+                o[j].length != r.length || o[j].identities != r.identities || o[j].head_x != r.head_x)
+                return IMSAME_E_STATE;                                   // NW is pure: cannot differ
+            r.path_off = o[j].path_off; r.path_len = o[j].path_len;
+        }
+        st->n_rewalk += m;
+    }
+    uint64_t u = 0;
+    HIPCHK(hipMemcpyAsync(&u, ctr + C_PATHS, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    *used = (uint32_t)u;
     return 0;
 }
 
@@ -526,8 +643,8 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
     const double t_start = now_ms();
     if (!c || !p || (!res && read_to > read_from)) return IMSAME_E_ARG;
     if (!c->have_index || !c->have_query) return IMSAME_E_STATE;
-    if (read_to > c->n_q || read_from > read_to) return IMSAME_E_ARG;
-    if (p->want_paths && !paths) return IMSAME_E_ARG;
+    if (read_from < c->q_lo || read_to > c->q_hi || read_from > read_to) return IMSAME_E_ARG;
+    if (p->want_paths && !paths && paths_cap) return IMSAME_E_ARG;
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     const uint32_t n = (uint32_t)(read_to - read_from);
@@ -536,18 +653,21 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
     st.n_reads = n;
     st.err_read = ~0ull;
     if (paths_used) *paths_used = 0;
+    c->paths_n = 0; c->paths_on_host = false;
     // shapes
     uint32_t ymax = 0;
-    for (uint64_t r = read_from; r < read_to; ++r)
-        ymax = (uint32_t)std::max<uint64_t>(ymax, c->h_q_start[r + 1] - c->h_q_start[r]);
+    for (uint64_t r = read_from; r < read_to; ++r) ymax = (uint32_t)std::max<uint64_t>(ymax, hqs(c, r + 1) - hqs(c, r));
     const uint32_t xcap = (uint32_t)std::min<uint64_t>(c->max_rec, p->max_read_size);
     const uint32_t ycap = (uint32_t)std::min<uint64_t>(ymax, p->max_read_size);
     if (!imsame_gaps_in_range(p->igap, p->egap, xcap, ycap)) return IMSAME_E_RANGE;
     if (std::max(xcap, ycap) > 0x3FFF) return IMSAME_E_ARG;       // 14-bit traceback coordinates
     int rc = build_tables(c, p, ymax, xcap);
     if (rc) return rc;
+    // device path arena: what the caller offers, or what the last call needed per read
     uint32_t pcap = 0;
-    if ((rc = paths_setup(c, p, paths_cap, &pcap))) return rc;
+    const uint64_t want_cap = std::max<uint64_t>(std::max<uint64_t>(paths_cap, 2ull * n + 1024),
+                                                 (uint64_t)(c->paths_hint * 1.25 * n) + 1024);
+    if ((rc = paths_setup(c, p, want_cap, &pcap))) return rc;
     if (n == 0) { if (stats) *stats = st; return IMSAME_OK; }
     if (c->res.ensure((uint64_t)n * 64) || c->cur_p.ensure((uint64_t)n * 8) || c->cur_h.ensure((uint64_t)n * 4) ||
         c->memo.ensure((uint64_t)n * 4 * MEMO) || c->nmemo.ensure(n) || c->rstat.ensure(n) ||
@@ -562,11 +682,13 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
     const uint32_t spec_later = spec_env ? (uint32_t)std::max(1, std::min(SPEC_MAX, atoi(spec_env))) : (uint32_t)SPEC_MAX;
     const char *bud_env = getenv("IMSAME_SEED_BUDGET");
     const uint32_t budget1 = bud_env ? (uint32_t)std::max(0, atoi(bud_env)) : SEED_BUDGET1;
+    const uint8_t *qd = dev_q(c);
+    const uint64_t *qsd = dev_qs(c);
     uint64_t *ctr = c->ctr.as<uint64_t>();
     HIPCHK(hipMemsetAsync(ctr, 0, C_NSLOTS * 8, s));
     const unsigned long long errinit = ~0ull;
     HIPCHK(hipMemcpyAsync(ctr + C_ERR, &errinit, 8, hipMemcpyHostToDevice, s));
-    InitLaunch I = {c->q_start.as<uint64_t>(), read_from, n, c->res.as<imsame_read_result>(), c->cur_p.as<uint64_t>(),
+    InitLaunch I = {qsd, read_from, n, c->res.as<imsame_read_result>(), c->cur_p.as<uint64_t>(),
                     c->cur_h.as<uint32_t>(), c->nmemo.as<uint8_t>(), c->rstat.as<uint8_t>(), c->act0.as<uint32_t>()};
     init_kernel<<<nblk(n, 256), 256, 0, s>>>(I);
     HIPCHK(hipGetLastError());
@@ -579,7 +701,8 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
         HIPCHK(hipMemsetAsync(ctr + C_NCAND, 0, 3 * 8, s));     // NCAND, NCAND2, NNEXT
         SeedLaunch S;
         S.db = c->db.as<uint8_t>(); S.db_start = c->db_start.as<uint64_t>(); S.n_db = c->n_db; S.db_len = c->db_len;
-        S.q = c->q.as<uint8_t>(); S.q_start = c->q_start.as<uint64_t>(); S.n_q = c->n_q; S.q_len = c->q_len;
+        S.q = qd; S.q_start = qsd; S.n_q = c->n_q; S.q_len = c->q_len;
+        S.qs_lo = c->q_lo; S.qs_lo_first = c->q_lo_first;
         S.off = c->off.as<uint64_t>(); S.ent = c->ent.as<uint2>();
         S.active = act; S.n_active = nact;
         S.read_from = read_from;
@@ -627,9 +750,13 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
             if ((rc = plan_nw(c, cls[k].ylim, xcap, cls[k].n, p, c->q_len_mult, &pl))) return rc;
             double ms = 0;
             rc = launch_nw(c, pl, cls[k].cr, cls[k].cs, cls[k].n, cls[k].o, p->igap, p->egap, p, ymax, xcap,
-                           (uint32_t *)(ctr + cls[k].work), c->db.as<uint8_t>(), c->db_start.as<uint64_t>(),
-                           c->q.as<uint8_t>(), c->q_start.as<uint64_t>(), pcap, &ms);
+                           (uint32_t *)(ctr + cls[k].work), c->db.as<uint8_t>(), c->db_start.as<uint64_t>(), qd, qsd,
+                           pcap, &ms);
             if (rc) return rc;
+            if (st.nw_launches < IMSAME_LAUNCH_STATS) {
+                st.launch_cand[st.nw_launches] = cls[k].n;
+                st.launch_ms[st.nw_launches] = ms;
+            }
             st.ms_nw += ms; st.nw_launches++; st.n_nw += cls[k].n;
             UpdLaunch U = {cls[k].cr, cls[k].cs, cls[k].n, cls[k].o, read_from, c->res.as<imsame_read_result>(),
                            c->rstat.as<uint8_t>(), c->memo.as<uint32_t>(), c->nmemo.as<uint8_t>(),
@@ -675,9 +802,15 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
         ret = IMSAME_E_READ_TOO_LONG;
     }
     if (p->want_paths) {
-        const uint64_t used = (uint32_t)hc[C_PATHS];
+        uint64_t used = std::min<uint64_t>((uint32_t)hc[C_PATHS], pcap);
+        if (hc[C_FLAGS] & 1) {
+            rc = rewalk_lost(c, p, read_from, n, res, ymax, xcap, ycap, short_y, &used, &st);
+            if (rc) return rc;
+        }
+        c->paths_n = used;
+        c->paths_hint = std::min(64.0, (double)used / n);
         if (paths_used) *paths_used = used;
-        if (hc[C_FLAGS] & 1) { if (ret == IMSAME_OK) ret = IMSAME_E_PATHS; }
+        if (used > paths_cap) { if (ret == IMSAME_OK) ret = IMSAME_E_PATHS; }
         else if (used) {
             HIPCHK(hipMemcpyAsync(paths, c->paths.p, used * 4, hipMemcpyDeviceToHost, s));
             HIPCHK(hipStreamSynchronize(s));
@@ -686,6 +819,22 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
     st.ms_total = now_ms() - t_start;
     if (stats) *stats = st;
     return ret;
+}
+
+extern "C" int imsame_dev_fetch_paths(imsame_ctx *c, uint32_t *paths, uint64_t paths_cap, uint64_t *paths_used) {
+    if (!c) return IMSAME_E_ARG;
+    if (paths_used) *paths_used = c->paths_n;
+    if (c->paths_n > paths_cap) return IMSAME_E_PATHS;
+    if (!c->paths_n) return IMSAME_OK;
+    if (!paths) return IMSAME_E_ARG;
+    if (c->paths_on_host) {
+        memcpy(paths, c->paths_host.data(), c->paths_n * 4);
+        return IMSAME_OK;
+    }
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpyAsync(paths, c->paths.p, c->paths_n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return IMSAME_OK;
 }
 
 // Unit-level entry: NW + backtrack + acceptance for explicit (X_k, Y_k) pairs
@@ -714,7 +863,7 @@ extern "C" int imsame_dev_align_windows(imsame_ctx *c, uint64_t read_from, uint6
                                         imsame_stats *stats) {
     if (!c || !p || (read_to > read_from && (!res || !win))) return IMSAME_E_ARG;
     if (!c->have_index || !c->have_query) return IMSAME_E_STATE;
-    if (read_to > c->n_q || read_from > read_to) return IMSAME_E_ARG;
+    if (read_from < c->q_lo || read_to > c->q_hi || read_from > read_to) return IMSAME_E_ARG;
     HIPCHK(hipSetDevice(c->device));
     const uint32_t n = (uint32_t)(read_to - read_from);
     if (c->wcap.ensure((uint64_t)n * 8 + 8) || c->wout.ensure((uint64_t)n * 8 + 8) ||
@@ -726,19 +875,20 @@ extern "C" int imsame_dev_align_windows(imsame_ctx *c, uint64_t read_from, uint6
     HIPCHK(hipMemsetAsync(c->wout.p, 0xFF, (uint64_t)n * 8, c->stream));
     uint64_t ymax = 0;
     for (uint64_t r = read_from; r < read_to; ++r)
-        ymax = std::max<uint64_t>(ymax, c->h_q_start[r + 1] - c->h_q_start[r]);
+        ymax = std::max<uint64_t>(ymax, hqs(c, r + 1) - hqs(c, r));
     c->ev_db_len = ev_db_len;
     c->use_wcap = true;
     c->use_wstart = win_start != nullptr;
     int rc = imsame_dev_align(c, read_from, read_to, n_threads_semantic, p, res, paths, paths_cap, paths_used, stats);
     c->ev_db_len = 0;
     c->use_wcap = c->use_wstart = false;
-    if (n && (rc == IMSAME_OK || rc == IMSAME_E_READ_TOO_LONG)) {
+    if (n && (rc == IMSAME_OK || rc == IMSAME_E_READ_TOO_LONG || rc == IMSAME_E_PATHS)) {
         // window of each accepted hit (same read-start logic and cap as the pass)
         SeedLaunch S;
         memset(&S, 0, sizeof S);
         S.db = c->db.as<uint8_t>(); S.db_start = c->db_start.as<uint64_t>(); S.n_db = c->n_db; S.db_len = c->db_len;
-        S.q = c->q.as<uint8_t>(); S.q_start = c->q_start.as<uint64_t>(); S.n_q = c->n_q; S.q_len = c->q_len;
+        S.q = dev_q(c); S.q_start = dev_qs(c); S.n_q = c->n_q; S.q_len = c->q_len;
+        S.qs_lo = c->q_lo; S.qs_lo_first = c->q_lo_first;
         S.off = c->off.as<uint64_t>(); S.ent = c->ent.as<uint2>();
         S.read_from = read_from;
         S.T = n_threads_semantic ? n_threads_semantic : 1;
@@ -763,7 +913,8 @@ extern "C" int imsame_dev_align_sliced(imsame_ctx *c, const uint8_t *db_seq, uin
     const double t_start = now_ms();
     if (!c || !p || (!res && read_to > read_from) || (n_db && !db_start) || (db_len && !db_seq)) return IMSAME_E_ARG;
     if (!c->have_query) return IMSAME_E_STATE;
-    if (read_to > c->n_q || read_from > read_to || n_db == 0 || slice_bases == 0) return IMSAME_E_ARG;
+    if (read_from < c->q_lo || read_to > c->q_hi || read_from > read_to || n_db == 0 || slice_bases == 0)
+        return IMSAME_E_ARG;
     if (p->want_paths && !paths) return IMSAME_E_ARG;
     // the size error aborts the reference at its first e-value pass in visiting
     // order; slices would see such hits out of order, so the sliced path takes
@@ -772,7 +923,7 @@ extern "C" int imsame_dev_align_sliced(imsame_ctx *c, const uint8_t *db_seq, uin
     uint64_t max_rec = 0, ymax = 0;
     for (uint64_t k = 0; k < n_db; ++k) max_rec = std::max<uint64_t>(max_rec, rec_end(k) - db_start[k]);
     for (uint64_t r = read_from; r < read_to; ++r)
-        ymax = std::max<uint64_t>(ymax, c->h_q_start[r + 1] - c->h_q_start[r]);
+        ymax = std::max<uint64_t>(ymax, hqs(c, r + 1) - hqs(c, r));
     if (max_rec > p->max_read_size || ymax > p->max_read_size) return IMSAME_E_ARG;
     // slices: record ranges [lo, hi), top down, each <= slice_bases (>= 1 record)
     std::vector<std::pair<uint64_t, uint64_t>> sl;
@@ -798,10 +949,11 @@ extern "C" int imsame_dev_align_sliced(imsame_ctx *c, const uint8_t *db_seq, uin
     // be scanned over all windows before a cap exists.)
     const uint64_t BAND = 8;
     std::vector<uint64_t> cap(n), wstart(n), wout(n);
-    for (uint32_t r = 0; r < n; ++r) cap[r] = c->h_q_start[read_from + r] + IMSAME_FIXED_K - 1 + BAND;
+    for (uint32_t r = 0; r < n; ++r) cap[r] = hqs(c, read_from + r) + IMSAME_FIXED_K - 1 + BAND;
     std::vector<imsame_read_result> tmp(n);
     std::vector<uint64_t> st_rebased;
     std::vector<uint8_t> brk;
+    std::vector<uint32_t> acc;
     uint64_t used = 0;
     int ret = IMSAME_OK;
     for (int phase = 0; phase < 2 && ret == IMSAME_OK; ++phase) {
@@ -834,11 +986,16 @@ extern "C" int imsame_dev_align_sliced(imsame_ctx *c, const uint8_t *db_seq, uin
             if (rc) return rc;
             imsame_stats st;
             uint64_t pu = 0;
+            // this slice's paths are appended to the host-side arena acc
             rc = imsame_dev_align_windows(c, read_from, read_to, n_threads_semantic, p, db_len,
                                           phase ? wstart.data() : nullptr, cap.data(), tmp.data(), wout.data(),
-                                          p->want_paths ? paths + used : nullptr, p->want_paths ? paths_cap - used : 0,
-                                          &pu, &st);
+                                          nullptr, 0, &pu, &st);
+            if (rc == IMSAME_E_PATHS) {
+                acc.resize(used + pu);
+                rc = imsame_dev_fetch_paths(c, acc.data() + used, pu, &pu);
+            }
             if (rc) { ret = rc; break; }
+            tot.n_rewalk += st.n_rewalk;
             tot.n_nw += st.n_nw; tot.nw_cells += st.nw_cells; tot.n_hits += st.n_hits; tot.rounds += st.rounds;
             tot.ms_seed += st.ms_seed; tot.ms_nw += st.ms_nw; tot.nw_launches += st.nw_launches;
             tot.nw_bytes += st.nw_bytes;
@@ -854,7 +1011,13 @@ extern "C" int imsame_dev_align_sliced(imsame_ctx *c, const uint8_t *db_seq, uin
             used += pu;
         }
     }
+    c->paths_host.swap(acc);
+    c->paths_n = used; c->paths_on_host = true;
     if (paths_used) *paths_used = used;
+    if (p->want_paths && ret == IMSAME_OK) {
+        if (used > paths_cap) ret = IMSAME_E_PATHS;                  // imsame_dev_fetch_paths
+        else if (used) memcpy(paths, c->paths_host.data(), used * 4);
+    }
     for (uint32_t r = 0; r < n; ++r) tot.n_accepted += res[r].status == 1;
     tot.nw_launch_ms = tot.nw_launches ? tot.ms_nw / tot.nw_launches : 0;
     tot.ms_total = now_ms() - t_start;

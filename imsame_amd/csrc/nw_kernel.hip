@@ -341,6 +341,9 @@ __device__ void nw_finish(const NwLaunch &P, const TB &acc32, const int xlen, co
             const bool ok = want && off != 0xFFFFFFFFu;
             nw_walk(acc32, xlen, ylen, bx, by, ok, gg, gl, G, ok ? P.paths + off : nullptr, true);
             if (ok) { poff = off; plen = (uint32_t)w.nent; }
+            // arena full: the path is LOST (path_off ~0) and path_len says how
+            // many entries it needs; the host re-walks exactly these pairs
+            else if (want) { poff = 0xFFFFFFFFu; plen = (uint32_t)w.nent; }
         }
         if (cvalid && gl == 0) {
             const int M = 2 * max(xlen, ylen);

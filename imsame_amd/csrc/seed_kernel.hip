@@ -22,6 +22,8 @@ struct SeedLaunch {
     const uint64_t *off; const uint2 *ent;        // CSR {pos - record start, record}, buckets in descending pos
     const uint32_t *active; uint32_t n_active;
     uint64_t read_from, rpt, T;
+    uint64_t qs_lo, qs_lo_first;          // q_start holds reads >= qs_lo (a shard upload); reads
+                                          // qs_lo_first .. qs_lo-1 are empty (see is_chunk_head)
     uint64_t *cur_p; uint32_t *cur_h; uint32_t *memo; uint8_t *nmemo; uint8_t *rstat;
     const uint64_t *minraw; uint32_t n_minraw;
     uint64_t max_rs; uint32_t short_ylen;
@@ -125,6 +127,18 @@ __device__ __forceinline__ uint64_t ungapped_raw(const uint8_t *__restrict__ db,
     return (uint64_t)idents * IMSAME_POINT - (t_len - idents) * IMSAME_POINT;
 }
 
+// Chunk heads (IMSAME.c:414,430-452): read r opens its
+// chunk iff it starts where the chunk's first read from_c = i*floor(n/T)
+// starts (empty reads in between hand the role on).  A shard upload holds the
+// starts of reads >= qs_lo only; for from_c < qs_lo, q_start[from_c] == rs
+// iff q_start[from_c] == q_start[qs_lo] (every read from_c .. qs_lo-1 empty,
+// i.e. from_c >= qs_lo_first, computed on the host) and rs == q_start[qs_lo].
+__device__ __forceinline__ bool is_chunk_head(const SeedLaunch &S, uint64_t r, uint64_t rs) {
+    const uint64_t from_c = (S.rpt == 0) ? 0 : min(r / S.rpt, S.T - 1) * S.rpt;
+    if (from_c >= S.qs_lo) return S.q_start[from_c] == rs;
+    return from_c >= S.qs_lo_first && rs == S.q_start[S.qs_lo];
+}
+
 // NW(record, read) cannot be accepted, whatever its path: acceptance
 // (alignmentFunctions.c:163) needs len >= minlen[ylen] and identities >=
 // minident[len], minident is nondecreasing in len, and identities <=
@@ -149,8 +163,7 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint
     // the previous read's last base (the skip at :96-105 does not advance
     // curr_pos) unless it opens its chunk; an empty chunk-opening read (UB in
     // the reference) hands that role to the next read.
-    const uint64_t from_c = (S.rpt == 0) ? 0 : min(r / S.rpt, S.T - 1) * S.rpt;
-    const bool head = S.q_start[from_c] == rs;
+    const bool head = is_chunk_head(S, r, rs);
     const uint64_t p0 = rs - (head ? 0 : 1);
     uint64_t up_to = (r + 1 < S.n_q) ? (re ? re - 1 : 0) : S.q_len;          // :93
     if (S.wcap) up_to = min(up_to, S.wcap[k]);
@@ -293,8 +306,7 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
     if (gvalid) {
         r = S.active[gidx]; k = r - S.read_from;
         rs = S.q_start[r]; re = S.q_start[r + 1]; ylen = re - rs;
-        const uint64_t from_c = (S.rpt == 0) ? 0 : min(r / S.rpt, S.T - 1) * S.rpt;   // chunk heads (Q4)
-        const bool head = S.q_start[from_c] == rs;
+        const bool head = is_chunk_head(S, r, rs);                                   // chunk heads (Q4)
         const uint64_t p0 = rs - (head ? 0 : 1);
         up_to = (r + 1 < S.n_q) ? (re ? re - 1 : 0) : S.q_len;                     // :93
         if (S.wcap) up_to = min(up_to, S.wcap[k]);
@@ -417,8 +429,7 @@ __device__ __forceinline__ void accept_window_one(const SeedLaunch &S, const ims
     if (res[k].status != 1) return;
     const uint64_t r = S.read_from + k;
     const uint64_t rs = S.q_start[r], re = S.q_start[r + 1], ylen = re - rs;
-    const uint64_t from_c = (S.rpt == 0) ? 0 : min(r / S.rpt, S.T - 1) * S.rpt;
-    const bool head = S.q_start[from_c] == rs;
+    const bool head = is_chunk_head(S, r, rs);
     const uint64_t p0 = rs - (head ? 0 : 1);
     uint64_t up_to = (r + 1 < S.n_q) ? (re ? re - 1 : 0) : S.q_len;
     if (S.wcap) up_to = min(up_to, S.wcap[k]);

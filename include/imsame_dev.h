@@ -90,6 +90,7 @@ typedef struct imsame_read_result {
 #define IMSAME_MOVE_UP   1u   /* one jump of n rows: X[px..px-n+1] vs '-'      */
 #define IMSAME_MOVE_LEFT 2u   /* one jump of n cols: '-' vs Y[py..py-n+1]      */
 
+#define IMSAME_LAUNCH_STATS 16
 typedef struct imsame_stats {
     uint64_t n_reads;       /* reads processed                       */
     uint64_t n_accepted;    /* reads accepted                        */
@@ -105,6 +106,12 @@ typedef struct imsame_stats {
     double   nw_launch_ms;  /* average NW kernel launch duration      */
     uint64_t nw_launches;
     uint64_t nw_bytes;      /* 2 B per NW cell (traceback floor) */
+    /* per NW launch, in launch order (first IMSAME_LAUNCH_STATS launches):
+     * candidates (read, record) pairs aligned and device milliseconds */
+    uint64_t launch_cand[IMSAME_LAUNCH_STATS];
+    double   launch_ms[IMSAME_LAUNCH_STATS];
+    uint64_t n_rewalk;      /* accepted reads whose path overflowed the device
+                               arena and was re-walked (want_paths)      */
 } imsame_stats;
 
 typedef struct imsame_ctx imsame_ctx;
@@ -140,13 +147,30 @@ int imsame_dev_index(imsame_ctx *ctx, const uint8_t *db_seq, uint64_t db_len,
 int imsame_dev_set_query(imsame_ctx *ctx, const uint8_t *q_seq, uint64_t q_len,
                          const uint64_t *q_start, uint64_t n_q);
 
+/* imsame_dev_set_query for a SHARD: the host arrays are the whole query (as
+ * the loader produced it), but only reads [read_from, read_to) -- their
+ * bases, one preceding base (a read borrows the previous read's last base,
+ * SURVEY Appendix A Q4) and their starts -- are copied to HBM.  Chunk heads
+ * keep the whole query's meaning (IMSAME.c:414: i*floor(n_q/T)), so
+ * imsame_dev_align over any sub-range of the shard gives the per-read
+ * results of a run over the whole query.  This is the per-GPU upload of a
+ * multi-GPU run: each device receives 1/N of the query. */
+int imsame_dev_set_query_range(imsame_ctx *ctx, const uint8_t *q_seq, uint64_t q_len,
+                               const uint64_t *q_start, uint64_t n_q,
+                               uint64_t read_from, uint64_t read_to);
+
 /* Replaces T x computeAlignmentsByThread (alignmentFunctions.c:43-208) over
- * reads [read_from, read_to) of the loaded query.  n_threads_semantic is the
+ * reads [read_from, read_to) of the loaded query (inside the uploaded range).  n_threads_semantic is the
  * reference's -n_threads: it fixes the chunk heads {i*floor(n/T)}
  * (IMSAME.c:414,430-452) whose first k-mer does not borrow the previous
  * read's last base, so results equal the reference's
  * for that -n_threads.  res[k] describes read read_from+k.  paths/paths_cap:
- * u32 arena for want_paths (may be NULL when want_paths == 0). */
+ * u32 arena for want_paths (may be NULL when want_paths == 0).  The device
+ * keeps its own arena, sized to what the alignments need (paths that
+ * overflow it are re-walked for exactly the reads concerned, never the whole
+ * call); if paths_cap is smaller than *paths_used the call returns
+ * IMSAME_E_PATHS with res[] complete and the paths still on the device:
+ * grow the host arena and call imsame_dev_fetch_paths. */
 int imsame_dev_align(imsame_ctx *ctx, uint64_t read_from, uint64_t read_to,
                      uint64_t n_threads_semantic, const imsame_params *prm,
                      imsame_read_result *res, uint32_t *paths, uint64_t paths_cap,
@@ -189,6 +213,16 @@ int imsame_dev_align_sliced(imsame_ctx *ctx, const uint8_t *db_seq, uint64_t db_
                             uint64_t n_threads_semantic, const imsame_params *prm,
                             imsame_read_result *res, uint32_t *paths, uint64_t paths_cap,
                             uint64_t *paths_used, uint64_t *n_slices, imsame_stats *stats);
+
+/* Copy the paths of the last imsame_dev_align / _align_windows /
+ * _align_sliced call (after IMSAME_E_PATHS) into paths[0 .. *paths_used):
+ * IMSAME_E_PATHS again if paths_cap is still too small. */
+int imsame_dev_fetch_paths(imsame_ctx *ctx, uint32_t *paths, uint64_t paths_cap, uint64_t *paths_used);
+
+/* Page-locked host memory for query/database buffers (faster H2D than
+ * pageable memory); NULL without a GPU.  Free with imsame_host_free. */
+void *imsame_host_alloc(uint64_t bytes);
+void  imsame_host_free(void *p);
 
 /* Unit-level entry replacing build_alignment (alignmentFunctions.c:210-274:
  * NW + backtrackingNW + identities) plus the acceptance test (:163) for

@@ -136,12 +136,32 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
     // aligned copies with the 64-byte tail padding the device buffers carry (chunked loads)
     std::vector<uint32_t> dbpad(db_len / 4 + 17, 0), qpad(q_len / 4 + 17, 0);
     if (db_len) memcpy(dbpad.data(), db, db_len);
-    if (q_len) memcpy(qpad.data(), q, q_len);
     db = (const uint8_t *)dbpad.data();
+    // The query as imsame_dev_set_query_range uploads a shard: only reads
+    // [read_from, read_to) (their starts, bases and QPAD bases before them)
+    // hold data; every other byte / start is POISON, so a kernel that used
+    // anything outside the shard would diverge from the oracle.
+    const uint64_t b0 = qs[read_from], b1 = qs[read_to], qbase = b0 > 64 ? b0 - 64 : 0;
+    memset(qpad.data(), 0xEE, qpad.size() * 4);
+    if (b1 > qbase) memcpy((uint8_t *)qpad.data() + qbase, q + qbase, b1 - qbase);
+    memset((uint8_t *)qpad.data() + b1, 0, std::min<uint64_t>(64, qpad.size() * 4 - b1));
     q = (const uint8_t *)qpad.data();
-    std::vector<uint64_t> off;
-    std::vector<uint2> ent;
-    build_csr(db, db_len, dbs.data(), n_db, db_brk, off, ent);
+    std::vector<uint64_t> qsv(qs.size(), 0xDEADBEEFDEADBEEFull);
+    for (uint64_t r = read_from; r <= read_to; ++r) qsv[r] = qs[r];
+    uint64_t qlo_first = read_from;
+    while (qlo_first > 0 && qs[qlo_first - 1] == qs[read_from]) --qlo_first;
+    // the CSR of the last database is kept (tests align many shards against one)
+    static std::vector<uint8_t> key;
+    static std::vector<uint64_t> off;
+    static std::vector<uint2> ent;
+    std::vector<uint8_t> k2(db, db + db_len);
+    k2.insert(k2.end(), (const uint8_t *)dbs.data(), (const uint8_t *)(dbs.data() + dbs.size()));
+    if (db_brk) k2.insert(k2.end(), db_brk, db_brk + (db_len + 7) / 8);
+    k2.push_back(db_brk ? 1 : 0);
+    if (k2 != key || off.empty()) {
+        build_csr(db, db_len, dbs.data(), n_db, db_brk, off, ent);
+        key.swap(k2);
+    }
     uint32_t max_rec = 0, ymax = 0;
     for (uint64_t s = 0; s < n_db; ++s) max_rec = std::max<uint32_t>(max_rec, (uint32_t)(dbs[s + 1] - dbs[s]));
     for (uint64_t r = read_from; r < read_to; ++r) ymax = std::max<uint32_t>(ymax, (uint32_t)(qs[r + 1] - qs[r]));
@@ -161,7 +181,7 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
     const uint32_t budget1 = bud_env ? (uint32_t)std::max(0, atoi(bud_env)) : SEED_BUDGET1;
     std::vector<uint8_t> nmemo(n), rstat(n);
     std::vector<imsame_read_result> o1(n), o2(n);
-    InitLaunch I = {qs.data(), read_from, n, res, cur_p.data(), cur_h.data(), nmemo.data(), rstat.data(), act.data()};
+    InitLaunch I = {qsv.data(), read_from, n, res, cur_p.data(), cur_h.data(), nmemo.data(), rstat.data(), act.data()};
     for (uint32_t k = 0; k < n; ++k) init_one(I, k);
     uint32_t nc[3] = {0, 0, 0}, pused = 0, flags = 0;
     unsigned long long err = ~0ull, nhits = 0, cells = 0, nacc = 0;
@@ -174,7 +194,8 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
         nc[0] = nc[1] = nc[2] = 0;
         SeedLaunch S;
         S.db = db; S.db_start = dbs.data(); S.n_db = n_db; S.db_len = db_len;
-        S.q = q; S.q_start = qs.data(); S.n_q = n_q; S.q_len = q_len;
+        S.q = q; S.q_start = qsv.data(); S.n_q = n_q; S.q_len = q_len;
+        S.qs_lo = read_from; S.qs_lo_first = qlo_first;
         S.off = off.data(); S.ent = ent.data(); S.wcap = nullptr; S.wstart = nullptr;
         S.active = act.data(); S.n_active = nact;
         S.read_from = read_from; S.T = T ? T : 1;
@@ -214,7 +235,7 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
             {nc[0], cr.data(), cs.data(), o1.data(), short_y}, {nc[1], cr2.data(), cs2.data(), o2.data(), ycap}};
         for (auto &c : cls) {
             if (!c.n) continue;
-            run_nw(db, dbs.data(), q, qs.data(), c.r, c.s, c.n, p, c.y, xcap, ml, mi, c.o, paths,
+            run_nw(db, dbs.data(), q, qsv.data(), c.r, c.s, c.n, p, c.y, xcap, ml, mi, c.o, paths,
                    (uint32_t)paths_cap, &pused, &flags);
             st.n_nw += c.n;
             UpdLaunch U = {c.r, c.s, c.n, c.o, read_from, res, rstat.data(), memo.data(), nmemo.data(),

@@ -26,7 +26,7 @@ def emu():
 def _declared_symbols():
     import re
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|void|const char \*)\s*(imsame_\w+)\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char \*)\s*\*?\s*(imsame_\w+)\(", txt, re.M)))
 
 
 def test_library_exports_every_declared_symbol():
@@ -277,3 +277,31 @@ def test_emulated_a_priori_rejection(emu, oracle, rec_bp, expect_nw):
     for f in PARITY_FIELDS:
         assert np.array_equal(r1[f], r2[f]), f
     assert (st.n_nw > 0) == expect_nw
+
+
+@pytest.mark.parametrize("name", ["empty_not_head", "borrowed", "edges"])
+def test_emulated_query_shards_equal_whole_run(emu, oracle, name, monkeypatch):
+    """imsame_dev_set_query_range semantics (the emulator uploads ONLY the
+    shard's reads and poisons everything else): two shards split at every
+    read (empty reads right before a shard, chunk heads outside it, the
+    borrowed base across the cut) concatenate to the oracle's whole-query
+    run, for every -n_threads of the golden case."""
+    monkeypatch.setenv("IMSAME_SEED_L", "1")
+    case = G.e2e_case(name)
+    db, dbs, brk = fasta.load(case["db"], True)
+    q, qs, _ = fasta.load(case["query"])
+    n = len(qs)
+    cuts = range(1, n) if n <= 12 else sorted({1, n // 2, n - 1})
+    for T in [int(list(case["meta"]["runs"])[-1])]:        # the most chunk heads
+        rc, exp, er = oracle.align(db, dbs, q, qs, oracle.params(), T, brk)
+        if rc:
+            continue                      # the size abort: covered by the pipeline tests
+        for k in cuts:
+            parts = []
+            for a, b in ((0, k), (k, n)):
+                rc2, r, _, _ = emu.align(db, dbs, q, qs, oracle.params(), T, read_from=a, read_to=b, db_brk=brk)
+                assert rc2 == 0
+                parts.append(r)
+            got = np.concatenate(parts)
+            for f in PARITY_FIELDS:
+                assert np.array_equal(got[f], exp[f]), (name, T, k, f)
