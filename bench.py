@@ -2,22 +2,27 @@
 """Benchmark of the IMSAME seed-and-extend hot path on MI355X.
 
 Metric (BASELINE.json): reads aligned/sec (node), 1M x 150 bp synthetic
-Illumina-like reads vs a 50 Mbp synthetic reference (configs[1]).
+Illumina-like reads vs a 50 Mbp synthetic reference (configs[1]), at 1, 2, 4
+and 8 GPUs.
 
-One step = one imsame_dev_align pass over the rank's 1M-read shard (seed
-scan + ungapped/e-value + NW wavefront + backtrack + acceptance + D2H of the
-per-read results), inputs resident in HBM.  N GPUs: one process per GPU
-(torchrun), each aligns its OWN 1M-read shard against its replica of the
-index (weak scaling, no data-path collective); the accepted-read counters are
-all-reduced over RCCL at the end.  value = N * 1M * steps / max-over-ranks
-wall time of the timed region.
+One step = the rank's shard of the query uploaded (H2D from page-locked host
+memory) + one imsame_dev_align pass over it (seed scan + ungapped/e-value +
+NW wavefront + backtrack + acceptance + D2H of the per-read results).
+N GPUs (strong scaling, the default): one process per GPU (torchrun); the
+1M-read query is cut into N contiguous shards (imsame_amd.dist.shard_range),
+each rank aligns its shard against its replica of the index with the chunk
+heads of -n_threads over the WHOLE query, so the union of the shards is
+exactly the single-GPU run; the only collective is an RCCL all-reduce of the
+clock (max) and the accepted count.  value = 1M * steps / max-over-ranks wall
+time of the timed region.  --scaling weak gives every rank its own 1M reads.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c5|c5w]
 """
 import argparse
 import ctypes as C
 import json
 import os
+import platform
 import sys
 import time
 
@@ -30,14 +35,14 @@ METRIC = "reads aligned/sec (node), 1M×150bp vs 50Mbp ref, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md, chip-level parameters
 
 
-# BASELINE.json configs, per GPU (SURVEY 8(d) canonical inputs).  c2 is the
-# metric's configuration and the default; c3 is configs[2]'s per-GPU shard
-# (10M reads / 8 GPUs vs 500 Mbp); c5 is configs[4] (ONT-like 10 kbp reads,
-# raised MAX_READ_SIZE, reads capped per GPU by --reads).
+# BASELINE.json configs (SURVEY 8(d) canonical inputs).  c2 is the metric's
+# configuration and the default; c3 is configs[2]'s per-GPU shard (10M reads /
+# 8 GPUs vs 500 Mbp); c5 is configs[4] (ONT-like 10 kbp reads, raised
+# MAX_READ_SIZE, reads capped by --reads); c5w the same reads vs long records.
 CONFIGS = {
     "c2": dict(reads=1_000_000, read_len=150, ref_bp=50_000_000, record_bp=2_000, ont=False, max_rs=None,
                cpu_sample=40_000, seeds=(42, 43),
-               workload="C2: 1M x 150 bp Illumina-like reads per GPU vs 50 Mbp synthetic reference "
+               workload="C2: 1M x 150 bp Illumina-like reads vs 50 Mbp synthetic reference "
                         "(2 kbp records), BASELINE.json configs[1]"),
     "c3": dict(reads=1_250_000, read_len=150, ref_bp=500_000_000, record_bp=2_000, ont=False, max_rs=None,
                cpu_sample=4_000, seeds=(43, 44),
@@ -46,7 +51,15 @@ CONFIGS = {
     "c5": dict(reads=100_000, read_len=10_000, ref_bp=50_000_000, record_bp=2_000, ont=True, max_rs=10_001,
                cpu_sample=0, seeds=(42, 48),
                workload="C5: 10 kbp ONT-like reads (5% sub, 2.5% ins, 2.5% del) vs 50 Mbp synthetic reference, "
-                        "MAX_READ_SIZE raised to 10001, BASELINE.json configs[4]"),
+                        "MAX_READ_SIZE raised to 10001, BASELINE.json configs[4] (2 kbp records: every hit is "
+                        "rejected a priori, seed scan only)"),
+    # C5 against records long enough to hold a read: the long-read NW runs
+    # (10 kbp x 12 kbp = 120M cells per candidate, int32 multi-strip kernel)
+    "c5w": dict(reads=4_096, read_len=10_000, ref_bp=50_004_000, record_bp=12_001, ont=True, max_rs=12_001,
+                cpu_sample=0, seeds=(42, 48),
+                workload="C5w: 10 kbp ONT-like reads vs 50 Mbp synthetic reference in 12,001 bp records, "
+                         "MAX_READ_SIZE raised to 12001 (BASELINE.json configs[4] shape with records that "
+                         "can hold a read, so the long-read NW runs)"),
 }
 
 
@@ -66,27 +79,63 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="c2",
-                    help="BASELINE.json workload (c2 = the metric's config; c3/c5 are stress runs)")
-    ap.add_argument("--reads", type=int, default=None, help="reads per GPU (default: the config's)")
+                    help="BASELINE.json workload (c2 = the metric's config; c3/c5/c5w are stress runs)")
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
+                    help="strong: ONE query of --reads reads split over the ranks (the metric); "
+                         "weak: every rank its own --reads reads")
+    ap.add_argument("--reads", type=int, default=None, help="reads in the query (weak: per rank)")
     ap.add_argument("--read-len", type=int, default=None)
     ap.add_argument("--ref-bp", type=int, default=None)
     ap.add_argument("--record-bp", type=int, default=None)
     ap.add_argument("--n-threads", type=int, default=16, help="reference -n_threads semantics")
     ap.add_argument("--cpu-sample", type=int, default=None,
                     help="reads in the CPU baseline sample (0: skip; default: the config's)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="threads of the CPU baseline (default: the host cores this process may use)")
     ap.add_argument("--cpu-kind", choices=("auto", "port", "reference"), default="auto",
                     help="auto: the compiled reference (oracle/_ref/IMSAME) when present, else the port")
     ap.add_argument("--slice-bases", type=int, default=0,
                     help="search the database in slices of at most this many bases, one slice's index in HBM "
                          "at a time (imsame_dev_align_sliced; the index rebuilds are inside the timed step)")
+    ap.add_argument("--e2e", choices=("auto", "on", "off"), default="auto",
+                    help="end-to-end imsame CLI run (parse, index, align, render, write) after the timed steps "
+                         "(auto: on for c2 at N=1)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "nw_traffic.json"))
+    ap.add_argument("--valu-json", default=os.path.join(REPO, "profiles", "nw_valu.json"))
     a = ap.parse_args()
     cfg = CONFIGS[a.config]
     for k in ("reads", "read_len", "ref_bp", "record_bp", "cpu_sample"):
         if getattr(a, k) is None:
             setattr(a, k, cfg[k])
     return a
+
+
+def host_cpu():
+    """The host this process runs on: model, online CPUs (nproc), the CPUs it
+    may run on (affinity) and its cgroup CPU quota; `usable` is what the CPU
+    baseline gets (the GPU box gives a process a share of a larger host)."""
+    model = platform.processor() or ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    nproc = os.cpu_count() or 1
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else nproc
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    usable = aff if quota is None else max(1, min(aff, int(quota)))
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit():
+        usable = min(usable, int(env))
+    return {"model": model, "nproc": nproc, "affinity": aff, "cgroup_quota_cpus": quota, "usable": usable}
 
 
 def main():
@@ -101,29 +150,40 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import imsame_amd
+    from imsame_amd.dist import shard_range
     from tests import synth
 
-    # synthetic C2 inputs: the reference is replicated, each rank has its own reads
+    # synthetic inputs: the reference is replicated; strong scaling = ONE query
+    # (the metric's 1M reads) whose contiguous shards go to the ranks, with the
+    # chunk heads of -n_threads over the whole query
     cfg = CONFIGS[a.config]
     ref, rst = synth.make_reference_arr(a.ref_bp, a.record_bp, seed=cfg["seeds"][0])
     gen = synth.make_long_reads_arr if cfg["ont"] else synth.make_reads_arr
-    q, qs = gen(ref, a.reads, a.read_len, seed=cfg["seeds"][1] + 1000 * rank)
+    strong = a.scaling == "strong"
+    q, qs = gen(ref, a.reads, a.read_len, seed=cfg["seeds"][1] + (0 if strong else 1000 * rank))
+    lo, hi = shard_range(a.reads, rank, world) if strong else (0, a.reads)
     dev = imsame_amd.Device(local)
     t0 = time.time()
     dev.index(ref, rst)
     t_index = time.time() - t0
-    dev.set_query(q, qs)                               # H2D once: inputs resident in HBM
+    pin = imsame_amd.PinnedArray(len(q))              # page-locked source of the per-step upload
+    pin.array[:] = q
+    qp = pin.array
     params = dev.params(max_read_size=cfg["max_rs"]) if cfg["max_rs"] else dev.params()
 
     n_slices = 1
+    h2d = []
 
     def step():
         nonlocal n_slices
+        t = time.perf_counter()
+        dev.set_query(qp, qs, lo, hi)                   # H2D of this rank's shard: inside the step
+        h2d.append(time.perf_counter() - t)
         if a.slice_bases:
             res, paths, st, n_slices = dev.align_sliced(ref, rst, a.slice_bases, n_threads=a.n_threads,
-                                                        params=params)
+                                                        params=params, read_from=lo, read_to=hi)
             return res, paths, st
-        return dev.align(0, a.reads, n_threads=a.n_threads, params=params)
+        return dev.align(lo, hi, n_threads=a.n_threads, params=params)
 
     def barrier():
         if dist is not None:
@@ -131,6 +191,7 @@ def main():
 
     for _ in range(a.warmup):
         step()
+    h2d.clear()
     barrier()
     stats = []
     t0 = time.perf_counter()
@@ -146,12 +207,12 @@ def main():
         accepted_all = int(all_reduce([accepted])[0])
     else:
         accepted_all = accepted
-    total_reads = world * a.reads * a.steps
+    total_reads = (a.reads if strong else world * a.reads) * a.steps
     value = total_reads / elapsed
 
-    # dominant kernel: nw_kernel.  Algorithmic bytes per NW candidate (SURVEY
-    # 8(d)): record + read + 2 B/cell traceback floor; HIP events on the
-    # library's own stream bracket every NW launch.
+    # dominant kernel: the NW launches.  Algorithmic bytes per NW candidate
+    # (SURVEY 8(d)): record + read + 2 B/cell traceback floor; HIP events on
+    # the library's own stream bracket every NW launch.
     nw_ms = sum(s["ms_nw"] for s in stats)
     nw_launches = sum(s["nw_launches"] for s in stats)
     cells = sum(s["nw_cells"] for s in stats)
@@ -161,20 +222,24 @@ def main():
     achieved = alg_bytes / (nw_ms / 1e3) / 1e9 if nw_ms else 0.0
     kernel = nw_kernel_name(a.read_len, a.record_bp) if not stats[-1]["nw_launches"] or a.read_len <= 160 \
         else "nw_kernel"
+    per_launch = alg_bytes / max(nw_launches, 1)
     traffic = None
     if os.path.exists(a.traffic_json):
         try:
             tj = json.load(open(a.traffic_json))
-            if tj.get("kernel") == kernel:          # PMC pass of THIS kernel (profiles/)
+            if tj.get("kernel") == kernel and tj.get("config", "c2") == a.config:   # PMC pass of THIS kernel
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
+    cells_per_s = cells / (nw_ms / 1e3) if nw_ms else 0.0
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "traffic_over_alg": round(traffic / per_launch, 4) if traffic and per_launch else None,
                 "kernel": kernel, "launches": nw_launches,
                 "avg_launch_ms": round(nw_ms / max(nw_launches, 1), 4),
-                "alg_bytes_per_launch": int(alg_bytes / max(nw_launches, 1)),
-                "cells_per_s": round(cells / (nw_ms / 1e3), 1) if nw_ms else 0.0}
+                "alg_bytes_per_launch": int(per_launch),
+                "cells_per_s": round(cells_per_s, 1),
+                "valu": valu_roofline(a.valu_json, kernel, a.config, cells_per_s)}
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_sample > 0:
@@ -182,28 +247,108 @@ def main():
             dev.index(ref, rst)                     # the sample is checked against the whole index
         cpu = cpu_baseline(dev, ref, rst, q, qs, a, params)
 
+    e2e = None
+    if rank == 0 and world == 1 and (a.e2e == "on" or (a.e2e == "auto" and a.config == "c2")):
+        dev.close()                                 # the CLI opens the device itself
+        e2e = run_e2e(ref, rst, q, qs, a)
+
     if rank == 0:
+        last = stats[-1]
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "reads/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "int32", "data": "synthetic",
-            "config": {"workload": cfg["workload"] + (f"; database searched in {n_slices} slices of <= "
-                                                       f"{a.slice_bases} bases" if a.slice_bases else ""),
-                       "reads_per_gpu": a.reads, "read_len": a.read_len, "ref_bp": a.ref_bp,
+            "scaling": a.scaling, "vs_baseline": None,
+            "dtype": "int16" if kernel == "nw16_kernel" else "int32", "data": "synthetic",
+            "config": {"workload": cfg["workload"] + (f"; {a.reads} reads total over {world} GPU(s), contiguous "
+                                                      f"shards" if strong else f"; {a.reads} reads per GPU")
+                       + (f"; database searched in {n_slices} slices of <= {a.slice_bases} bases"
+                          if a.slice_bases else ""),
+                       "reads": a.reads, "reads_per_gpu": hi - lo, "read_len": a.read_len, "ref_bp": a.ref_bp,
                        "record_bp": a.record_bp, "n_threads_semantic": a.n_threads,
                        "parallelism": f"dp{world} (read shards, replicated index)"},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "e2e": e2e,
             "detail": {"accepted_reads": accepted_all, "index_build_s": round(t_index, 3),
-                       "rounds": stats[-1]["rounds"], "nw_per_read": round(stats[-1]["n_nw"] / a.reads, 4),
-                       "hits_per_read": round(stats[-1]["n_hits"] / a.reads, 2),
-                       "ms_seed": round(stats[-1]["ms_seed"], 3), "ms_nw": round(stats[-1]["ms_nw"], 3),
-                       "ms_align_call": round(stats[-1]["ms_total"], 3)},
+                       "rounds": last["rounds"], "nw_per_read": round(last["n_nw"] / max(hi - lo, 1), 4),
+                       "hits_per_read": round(last["n_hits"] / max(hi - lo, 1), 2),
+                       "ms_h2d_query": round(1e3 * sum(h2d) / max(len(h2d), 1), 3),
+                       "ms_seed": round(last["ms_seed"], 3), "ms_nw": round(last["ms_nw"], 3),
+                       "ms_align_call": round(last["ms_total"], 3),
+                       "nw_launch_cand": last["launch_cand"],
+                       "nw_launch_ms": [round(x, 3) for x in last["launch_ms"]]},
         }
         print(json.dumps(line), flush=True)
     dev.close()
+    pin.free()
     if dist is not None:
         dist.destroy_process_group()
+
+
+# MI355X_MICROARCH.md: a wave issues one VALU instruction over 2 cycles
+# (64 lanes on a SIMD-32), 4 SIMDs x 256 CUs at 2.4 GHz
+VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 2.0     # wave-instructions / s
+
+
+def valu_roofline(path, kernel, config, cells_per_s):
+    """The NW kernel's binding resource is VALU issue.  Lane-
+    instructions per cell come from a PMC pass (SQ_INSTS_VALU x 64 / cells of
+    the same launches, profiles/nw_valu.json); achieved issue = that x the
+    cells/s measured here / 64, against the 2-cycle issue peak."""
+    if not os.path.exists(path):
+        return None
+    try:
+        vj = json.load(open(path))
+    except Exception:
+        return None
+    if vj.get("kernel") != kernel or vj.get("config", "c2") != config:
+        return None
+    ipc = vj["lane_instr_per_cell"]
+    rate = ipc * cells_per_s / 64.0
+    return {"instr_per_cell": round(ipc, 3), "achieved": round(rate / 1e9, 2), "issue_peak": round(VALU_ISSUE_PEAK / 1e9, 2),
+            "unit": "G wave-instr/s", "frac": round(rate / VALU_ISSUE_PEAK, 4), "source": os.path.relpath(path, REPO),
+            "note": "peak = 2 cycles per wave instruction; v_pk_*_i16 / v_perm issue at ~4 (profiles/r06_valu_rate.txt),"
+                    " so this instruction mix saturates near 0.5"}
+
+
+def run_e2e(ref, rst, q, qs, a):
+    """The whole imsame command on the same inputs written as FASTA: parse,
+    index, upload, align, render + write of the .align (SURVEY 8(d)
+    end-to-end wall; the reference's phases IMSAME.c:102,295,407,470).  The
+    CLI prints a JSON phase line on stderr."""
+    import re
+    import shutil
+    import subprocess
+    import tempfile
+    from tests import synth
+    cli = os.path.join(REPO, "imsame_amd", "bin", "imsame")
+    if not os.access(cli, os.X_OK):
+        return None
+    td = tempfile.mkdtemp(prefix="imsame_e2e_")
+    try:
+        dbf, qf, outf = os.path.join(td, "db.fa"), os.path.join(td, "q.fa"), os.path.join(td, "out.align")
+        synth.write_fasta(dbf, ref, rst, "ref", width=80)
+        synth.write_fasta(qf, q, qs, "read", width=0)
+        free = shutil.disk_usage(td).free
+        need = 4 * 1024 ** 3                         # ~3.3 KB of text per accepted read at C2
+        out = outf if free > need else "/dev/null"
+        t0 = time.monotonic()
+        p = subprocess.run([cli, "-query", qf, "-db", dbf, "-out", out, "-n_threads", str(a.n_threads)],
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=900)
+        wall = time.monotonic() - t0
+        m = re.search(rb"\[imsame\] phases (\{.*\})", p.stderr)
+        if p.returncode != 0 or not m:
+            return {"error": f"rc {p.returncode}: {p.stderr[-300:].decode(errors='replace')}"}
+        ph = json.loads(m.group(1))
+        ph = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in ph.items()}
+        ph.update({"process_wall_s": round(wall, 3), "output": "file" if out == outf else "/dev/null (disk full)",
+                   "reads_per_s_e2e": round(len(qs) / wall, 1),
+                   "note": "imsame -query q.fa -db db.fa -out out.align -n_threads %d on one GPU; render+write of "
+                           "finished batches overlaps the device's later batches; render_tail_s = exposed output "
+                           "time after the last batch" % a.n_threads})
+        return ph
+    finally:
+        shutil.rmtree(td, ignore_errors=True)
 
 
 def cpu_baseline(dev, ref, rst, q, qs, a, params):
@@ -214,6 +359,9 @@ def cpu_baseline(dev, ref, rst, q, qs, a, params):
     with the same -n_threads and every per-read result is compared."""
     from tests.oracle_bind import Oracle
     from imsame_amd import PARITY_FIELDS
+    hc = host_cpu()
+    if a.cpu_threads is None:
+        a.cpu_threads = hc["usable"]
     o = Oracle.load()
     n = min(a.cpu_sample, len(qs))
     qv = q[:int(qs[n])] if n < len(qs) else q
@@ -223,11 +371,12 @@ def cpu_baseline(dev, ref, rst, q, qs, a, params):
     secs = o.lib.or_last_align_seconds()
     dev.set_query(qv, qs[:n])
     got, _, _ = dev.align(0, n, n_threads=a.cpu_threads, params=params)
+    host = dict(hc, threads_used=a.cpu_threads)
     same = int(np.all([exp[f] == got[f] for f in PARITY_FIELDS], axis=0).sum())
     port = {"value": round(n / secs, 1), "unit": "reads/s", "cores": a.cpu_threads, "kind": "port",
             "sample": f"first {n} reads of the rank-0 shard as their own query, oracle/imsame_oracle.c "
                       f"-n_threads {a.cpu_threads}, alignment-phase wall {secs:.2f} s",
-            "sample_reads_identical_to_gpu": same, "sample_reads_compared": n}
+            "sample_reads_identical_to_gpu": same, "sample_reads_compared": n, "host": host}
     ref_bin = os.path.join(REPO, "oracle", "_ref", "IMSAME")
     if a.cpu_kind == "port" or (a.cpu_kind == "auto" and not os.access(ref_bin, os.X_OK)):
         return port
@@ -238,7 +387,7 @@ def cpu_baseline(dev, ref, rst, q, qs, a, params):
                       f"IMSAME compiled from the reference sources (oracle/Makefile ref, gcc -O3) -n_threads "
                       f"{a.cpu_threads}; alignment phase = process wall {r['wall_s']:.2f} s minus its single-threaded "
                       f"setup phases {r['setup_s']:.2f} s = {r['align_s']:.2f} s",
-            "reference_accepted": r["accepted"], "gpu_accepted": gpu_acc,
+            "reference_accepted": r["accepted"], "gpu_accepted": gpu_acc, "host": host,
             "port": port}
 
 

@@ -41,12 +41,15 @@
 #include <inttypes.h>
 #include <sys/stat.h>
 #include "../../../include/imsame_dev.h"
+#include <fcntl.h>
+#include <unistd.h>
 #include "imsame_host.h"
+#include "imsame_pipe.h"
 
-#define MAX_DEV 64
+#define MAX_DEV PIPE_MAX_DEV
 
 /* wall seconds per phase over the job (stderr summary) */
-static double ph_read, ph_parse, ph_revcomp, ph_align, ph_render, ph_write;
+static double ph_read, ph_parse, ph_revcomp, ph_index, ph_align, ph_render, ph_write, ph_tail;
 
 static double now_s(void) {
     struct timespec ts;
@@ -84,163 +87,56 @@ static int is_file(const char *p) {
     return stat(p, &sb) == 0 && S_ISREG(sb.st_mode);
 }
 
-/* ---- device workers --------------------------------------------------------- */
-typedef struct {
-    int device;
-    imsame_ctx *ctx;
-    const host_seqs *db_now, *q_now;        /* what the context holds */
-    /* job */
-    const host_seqs *db, *q;
-    uint64_t from, to, T, stop;
-    const imsame_params *prm;
-    imsame_read_result *res;                /* global array; this shard writes [from, to) */
-    uint32_t *paths;
-    uint64_t cap, used;
-    imsame_stats st;
-    int rc;
-    host_text text;
-    double t_index;
-} worker;
-
-static void *align_run(void *arg) {
-    worker *w = arg;
-    double t0 = now_s();
-    w->rc = 0;
-    if (w->db_now != w->db) {
-        w->rc = imsame_dev_index(w->ctx, w->db->seq, w->db->len, w->db->start, w->db->n, w->db->brk);
-        if (w->rc) return NULL;
-        w->db_now = w->db;
-    }
-    w->t_index = now_s() - t0;
-    if (w->q_now != w->q) {
-        w->rc = imsame_dev_set_query(w->ctx, w->q->seq, w->q->len, w->q->start, w->q->n);
-        if (w->rc) return NULL;
-        w->q_now = w->q;
-    }
-    memset(&w->st, 0, sizeof w->st);
-    if (w->to <= w->from) return NULL;
-    for (;;) {
-        w->rc = imsame_dev_align(w->ctx, w->from, w->to, w->T, w->prm, w->res + w->from, w->paths, w->cap,
-                                 &w->used, &w->st);
-        if (w->rc != IMSAME_E_PATHS) break;
-        w->cap = w->used + w->used / 4 + 1024;
-        uint32_t *p = realloc(w->paths, w->cap * sizeof(uint32_t));
-        if (!p) { w->rc = IMSAME_E_OOM; break; }
-        w->paths = p;
-    }
-    return NULL;
-}
-
-/* The record of alignmentFunctions.c:165-168, rendered for reads [from, stop). */
-static void *render_run(void *arg) {
-    worker *w = arg;
-    w->text.len = 0;
-    host_text one = {0};
-    const uint64_t hi = w->stop < w->to ? w->stop : w->to;
-    for (uint64_t r = w->from; r < hi; r++) {
-        const imsame_read_result *x = &w->res[r];
-        if (x->status != 1) continue;
-        const uint64_t yl = x->ylen, s = x->db_seq;
-        const uint64_t pid = 100 * (uint64_t)x->identities / x->length, pcv = 100 * (uint64_t)x->length / yl;
-        char head[160];
-        const int hn = snprintf(head, sizeof head, "(%" PRIu64 ", %" PRIu64 ") : %d%% %d%% %" PRIu64 "\n $$$$$$$ \n",
-                                r, s, (int)pid < 100 ? (int)pid : 100, (int)pcv < 100 ? (int)pcv : 100, yl);
-        host_render(w->db->seq + w->db->start[s], w->db->start[s + 1] - w->db->start[s], w->q->seq + w->q->start[r],
-                    yl, x, w->paths + x->path_off, &one);
-        if (w->text.len + hn + one.len > w->text.cap) {
-            w->text.cap = (w->text.len + hn + one.len) * 2 + 65536;
-            w->text.buf = realloc(w->text.buf, w->text.cap);
-        }
-        memcpy(w->text.buf + w->text.len, head, hn);
-        memcpy(w->text.buf + w->text.len + hn, one.buf, one.len);
-        w->text.len += hn + one.len;
-    }
-    free(one.buf);
-    return NULL;
-}
-
-static void run_workers(worker *w, int G, void *(*fn)(void *)) {
-    pthread_t th[MAX_DEV];
-    for (int g = 1; g < G; ++g)
-        if (pthread_create(&th[g], NULL, fn, &w[g])) { fn(&w[g]); th[g] = 0; }
-    fn(&w[0]);
-    for (int g = 1; g < G; ++g)
-        if (th[g]) pthread_join(th[g], NULL);
-}
-
-/* One IMSAME run (IMSAME.c:34-478 semantics, as imsame_cli.c) over G shards. */
-static void imsame_run(worker *w, int G, const host_seqs *q, const host_seqs *db, uint64_t T,
-                       const imsame_params *prm_in, const char *opath) {
-    imsame_params prm = *prm_in;
-    FILE *out = fopen(opath, "wt");
+/* One IMSAME run (IMSAME.c:34-478 semantics, as imsame_cli.c) over the G
+ * contexts: shards, batches and parallel rendering by imsame_pipe.c. */
+static void imsame_run(pipe_dev *dv, int G, const host_seqs *q, const host_seqs *db, uint64_t T,
+                       const imsame_params *prm, const char *opath) {
+    const int out_fd = open(opath, O_WRONLY | O_CREAT | O_TRUNC, 0666);
     double t0 = now_s();
     printf("[INFO] Init. quick table\n");
     printf("[INFO] Initialization took %e seconds \n", now_s() - t0);
     printf("[INFO] Loading database\n");
-    const uint64_t n = q->n;
-    imsame_read_result *res = calloc(n + 1, sizeof *res);
-    if (!res) die("Could not allocate memory for results");
-    prm.want_paths = out ? 1 : 0;
-    for (int g = 0; g < G; ++g) {
-        w[g].db = db; w[g].q = q; w[g].T = T; w[g].prm = &prm; w[g].res = res;
-        w[g].from = (uint64_t)g * n / G; w[g].to = (uint64_t)(g + 1) * n / G;
-        if (out && !w[g].paths) {
-            w[g].cap = (w[g].to - w[g].from + 1) * 8 + 1024;
-            w[g].paths = malloc(w[g].cap * sizeof(uint32_t));
-        }
-    }
-    /* index build and query upload happen inside the workers, overlapped
-     * with alignment; the phase lines keep the stock order and lengths */
+    double tp = now_s();
+    int rc = pipe_index(dv, G, db);
+    if (rc) die(imsame_strerror(rc));
+    ph_index += now_s() - tp;
     printf("[INFO] Database loaded and of length %" PRIu64 ". Hash table building took %e seconds\n", db->len,
            now_s() - t0);
     printf("[INFO] Loading query.\n");
-    printf("[INFO] Query loaded and of length %" PRIu64 ". Took %e seconds\n", q->len, 0.0);
+    t0 = now_s();
+    rc = pipe_set_query(dv, G, q);
+    if (rc) die(imsame_strerror(rc));
+    printf("[INFO] Query loaded and of length %" PRIu64 ". Took %e seconds\n", q->len, now_s() - t0);
     t0 = now_s();
     printf("[INFO] Computing alignments.\n");
     {
-        const uint64_t TT = T ? T : 1, rpt = (uint64_t)floorl((long double)n / (long double)TT);
+        const uint64_t n = q->n, TT = T ? T : 1, rpt = (uint64_t)floorl((long double)n / (long double)TT);
         for (uint64_t t = 0; t < TT; t++)
             printf("Going from %" PRIu64 " to %" PRIu64 "\n", t * rpt, t == TT - 1 ? n : (t + 1) * rpt);
     }
-    double tp = now_s();
-    run_workers(w, G, align_run);
-    ph_align += now_s() - tp;
-    uint64_t stop = n;
-    int fatal = 0;
-    for (int g = 0; g < G; ++g) {
-        if (w[g].rc == IMSAME_E_READ_TOO_LONG) { if (w[g].st.err_read < stop) stop = w[g].st.err_read; fatal = 1; }
-        else if (w[g].rc) die(imsame_strerror(w[g].rc));
-    }
-    uint64_t acc = 0;
-    for (uint64_t r = 0; r < stop; r++) acc += res[r].status == 1;
-    if (out) {
-        for (int g = 0; g < G; ++g) w[g].stop = stop;
-        tp = now_s();
-        run_workers(w, G, render_run);
-        ph_render += now_s() - tp;
-        tp = now_s();
-        for (int g = 0; g < G; ++g) fwrite(w[g].text.buf, 1, w[g].text.len, out);
-        fclose(out);
-        ph_write += now_s() - tp;
-    }
-    free(res);
-    if (fatal) {
+    fflush(stdout);
+    pipe_opts po = {.T = T, .prm = *prm, .out_fd = out_fd, .render_threads = 0, .batch_reads = 0};
+    pipe_result pr;
+    rc = pipe_align_render(dv, G, db, q, &po, &pr);
+    if (out_fd >= 0) close(out_fd);
+    ph_align += pr.t_align; ph_render += pr.t_render; ph_write += pr.t_write; ph_tail += pr.t_tail;
+    if (rc == IMSAME_E_READ_TOO_LONG) {
         printf("ERR**** Read size reached for gapped alignment. ****\n");
         fflush(stdout);
         return;
     }
+    if (rc) die(imsame_strerror(rc));
+    const uint64_t acc = pr.accepted, n = q->n;
     printf("[INFO] Alignments computed in %e seconds.\n", now_s() - t0);
     printf("[INFO] %" PRIu64 " reads (%" PRIu64 ") from the query were found in the database (%" PRIu64
            ") at a minimum e-value of %Le and minimum coverage of %d%%.\n",
-           acc, n, db->n, prm.min_e, (int)(100 * prm.min_coverage));
+           acc, n, db->n, prm->min_e, (int)(100 * prm->min_coverage));
     printf("[INFO] The Jaccard-index is: %Le\n", (long double)acc / ((db->n + n) - acc));
     printf("[INFO] Deallocating heap memory.\n");
     fflush(stdout);
-    uint64_t nw = 0, cells = 0;
-    double ms = 0;
-    for (int g = 0; g < G; ++g) { nw += w[g].st.n_nw; cells += w[g].st.nw_cells; if (w[g].st.ms_total > ms) ms = w[g].st.ms_total; }
     fprintf(stderr, "[imsame_all_vs_all] %s: reads=%" PRIu64 " accepted=%" PRIu64 " nw=%" PRIu64 " cells=%" PRIu64
-            " shards=%d align_ms(max)=%.3f\n", opath, n, acc, nw, cells, G, ms);
+            " shards=%d batches=%" PRIu64 " align_ms(max)=%.3f\n", opath, n, acc, pr.st.n_nw, pr.st.nw_cells, G,
+            pr.batches, pr.st.ms_total);
 }
 
 static void load_raw(mgen *m) {
@@ -321,25 +217,13 @@ int main(int argc, char **argv) {
 
     int devs[MAX_DEV], G = 0;
     if (!dry) {
-        const int avail = imsame_dev_count();
-        if (devspec && strchr(devspec, ',')) {
-            for (const char *s = devspec; *s && G < MAX_DEV; ) {
-                devs[G++] = atoi(s);
-                const char *c = strchr(s, ',');
-                if (!c) break;
-                s = c + 1;
-            }
-        } else {
-            const int want = devspec ? atoi(devspec) : avail;
-            for (int g = 0; g < want && g < MAX_DEV; ++g) devs[G++] = g;
-        }
+        if (devspec) G = pipe_parse_devices(devspec, devs, MAX_DEV);
+        else
+            for (int g = 0, avail = imsame_dev_count(); g < avail && g < MAX_DEV; ++g) devs[G++] = g;
         if (G == 0) die("Could not open the GPU device");
     }
-    worker *w = calloc(G ? G : 1, sizeof *w);
-    for (int g = 0; g < G; ++g) {
-        w[g].device = devs[g];
-        if (imsame_dev_open(devs[g], &w[g].ctx)) die("Could not open the GPU device");
-    }
+    pipe_dev dv[MAX_DEV];
+    if (G && pipe_open(dv, devs, G)) die("Could not open the GPU device");
 
     char op[8192];
     const double t_job = now_s();
@@ -357,26 +241,22 @@ int main(int argc, char **argv) {
                     continue;
                 }
                 load_fwd(&m[i]);
-                if (rev) load_rc(&m[j], w[0].ctx);
+                if (rev) load_rc(&m[j], dv[0].ctx);
                 else load_fwd(&m[j]);
-                imsame_run(w, G, &m[i].fwd, rev ? &m[j].rc : &m[j].fwd, T, &prm, op);
+                imsame_run(dv, G, &m[i].fwd, rev ? &m[j].rc : &m[j].fwd, T, &prm, op);
             }
         }
-    fprintf(stderr, "[imsame_all_vs_all] phase read=%.3f parse=%.3f revcomp=%.3f align=%.3f render=%.3f write=%.3f\n",
-            ph_read, ph_parse, ph_revcomp, ph_align, ph_render, ph_write);
+    fprintf(stderr, "[imsame_all_vs_all] phase read=%.3f parse=%.3f revcomp=%.3f index=%.3f align=%.3f render=%.3f "
+            "write=%.3f render_tail=%.3f\n", ph_read, ph_parse, ph_revcomp, ph_index, ph_align, ph_render, ph_write,
+            ph_tail);
     fprintf(stderr, "[imsame_all_vs_all] %zu metagenomes, %" PRIu64 " runs, %" PRIu64 " skipped, %d device contexts, %.3f s\n",
             nm, runs, skipped, G, now_s() - t_job);
-    for (int g = 0; g < G; ++g) {
-        imsame_dev_close(w[g].ctx);
-        free(w[g].paths);
-        free(w[g].text.buf);
-    }
+    pipe_close(dv, G);
     for (size_t k = 0; k < nm; ++k) {
         free(m[k].name); free(m[k].path); free(m[k].raw);
         host_free_seqs(&m[k].fwd); host_free_seqs(&m[k].rc);
     }
     free(m);
-    free(w);
     if (grc == 0) globfree(&gl);
     return 0;
 }

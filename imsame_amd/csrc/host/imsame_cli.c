@@ -8,10 +8,15 @@
  * -n_threads T the record set equals the reference's (its own file
  * interleaves thread output at fprintf granularity).
  *
- * Extra flags (not in the reference): -device D, -max_read_size N (raise the
- * 3000-base NW cap of structs.h:19; the reference has it compile-time only).
- * Timing lines report wall-clock seconds (the reference prints clock(),
- * i.e. CPU time summed over threads).
+ * Extra flags (not in the reference): -device D, -devices N|d0,d1,... (the
+ * reads are sharded over several device contexts, the multi-GPU form of the
+ * reference's -n_threads fan-out, IMSAME.c:414-467), -max_read_size N (raise
+ * the 3000-base NW cap of structs.h:19; the reference has it compile-time
+ * only), -slice_bases N, -render_threads N, -batch_reads N.  The .align
+ * records are rendered by a thread pool while the GPUs align later batches
+ * (imsame_pipe.c).  Timing lines report wall-clock seconds (the reference
+ * prints clock(), i.e. CPU time summed over threads); a JSON phase line goes
+ * to stderr.
  */
 #define _GNU_SOURCE
 #include <stdio.h>
@@ -21,7 +26,10 @@
 #include <time.h>
 #include <inttypes.h>
 #include "../../../include/imsame_dev.h"
+#include <fcntl.h>
+#include <unistd.h>
 #include "imsame_host.h"
+#include "imsame_pipe.h"
 
 static double now_s(void) {
     struct timespec ts;
@@ -49,18 +57,21 @@ static void usage(void) {
     printf("           --verbose   Turns verbose on\n");
     printf("           --help      Shows help for program usage\n");
     printf("           -device     [Integer: HIP device] (default 0)\n");
+    printf("           -devices    [N | d0,d1,...: shard the reads over these HIP devices]\n");
     printf("           -max_read_size [Integer] (default 3000)\n");
     printf("           -slice_bases [Integer: index the database in slices of at most this many bases]\n");
+    printf("           -render_threads [Integer: host threads writing the .align records]\n");
+    printf("           -batch_reads [Integer: reads per device call]\n");
     exit(1);
 }
 
 int main(int argc, char **argv) {
-    const char *qpath = NULL, *dpath = NULL, *opath = NULL;
+    const char *qpath = NULL, *dpath = NULL, *opath = NULL, *devspec = NULL;
     imsame_params prm;
     imsame_params_default(&prm);
     uint64_t T = 4;                                   /* IMSAME.c:49 */
-    int device = 0;
-    uint64_t slice_bases = 0;                        /* 0: one index (the reference's) */
+    int device = 0, render_threads = 0;
+    uint64_t slice_bases = 0, batch_reads = 0;       /* 0: one index (the reference's) */
     /* init_args, IMSAME.c:520-578 (same strcmp scan over every argv slot) */
     for (int a = 0; a < argc; a++) {
         if (!strcmp(argv[a], "--help")) usage();
@@ -84,35 +95,47 @@ int main(int argc, char **argv) {
         if (!strcmp(argv[a], "-egap")) prm.egap = -atoi(argv[a + 1]);
         if (!strcmp(argv[a], "-n_threads")) T = (uint64_t)atoi(argv[a + 1]);
         if (!strcmp(argv[a], "-device")) device = atoi(argv[a + 1]);
+        if (!strcmp(argv[a], "-devices")) devspec = argv[a + 1];
         if (!strcmp(argv[a], "-max_read_size")) prm.max_read_size = strtoull(argv[a + 1], NULL, 10);
         if (!strcmp(argv[a], "-slice_bases")) slice_bases = strtoull(argv[a + 1], NULL, 10);
+        if (!strcmp(argv[a], "-render_threads")) render_threads = atoi(argv[a + 1]);
+        if (!strcmp(argv[a], "-batch_reads")) batch_reads = strtoull(argv[a + 1], NULL, 10);
     }
     if (!qpath || !dpath) terror("A query and database is required");
-    FILE *out = NULL;
-    if (opath) out = fopen(opath, "wt");
+    /* the reference fopen()s "wt" and never checks it (IMSAME.c:541-551) */
+    int out_fd = opath ? open(opath, O_WRONLY | O_CREAT | O_TRUNC, 0666) : -1;
+    int devs[PIPE_MAX_DEV], G = 1;
+    devs[0] = device;
+    if (devspec) G = pipe_parse_devices(devspec, devs, PIPE_MAX_DEV);
+    if (G < 1) terror("Could not open the GPU device");
+    if (slice_bases && G > 1) terror("-slice_bases runs on one device");
 
+    const double t_wall = now_s();
     double t0 = now_s();
     printf("[INFO] Init. quick table\n");
-    imsame_ctx *ctx = NULL;
-    int rc = imsame_dev_open(device, &ctx);
-    if (rc) terror("Could not open the GPU device");
+    pipe_dev dv[PIPE_MAX_DEV];
+    if (pipe_open(dv, devs, G)) terror("Could not open the GPU device");
     printf("[INFO] Initialization took %e seconds \n", now_s() - t0);
 
     printf("[INFO] Loading database\n");
     t0 = now_s();
     host_seqs db, q;
     if (host_load_fasta(dpath, 1, &db)) terror("Could not open database file");
+    const double t_parse_db = now_s() - t0;
     if (db.n == 0) slice_bases = 0;                  /* nothing to slice */
-    rc = slice_bases ? IMSAME_OK : imsame_dev_index(ctx, db.seq, db.len, db.start, db.n, db.brk);
+    int rc = slice_bases ? IMSAME_OK : pipe_index(dv, G, &db);
     if (rc) terror(imsame_strerror(rc));
+    const double t_index = now_s() - t0 - t_parse_db;
     printf("[INFO] Database loaded and of length %" PRIu64 ". Hash table building took %e seconds\n", db.len,
            now_s() - t0);
 
     t0 = now_s();
     printf("[INFO] Loading query.\n");
     if (host_load_fasta(qpath, 0, &q)) terror("Could not open query file");
-    rc = imsame_dev_set_query(ctx, q.seq, q.len, q.start, q.n);
+    const double t_parse_q = now_s() - t0;
+    rc = pipe_set_query(dv, G, &q);
     if (rc) terror(imsame_strerror(rc));
+    const double t_upload = now_s() - t0 - t_parse_q;
     printf("[INFO] Query loaded and of length %" PRIu64 ". Took %e seconds\n", q.len, now_s() - t0);
 
     t0 = now_s();
@@ -124,55 +147,62 @@ int main(int argc, char **argv) {
             printf("Going from %" PRIu64 " to %" PRIu64 "\n", t * rpt, t == TT - 1 ? q.n : (t + 1) * rpt);
         fflush(stdout);
     }
-    imsame_read_result *res = calloc(q.n + 1, sizeof *res);
-    uint64_t cap = out ? (q.n + 1) * 8 + 1024 : 0, used = 0;
-    uint32_t *paths = out ? malloc(cap * sizeof(uint32_t)) : NULL;
-    prm.want_paths = out ? 1 : 0;
-    imsame_stats st;
-    for (;;) {
-        rc = slice_bases ? imsame_dev_align_sliced(ctx, db.seq, db.len, db.start, db.n, db.brk, slice_bases, 0, q.n,
-                                                   T, &prm, res, paths, cap, &used, NULL, &st)
-                         : imsame_dev_align(ctx, 0, q.n, T, &prm, res, paths, cap, &used, &st);
-        if (rc != IMSAME_E_PATHS) break;
-        cap = used + used / 4 + 1024 > 2 * cap ? used + used / 4 + 1024 : 2 * cap;   /* too small: grow, redo */
-        paths = realloc(paths, cap * sizeof(uint32_t));
+    pipe_result pr;
+    memset(&pr, 0, sizeof pr);
+    if (slice_bases) {
+        /* one device, database indexed slice by slice: one batch */
+        imsame_read_result *res = calloc(q.n + 1, sizeof *res);
+        uint64_t cap = out_fd >= 0 ? 2 * q.n + 1024 : 0, used = 0;
+        uint32_t *paths = cap ? malloc(cap * sizeof(uint32_t)) : NULL;
+        if (!res || (cap && !paths)) terror("Could not allocate memory for results");
+        prm.want_paths = out_fd >= 0;
+        const double ta = now_s();
+        rc = imsame_dev_align_sliced(dv[0].ctx, db.seq, db.len, db.start, db.n, db.brk, slice_bases, 0, q.n, T, &prm,
+                                     res, paths, cap, &used, NULL, &pr.st);
+        if (rc == IMSAME_E_PATHS) {
+            uint32_t *p2 = realloc(paths, (used + 1) * sizeof(uint32_t));
+            if (!p2) terror("Could not allocate memory for results");
+            paths = p2;
+            rc = imsame_dev_fetch_paths(dv[0].ctx, paths, used, &used);
+        }
+        pr.t_align = now_s() - ta;
+        if (rc == IMSAME_E_ARG) terror("-slice_bases needs every record and read within -max_read_size");
+        if (rc) terror(imsame_strerror(rc));
+        const double tr = now_s();
+        uint64_t off = 0;
+        if (out_fd >= 0 && pipe_render_range(&db, &q, res, paths, 0, q.n, out_fd, render_threads, &off, &pr))
+            terror("Could not write the output file");
+        pr.t_tail = now_s() - tr;
+        pr.stop = q.n;
+        for (uint64_t r = 0; r < q.n; r++) pr.accepted += res[r].status == 1;
+        free(res);
+        free(paths);
+    } else {
+        pipe_opts po = {.T = T, .prm = prm, .out_fd = out_fd, .render_threads = render_threads,
+                        .batch_reads = batch_reads};
+        rc = pipe_align_render(dv, G, &db, &q, &po, &pr);
+        if (rc && rc != IMSAME_E_READ_TOO_LONG) terror(imsame_strerror(rc));
     }
-    if (rc == IMSAME_E_ARG && slice_bases)
-        terror("-slice_bases needs every record and read within -max_read_size");
-    if (rc && rc != IMSAME_E_READ_TOO_LONG) terror(imsame_strerror(rc));
-    const uint64_t stop = (rc == IMSAME_E_READ_TOO_LONG) ? st.err_read : q.n;
-    uint64_t acc = 0;
-    host_text txt = {0};
-    for (uint64_t r = 0; r < stop; r++) {
-        const imsame_read_result *x = &res[r];
-        if (x->status != 1) continue;
-        acc++;
-        if (!out) continue;
-        const uint64_t yl = x->ylen;
-        /* alignmentFunctions.c:167 */
-        const uint64_t pid = 100 * (uint64_t)x->identities / x->length, pcv = 100 * (uint64_t)x->length / yl;
-        fprintf(out, "(%" PRIu64 ", %" PRIu64 ") : %d%% %d%% %" PRIu64 "\n $$$$$$$ \n", r, x->db_seq,
-                (int)pid < 100 ? (int)pid : 100, (int)pcv < 100 ? (int)pcv : 100, yl);
-        const uint64_t s = x->db_seq;
-        host_render(db.seq + db.start[s], db.start[s + 1] - db.start[s], q.seq + q.start[r], yl, x,
-                    paths + x->path_off, &txt);
-        fwrite(txt.buf, 1, txt.len, out);
-    }
-    if (out) fclose(out);
+    if (out_fd >= 0) close(out_fd);
     if (rc == IMSAME_E_READ_TOO_LONG) terror("Read size reached for gapped alignment.");
+    const uint64_t acc = pr.accepted;
     printf("[INFO] Alignments computed in %e seconds.\n", now_s() - t0);
     printf("[INFO] %" PRIu64 " reads (%" PRIu64 ") from the query were found in the database (%" PRIu64
            ") at a minimum e-value of %Le and minimum coverage of %d%%.\n",
            acc, q.n, db.n, prm.min_e, (int)(100 * prm.min_coverage));
     printf("[INFO] The Jaccard-index is: %Le\n", (long double)acc / ((db.n + q.n) - acc));
     printf("[INFO] Deallocating heap memory.\n");
+    fflush(stdout);
     fprintf(stderr, "[imsame] rounds=%" PRIu64 " nw=%" PRIu64 " cells=%" PRIu64 " seed_ms=%.3f nw_ms=%.3f total_ms=%.3f\n",
-            st.rounds, st.n_nw, st.nw_cells, st.ms_seed, st.ms_nw, st.ms_total);
-    free(txt.buf);
-    free(res);
-    free(paths);
+            pr.st.rounds, pr.st.n_nw, pr.st.nw_cells, pr.st.ms_seed, pr.st.ms_nw, pr.st.ms_total);
+    fprintf(stderr, "[imsame] phases {\"devices\": %d, \"batches\": %" PRIu64 ", \"parse_db_s\": %.4f, \"index_s\": %.4f, "
+            "\"parse_query_s\": %.4f, \"upload_s\": %.4f, \"align_s\": %.4f, \"render_busy_s\": %.4f, "
+            "\"write_busy_s\": %.4f, \"render_tail_s\": %.4f, \"bytes_out\": %" PRIu64 ", \"accepted\": %" PRIu64
+            ", \"wall_s\": %.4f}\n",
+            G, pr.batches, t_parse_db, t_index, t_parse_q, t_upload, pr.t_align, pr.t_render, pr.t_write, pr.t_tail,
+            pr.bytes_out, acc, now_s() - t_wall);
     host_free_seqs(&db);
     host_free_seqs(&q);
-    imsame_dev_close(ctx);
+    pipe_close(dv, G);
     return 0;
 }

@@ -241,15 +241,41 @@ void host_free_seqs(host_seqs *s) {
 static void text_reserve(host_text *t, size_t n) {
     if (t->len + n <= t->cap) return;
     t->cap = (t->len + n) * 2 + 4096;
-    t->buf = realloc(t->buf, t->cap);
+    char *b = realloc(t->buf, t->cap);
+    if (!b) { fprintf(stderr, "[imsame] out of host memory (render)\n"); exit(-1); }
+    t->buf = b;
 }
 
-uint64_t host_render(const uint8_t *X, uint64_t xlen, const uint8_t *Y, uint64_t ylen, const imsame_read_result *r,
-                     const uint32_t *path, host_text *t) {
+/* bytes of build_alignment's text (alignmentFunctions.c:233-271) for a path
+ * whose strings start at head_x+1 / head_y+1 of 2*max(xlen, ylen) */
+uint64_t host_render_size(uint64_t xlen, uint64_t ylen, const imsame_read_result *r) {
     const uint64_t M = 2 * (xlen > ylen ? xlen : ylen);
-    char *rx = malloc(2 * M + 4), *ry = malloc(2 * M + 4);
-    memset(rx, 0, 2 * M + 4);
-    memset(ry, 0, 2 * M + 4);
+    uint64_t i = (uint64_t)r->head_x + 1, j = (uint64_t)r->head_y + 1, n = 1;
+    while (i <= M && j <= M) {
+        const uint64_t nx = M - i + 1 < IMSAME_ALIGN_LEN ? M - i + 1 : IMSAME_ALIGN_LEN;
+        const uint64_t ny = M - j + 1 < IMSAME_ALIGN_LEN ? M - j + 1 : IMSAME_ALIGN_LEN;
+        n += 2 * nx + ny + 3;
+        i += nx; j += ny;
+    }
+    return n;
+}
+
+/* backtrackingNW's strings (:493-560) from the path, right to left into
+ * rx/ry (scratch of >= 2M+2 bytes each, reused across records), then the
+ * 60-column blocks appended to t. */
+uint64_t host_render_scratch(const uint8_t *X, uint64_t xlen, const uint8_t *Y, uint64_t ylen,
+                             const imsame_read_result *r, const uint32_t *path, host_text *t, host_text *scratch) {
+    const uint64_t M = 2 * (xlen > ylen ? xlen : ylen);
+    if (scratch->cap < 2 * (M + 2) + IMSAME_ALIGN_LEN + 8) {
+        free(scratch->buf);
+        scratch->cap = 2 * (M + 2) + 4096;
+        scratch->buf = malloc(scratch->cap);
+        if (!scratch->buf) { fprintf(stderr, "[imsame] out of host memory (render)\n"); exit(-1); }
+    }
+    char *rx = scratch->buf, *ry = scratch->buf + M + 2;
+    /* the last block's match line pairs X with up to 60 bytes past ry[M]:
+     * zero there, as in the reference's memset buffers (never a '*') */
+    memset(ry + M + 1, 0, IMSAME_ALIGN_LEN + 4);
     uint64_t hx = M, hy = M, k;
     for (k = xlen - 1; k > r->bx; k--) rx[hx--] = '-';
     for (k = ylen - 1; k > r->by; k--) ry[hy--] = '-';
@@ -270,26 +296,35 @@ uint64_t host_render(const uint8_t *X, uint64_t xlen, const uint8_t *Y, uint64_t
     for (k = 0; k < py; k++) ry[hy--] = '-';
     if (px >= py) for (k = 0; k < px; k++) ry[hy--] = ' ';
     else          for (k = 0; k < py; k++) rx[hx--] = ' ';
-    /* build_alignment's loop (:233-271) */
-    t->len = 0;
+    /* build_alignment's loop (:233-271): the strings are [hx+1, M] and [hy+1, M]
+     * (the reference prints bytes of rec_X/rec_Y up to index M) */
+    text_reserve(t, host_render_size(xlen, ylen, r));
+    char *o = t->buf + t->len;
     uint64_t i = hx + 1, j = hy + 1, ident = 0;
     while (i <= M && j <= M) {
-        text_reserve(t, 3 * IMSAME_ALIGN_LEN + 8);
-        uint64_t bi = i, bj = j, o;
-        for (o = 0; o < IMSAME_ALIGN_LEN && i <= M; o++, i++) t->buf[t->len++] = rx[i];
-        t->buf[t->len++] = '\n';
-        for (o = 0; o < IMSAME_ALIGN_LEN && j <= M; o++, j++) t->buf[t->len++] = ry[j];
-        t->buf[t->len++] = '\n';
-        for (; bi < i; bi++, bj++) {
-            const int star = rx[bi] != '-' && ry[bj] != '-' && rx[bi] == ry[bj];
+        const uint64_t nx = M - i + 1 < IMSAME_ALIGN_LEN ? M - i + 1 : IMSAME_ALIGN_LEN;
+        const uint64_t ny = M - j + 1 < IMSAME_ALIGN_LEN ? M - j + 1 : IMSAME_ALIGN_LEN;
+        memcpy(o, rx + i, nx); o += nx; *o++ = '\n';
+        memcpy(o, ry + j, ny); o += ny; *o++ = '\n';
+        for (uint64_t b = 0; b < nx; b++) {
+            const char a = rx[i + b], c = ry[j + b];
+            const int star = a != '-' && c != '-' && a == c;
             ident += star;
-            t->buf[t->len++] = star ? '*' : ' ';
+            *o++ = star ? '*' : ' ';
         }
-        t->buf[t->len++] = '\n';
+        *o++ = '\n';
+        i += nx; j += ny;
     }
-    text_reserve(t, 2);
-    t->buf[t->len++] = '\n';
-    free(rx);
-    free(ry);
+    *o++ = '\n';
+    t->len = (size_t)(o - t->buf);
+    return ident;
+}
+
+uint64_t host_render(const uint8_t *X, uint64_t xlen, const uint8_t *Y, uint64_t ylen, const imsame_read_result *r,
+                     const uint32_t *path, host_text *t) {
+    host_text scratch = {0};
+    t->len = 0;
+    const uint64_t ident = host_render_scratch(X, xlen, Y, ylen, r, path, t, &scratch);
+    free(scratch.buf);
     return ident;
 }

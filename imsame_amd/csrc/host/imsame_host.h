@@ -34,5 +34,11 @@ int  host_read_file(const char *path, uint8_t **buf, uint64_t *len);
  * Returns the identities counted by the text loop. */
 uint64_t host_render(const uint8_t *X, uint64_t xlen, const uint8_t *Y, uint64_t ylen,
                      const imsame_read_result *r, const uint32_t *path, host_text *t);
+/* host_render APPENDING to t, with caller-owned scratch reused across
+ * records (no allocation per record once it has grown) */
+uint64_t host_render_scratch(const uint8_t *X, uint64_t xlen, const uint8_t *Y, uint64_t ylen,
+                             const imsame_read_result *r, const uint32_t *path, host_text *t, host_text *scratch);
+/* exact byte count of the text host_render produces for r */
+uint64_t host_render_size(uint64_t xlen, uint64_t ylen, const imsame_read_result *r);
 
 #endif

@@ -665,8 +665,9 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
     if (rc) return rc;
     // device path arena: what the caller offers, or what the last call needed per read
     uint32_t pcap = 0;
-    const uint64_t want_cap = std::max<uint64_t>(std::max<uint64_t>(paths_cap, 2ull * n + 1024),
-                                                 (uint64_t)(c->paths_hint * 1.25 * n) + 1024);
+    uint64_t want_cap = std::max<uint64_t>(std::max<uint64_t>(paths_cap, 2ull * n + 1024),
+                                           (uint64_t)(c->paths_hint * 1.25 * n) + 1024);
+    if (const char *pc = getenv("IMSAME_DEV_PATHS_CAP")) want_cap = strtoull(pc, nullptr, 10);   // test hook
     if ((rc = paths_setup(c, p, want_cap, &pcap))) return rc;
     if (n == 0) { if (stats) *stats = st; return IMSAME_OK; }
     if (c->res.ensure((uint64_t)n * 64) || c->cur_p.ensure((uint64_t)n * 8) || c->cur_h.ensure((uint64_t)n * 4) ||

@@ -67,9 +67,14 @@ def db_shard_records(db_starts, db_len, rank, world):
 
 
 def shard_keys(res, win, rank, world):
-    """Per-read key of this shard's result: window * world + rank if accepted."""
+    """Per-read key of this shard's result: window * world + rank if accepted.
+    An accepted row always carries the window of its hit
+    (imsame_dev_align_windows); ~0 there would make a negative key win the
+    min, so it is refused (the C sliced path refuses it with IMSAME_E_STATE)."""
     acc = res["status"] == 1
     w = np.asarray(win, dtype=np.uint64)
+    if np.any(w[acc] >= np.uint64(1) << np.uint64(62)):
+        raise ValueError("accepted read without the window of its hit")
     return np.where(acc, (w.astype(np.int64) * world + rank), NO_KEY).astype(np.int64)
 
 
@@ -91,7 +96,10 @@ def merge_shard_results(parts):
 def merge_db_sharded(res, win, rec_lo, rank, world):
     """merge_shard_results over torch.distributed ranks (RCCL "nccl" on
     GPUs, gloo on CPU): min all-reduce of the keys, sum all-reduce of the
-    winning rows (64 B each, so exactly one rank contributes a row)."""
+    winning rows (64 B each, so exactly one rank contributes a row).
+    The merged rows are the per-read results; their path_off/path_len point
+    into the WINNING rank's path arena, so .align text is rendered by that
+    rank (or after gathering its paths), not from the merged rows alone."""
     import torch
     import torch.distributed as dist
     dev = _device_for_backend()

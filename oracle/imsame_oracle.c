@@ -393,6 +393,8 @@ typedef struct {
     char **texts;                  /* optional: text of accepted reads */
     int status; uint64_t err_read, err_dbseq;
     uint64_t n_nw;
+    int mid;                       /* window view: start inside the chunk at read `from`,
+                                      having borrowed start[from]-1 from the read before */
 } or_chunk;
 
 /* Test-speed option, off by default: skip the NW of a (read, record) pair
@@ -412,8 +414,11 @@ static void *scan_chunk(void *arg) {
     /* An empty read at a chunk head makes the reference scan the rest of the
      * query as that read and reach NW with ylen = 0 (undefined behaviour).
      * Restated contract: skip it and let the next read open the chunk. */
-    while (r < ch->to && r + 1 < q->n && q->start[r] == q->start[r + 1]) r++;
-    uint64_t p = (r < q->n) ? q->start[r] : q->len;
+    if (!ch->mid)
+        while (r < ch->to && r + 1 < q->n && q->start[r] == q->start[r + 1]) r++;
+    /* mid-chunk (a window): every read before `from` left p at start[from]-1,
+     * accepted (:190) or scanned to its end (:93-105) */
+    uint64_t p = ch->mid ? q->start[r] - 1 : (r < q->n) ? q->start[r] : q->len;
     unsigned run = 0;                  /* consecutive bases buffered (crrSeqL) */
     while (r < ch->to && p < q->len) {
         uint64_t lim = (r + 1 < q->n) ? q->start[r + 1] - 1 : q->len;
@@ -553,6 +558,65 @@ int or_align(const uint8_t *dbs, uint64_t db_len, const uint64_t *db_start, uint
         fprintf(stderr, "[oracle] index %.2f s, align %.2f s\n", (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec),
                 (t2.tv_sec - t1.tv_sec) + 1e-9 * (t2.tv_nsec - t1.tv_nsec));
     if (err_read) *err_read = er;
+    or_free_index(&ix);
+    free(db.start); free(q.start); free(db.brk);
+    return st;
+}
+
+/* or_align restricted to the reads of windows [from[w], to[w]) of the WHOLE
+ * query: the same chunk heads (IMSAME.c:414,430-452), each chunk's part
+ * inside a window scanned with the state the reference's thread has on
+ * reaching it (a read inside a chunk borrows the previous read's last base,
+ * Q4).  Lets tests compare windows deep inside a large query without
+ * running all of it; the index is built once.  res: n_q entries (only the
+ * windows' are written). */
+int or_align_windows(const uint8_t *dbs, uint64_t db_len, const uint64_t *db_start, uint64_t n_db,
+                     const uint8_t *db_brk, const uint8_t *qs, uint64_t q_len, const uint64_t *q_start, uint64_t n_q,
+                     const imsame_params *prm, uint64_t T, uint64_t nwin, const uint64_t *wfrom, const uint64_t *wto,
+                     imsame_read_result *res, uint64_t *err_read) {
+    or_seqs db = { (uint8_t *)dbs, malloc((n_db + 1) * sizeof(uint64_t)), n_db, db_len, NULL, 0 };
+    or_seqs q  = { (uint8_t *)qs,  malloc((n_q + 1) * sizeof(uint64_t)),  n_q,  q_len,  NULL, 0 };
+    memcpy(db.start, db_start, n_db * sizeof(uint64_t)); db.start[n_db] = db_len;
+    memcpy(q.start, q_start, n_q * sizeof(uint64_t));    q.start[n_q] = q_len;
+    db.brk = calloc(db_len / 8 + 2, 1);
+    if (db_brk) memcpy(db.brk, db_brk, (db_len + 7) / 8);
+    for (uint64_t s = 0; s < n_db; s++)
+        if (db.start[s] < db_len) db.brk[db.start[s] >> 3] |= (uint8_t)(1u << (db.start[s] & 7));
+    or_index ix;
+    or_build_index(&db, &ix);
+    if (T == 0) T = 1;
+    const uint64_t rpt = (uint64_t)floorl((long double)n_q / (long double)T);
+    const uint64_t nc = T * nwin;
+    or_chunk *ch = calloc(nc, sizeof(or_chunk));
+    pthread_t *th = calloc(nc, sizeof(pthread_t));
+    int *started = calloc(nc, sizeof(int));
+    for (uint64_t w = 0; w < nwin; w++)
+        for (uint64_t r = wfrom[w]; r < wto[w]; r++) {
+            memset(&res[r], 0, sizeof res[r]);
+            res[r].ylen = (uint32_t)(q.start[r + 1] - q.start[r]);
+        }
+    for (uint64_t w = 0; w < nwin; w++)
+        for (uint64_t t = 0; t < T; t++) {
+            const uint64_t f = t * rpt, e = (t == T - 1) ? n_q : (t + 1) * rpt;
+            const uint64_t lo = f > wfrom[w] ? f : wfrom[w], hi = e < wto[w] ? e : wto[w];
+            if (lo >= hi) continue;
+            or_chunk *c = &ch[w * T + t];
+            c->db = &db; c->q = &q; c->ix = &ix; c->prm = prm; c->res = res;
+            c->from = lo; c->to = hi;
+            /* the chunk's head role passes over empty reads: mid-chunk only
+             * if a read of [f, lo) has bases */
+            c->mid = lo > f && q.start[f] != q.start[lo];
+            started[w * T + t] = pthread_create(&th[w * T + t], NULL, scan_chunk, c) == 0 ? 1 : 2;
+            if (started[w * T + t] == 2) scan_chunk(c);
+        }
+    int st = 0;
+    uint64_t er = 0;
+    for (uint64_t k = 0; k < nc; k++) {
+        if (started[k] == 1) pthread_join(th[k], NULL);
+        if (started[k] && ch[k].status && (!st || ch[k].err_read < er)) { st = ch[k].status; er = ch[k].err_read; }
+    }
+    if (err_read) *err_read = er;
+    free(ch); free(th); free(started);
     or_free_index(&ix);
     free(db.start); free(q.start); free(db.brk);
     return st;

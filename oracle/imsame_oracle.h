@@ -52,6 +52,13 @@ int or_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_start, uint6
              const imsame_params *prm, uint64_t n_threads, imsame_read_result *res,
              uint64_t *err_read);
 
+/* or_align over the reads of DISJOINT windows [from[w], to[w]) only, with the whole
+ * query's chunk heads (res has n_q entries; the windows' are written). */
+int or_align_windows(const uint8_t *db, uint64_t db_len, const uint64_t *db_start, uint64_t n_db,
+                     const uint8_t *db_brk, const uint8_t *q, uint64_t q_len, const uint64_t *q_start, uint64_t n_q,
+                     const imsame_params *prm, uint64_t n_threads, uint64_t nwin, const uint64_t *from,
+                     const uint64_t *to, imsame_read_result *res, uint64_t *err_read);
+
 /* Reverse complement of a FASTA byte image (reverseComplement.c semantics). */
 int or_revcomp(const uint8_t *in, uint64_t in_len, uint8_t *out, uint64_t out_cap, uint64_t *out_len);
 /* test-speed option: skip re-running NW for (read, record) pairs already

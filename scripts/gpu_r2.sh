@@ -1,0 +1,44 @@
+#!/usr/bin/env bash
+# One GPU-box pass for round 2:  gpurun -- bash scripts/gpu_r2.sh <tag> [steps...]
+# steps: tests newtests smoke bench prof pmc ; a step that fails with anything
+# but pytest's "tests failed" (1) ends the script (no GPU work after a fault).
+set -uo pipefail
+TAG=${1:-x}; shift || true
+STEPS=${*:-"tests smoke bench prof"}
+cd "${GRAFT_REPO_ROOT:-.}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+ok_or_stop() {   # $1 = exit status, $2 = step
+  echo "$2 rc=$1" >> gpurun_out/steps_${TAG}.txt
+  if [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; then echo "stopping after $2 (rc $1)"; exit "$1"; fi
+}
+for s in $STEPS; do
+  case $s in
+    tests) timeout -k 10 1200 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
+             > gpurun_out/pytest_gpu_${TAG}.log 2>&1; ok_or_stop $? tests ;;
+    newtests) timeout -k 10 900 python -u -m pytest tests/test_gpu.py -m gpu -v --timeout 300 --timeout-method thread \
+             -k "query_shards or path_arena or cli_devices or multi_device or full_c2 or c3_" \
+             > gpurun_out/pytest_new_${TAG}.log 2>&1; ok_or_stop $? newtests ;;
+    smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_${TAG}.log 2>&1
+           ok_or_stop $? smoke ;;
+    bench) timeout -k 10 900 python -u bench.py > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err
+           ok_or_stop $? bench ;;
+    benchq) timeout -k 10 600 python -u bench.py --cpu-sample 0 --e2e off > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err
+           ok_or_stop $? benchq ;;
+    c5w) timeout -k 10 900 python -u bench.py --config c5w --steps 1 --warmup 0 > gpurun_out/bench_c5w_${TAG}.json \
+           2> gpurun_out/bench_c5w_${TAG}.err; ok_or_stop $? c5w ;;
+    prof) timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d gpurun_out/prof_${TAG} -o kt --output-format csv \
+            -- python3 bench.py --steps 2 --warmup 1 --cpu-sample 0 --e2e off > gpurun_out/bench_prof_${TAG}.json \
+            2> gpurun_out/bench_prof_${TAG}.err; ok_or_stop $? prof ;;
+    pmc) i=0
+         for grp in "SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_BUSY_CYCLES" \
+                    "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE"; do
+           i=$((i+1))
+           timeout -s KILL 300 rocprofv3 --pmc $grp --kernel-include-regex 'nw16_kernel|seed_' -T \
+             -d gpurun_out/pmc_${TAG}_p$i -o pmc --output-format csv \
+             -- python3 bench.py --steps 1 --warmup 0 --cpu-sample 0 --e2e off > gpurun_out/pmc_${TAG}_p$i.json \
+             2> gpurun_out/pmc_${TAG}_p$i.err
+           ok_or_stop $? pmc$i
+         done ;;
+  esac
+done

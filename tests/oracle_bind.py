@@ -58,6 +58,10 @@ class Oracle:
         lib.or_align.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p,
                                  C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
                                  C.POINTER(Params), C.c_uint64, C.c_void_p, C.POINTER(C.c_uint64)]
+        lib.or_align_windows.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p,
+                                         C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
+                                         C.POINTER(Params), C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p,
+                                         C.c_void_p, C.POINTER(C.c_uint64)]
         lib.or_revcomp.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
         lib.or_params_default.argtypes = [C.POINTER(Params)]
 
@@ -108,6 +112,27 @@ class Oracle:
                                q.ctypes.data, len(q), qs.ctypes.data, len(qs),
                                C.byref(p), n_threads, res.ctypes.data, C.byref(er))
         return rc, res, er.value
+
+    def align_windows(self, db, db_start, q, q_start, windows, params=None, n_threads=1, db_brk=None):
+        """Per-read results of the reads of windows [(a, b), ...] of the whole
+        query (its chunk heads), without aligning the rest: (rc, [res of each
+        window], err)."""
+        db = np.ascontiguousarray(db, dtype=np.uint8)
+        q = np.ascontiguousarray(q, dtype=np.uint8)
+        dbs = np.ascontiguousarray(db_start, dtype=np.uint64)
+        qs = np.ascontiguousarray(q_start, dtype=np.uint64)
+        p = params if params is not None else self.params()
+        res = np.zeros(len(qs), dtype=RESULT_DTYPE)
+        wf = np.array([w[0] for w in windows], dtype=np.uint64)
+        wt = np.array([w[1] for w in windows], dtype=np.uint64)
+        er = C.c_uint64()
+        brk = None if db_brk is None else np.ascontiguousarray(db_brk, dtype=np.uint8)
+        rc = self.lib.or_align_windows(db.ctypes.data, len(db), dbs.ctypes.data, len(dbs),
+                                       None if brk is None else brk.ctypes.data,
+                                       q.ctypes.data, len(q), qs.ctypes.data, len(qs),
+                                       C.byref(p), n_threads, len(windows), wf.ctypes.data, wt.ctypes.data,
+                                       res.ctypes.data, C.byref(er))
+        return rc, [res[a:b] for a, b in windows], er.value
 
     def revcomp(self, data):
         src = np.frombuffer(data, dtype=np.uint8)

@@ -212,14 +212,23 @@ def test_long_reads_multi_strip(dev, oracle):
     assert not _cmp(res, exp), _cmp(res, exp)
 
 
+def _windows(n, w=1500, T=16):
+    """start, middle (around a chunk head of -n_threads T) and end of a query"""
+    rpt = n // T
+    mid = (T // 2) * rpt
+    return [(0, w), (mid - w // 2, mid + w // 2), (n - w, n)]
+
+
 def test_full_c2_reference_properties(dev, oracle):
-    """BASELINE configs[1] reference (50 Mbp, 25k records) with 100k reads:
-    parity on a prefix sample vs the oracle + self-consistency on all."""
+    """BASELINE configs[1] reference (50 Mbp, 25k records) with 100k reads at
+    -n_threads 16: parity vs the oracle on three windows of the WHOLE query
+    (start, a chunk head in the middle, the end -- 4,500 reads) + path
+    self-consistency on all accepted reads' first 2000."""
     ref, rst = synth.make_reference_arr(50_000_000, 2_000, seed=42)
     q, qs = synth.make_reads_arr(ref, 100_000, 150, seed=43)
     dev.index(ref, rst)
     dev.set_query(q, qs)
-    res, paths, st = dev.align(n_threads=1, want_paths=True)
+    res, paths, st = dev.align(n_threads=16, want_paths=True)
     acc = res["status"] == 1
     assert acc.mean() > 0.85
     # every accepted path re-renders to the device's own identity count
@@ -230,11 +239,12 @@ def test_full_c2_reference_properties(dev, oracle):
         Y = q[int(qs[k]):int(qs[k]) + int(r["ylen"])]
         _, ident = render(X.tobytes(), Y.tobytes(), r, paths[r["path_off"]:r["path_off"] + r["path_len"]])
         assert ident == r["identities"]
-    # oracle on the first 1500 reads (T = 1: only the sample's last read sees a
-    # different end-of-query bound, so it is excluded)
-    n = 1500
-    rc, exp, _ = oracle.align(ref, rst, q[:int(qs[n])], qs[:n], None, 1)
-    assert not _cmp(res[:n - 1], exp[:n - 1]), _cmp(res[:n - 1], exp[:n - 1])
+    wins = _windows(len(qs))
+    rc, exp, _ = oracle.align_windows(ref, rst, q, qs, wins, None, 16)
+    assert rc == 0
+    for (a, b), e in zip(wins, exp):
+        assert not _cmp(res[a:b], e), ((a, b), _cmp(res[a:b], e))
+    assert sum(b - a for a, b in wins) >= 4_500
 
 
 @pytest.fixture
@@ -250,13 +260,14 @@ def oracle_memo(oracle):
 @pytest.mark.timeout(300)
 def test_c3_reference_500mbp(dev, oracle_memo):
     """BASELINE configs[2] per-GPU shard: 1.25M x 150 bp reads (10M / 8) vs
-    the 500 Mbp reference (250k records, 4 GB of CSR entries): oracle parity
-    on a prefix, path self-consistency and the accepted fraction on all."""
+    the 500 Mbp reference (250k records, 4 GB of CSR entries), -n_threads 16:
+    oracle parity on three windows of the whole query (start, a chunk head in
+    the middle, the end), path self-consistency and the accepted fraction."""
     ref, rst = synth.make_reference_arr(500_000_000, 2_000, seed=43)
     q, qs = synth.make_reads_arr(ref, 1_250_000, 150, seed=44)
     dev.index(ref, rst)
     dev.set_query(q, qs)
-    res, paths, st = dev.align(n_threads=1, want_paths=True)
+    res, paths, st = dev.align(n_threads=16, want_paths=True)
     acc = res["status"] == 1
     assert acc.mean() > 0.85, acc.mean()
     for k in np.flatnonzero(acc)[:1000]:
@@ -266,10 +277,11 @@ def test_c3_reference_500mbp(dev, oracle_memo):
         Y = q[int(qs[k]):int(qs[k]) + int(r["ylen"])]
         _, ident = render(X.tobytes(), Y.tobytes(), r, paths[r["path_off"]:r["path_off"] + r["path_len"]])
         assert ident == r["identities"]
-    n = 1000
-    rc, exp, _ = oracle_memo.align(ref, rst, q[:int(qs[n])], qs[:n], None, 1)
+    wins = _windows(len(qs))
+    rc, exp, _ = oracle_memo.align_windows(ref, rst, q, qs, wins, None, 16)
     assert rc == 0
-    assert not _cmp(res[:n - 1], exp[:n - 1]), _cmp(res[:n - 1], exp[:n - 1])
+    for (a, b), e in zip(wins, exp):
+        assert not _cmp(res[a:b], e), ((a, b), _cmp(res[a:b], e))
 
 
 @pytest.mark.timeout(300)
@@ -436,3 +448,95 @@ def test_cli_sliced_matches_reference_golden(name):
                 continue
             blob = open(outp, "rb").read() if os.path.exists(outp) else b""
             G.check_cli_against_golden(case, int(T), p.returncode, p.stdout, blob)
+
+
+def test_query_shards_equal_whole_run(dev, oracle):
+    """imsame_dev_set_query_range: each device holds only its shard of the
+    query (bench.py strong scaling, imsame -devices).  Shards of the
+    bench's split for 2, 3 and 8 ranks, and cuts after empty-free odd
+    places, concatenate to the whole-query run bit for bit (-n_threads 16:
+    chunk heads inside and outside the shards)."""
+    from imsame_amd.dist import shard_range
+    ref, rst = synth.make_reference_arr(2_000_000, 2_000, seed=42)
+    q, qs = synth.make_reads_arr(ref, 12_000, 150, seed=43)
+    dev.index(ref, rst)
+    dev.set_query(q, qs)
+    whole, _, _ = dev.align(n_threads=16)
+    for world in (2, 3, 8):
+        parts = []
+        for rank in range(world):
+            a, b = shard_range(len(qs), rank, world)
+            dev.set_query(q, qs, a, b)
+            parts.append(dev.align(a, b, n_threads=16)[0])
+        got = np.concatenate(parts)
+        assert not _cmp(got, whole), (world, _cmp(got, whole))
+    dev.set_query(q, qs, 749, 7501)                       # sub-ranges of a shard
+    got = np.concatenate([dev.align(749, 750, n_threads=16)[0], dev.align(750, 7501, n_threads=16)[0]])
+    assert not _cmp(got, whole[749:7501])
+    with pytest.raises(abi_error()):
+        dev.align(0, 10, n_threads=16)                    # outside the uploaded range
+    rc, exp, _ = oracle.align(ref, rst, q, qs, None, 16)
+    assert rc == 0 and not _cmp(whole, exp)
+
+
+def test_path_arena_overflow_rewalks_only_lost_reads(dev, monkeypatch):
+    """A device path arena too small for the accepted reads' paths: only the
+    reads whose path did not fit are re-walked (NW is pure, Appendix A Q18),
+    giving the same rows and the same .align text as an arena with room;
+    a host arena too small gets IMSAME_E_PATHS and fetches afterwards."""
+    ref, rst = synth.make_reference_arr(2_000_000, 2_000, seed=7)
+    q, qs = synth.make_reads_arr(ref, 6_000, 150, seed=8, ins=0.01, dele=0.01)
+    dev.index(ref, rst)
+    dev.set_query(q, qs)
+    base, bp, bst = dev.align(n_threads=8, want_paths=True)
+    assert bst.n_rewalk == 0
+    monkeypatch.setenv("IMSAME_DEV_PATHS_CAP", "3000")
+    res, paths, st = dev.align(n_threads=8, want_paths=True, paths_cap=16)
+    monkeypatch.delenv("IMSAME_DEV_PATHS_CAP")
+    assert st.n_rewalk > 100, st.n_rewalk
+    assert not _cmp(res, base)
+    for k in np.flatnonzero(res["status"] == 1)[::7]:
+        r, r0 = res[k], base[k]
+        s = int(r["db_seq"])
+        X = ref[int(rst[s]):int(rst[s]) + 2_000].tobytes()
+        Y = q[int(qs[k]):int(qs[k]) + 150].tobytes()
+        t1, _ = render(X, Y, r, paths[r["path_off"]:r["path_off"] + r["path_len"]])
+        t0, _ = render(X, Y, r0, bp[r0["path_off"]:r0["path_off"] + r0["path_len"]])
+        assert t1 == t0, k
+
+
+@pytest.mark.parametrize("name", G.e2e_cases())
+def test_cli_devices_matches_reference_golden(name):
+    """imsame -devices 0,0 (two contexts, each holding one shard of the
+    query) with tiny batches and 3 render threads: the reference's .align
+    bytes and [INFO] lines for every -n_threads."""
+    case = G.e2e_case(name)
+    for T in case["meta"]["runs"]:
+        with tempfile.TemporaryDirectory() as td:
+            outp = os.path.join(td, "o.align")
+            p = subprocess.run([CLI, "-query", case["query"], "-db", case["db"], "-out", outp, "-n_threads", T,
+                                "-devices", "0,0", "-batch_reads", "7", "-render_threads", "3",
+                                *case["meta"]["extra"]], stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=300)
+            blob = open(outp, "rb").read() if os.path.exists(outp) else b""
+            G.check_cli_against_golden(case, int(T), p.returncode, p.stdout, blob)
+
+
+def test_cli_multi_device_output_identical(tmp_path):
+    """C2 shape (2 Mbp, 12k reads) through the CLI: one context vs three
+    (-devices 0,0,0) with batches of 1000 reads -- identical .align bytes,
+    equal to the device results rendered record by record."""
+    ref, rst = synth.make_reference_arr(2_000_000, 2_000, seed=42)
+    q, qs = synth.make_reads_arr(ref, 12_000, 150, seed=43)
+    dbf, qf = str(tmp_path / "db.fa"), str(tmp_path / "q.fa")
+    synth.write_fasta(dbf, ref, rst, "ref")
+    synth.write_fasta(qf, q, qs, "read", width=0)
+    outs = []
+    for extra in ([], ["-devices", "0,0,0", "-batch_reads", "1000"], ["-render_threads", "1"]):
+        o = str(tmp_path / f"o{len(outs)}.align")
+        p = subprocess.run([CLI, "-query", qf, "-db", dbf, "-out", o, "-n_threads", "16", *extra],
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=300)
+        assert p.returncode == 0, p.stderr[-2000:]
+        assert b'"accepted"' in p.stderr
+        outs.append(open(o, "rb").read())
+    assert outs[0] == outs[1] == outs[2]
+    assert outs[0].count(b" $$$$$$$ \n") > 10_000

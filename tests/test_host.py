@@ -305,3 +305,29 @@ def test_emulated_query_shards_equal_whole_run(emu, oracle, name, monkeypatch):
             got = np.concatenate(parts)
             for f in PARITY_FIELDS:
                 assert np.array_equal(got[f], exp[f]), (name, T, k, f)
+
+
+def test_render_of_emulated_paths_matches_reference_text(emu, oracle):
+    """host_render (the CLI's .align text, alignmentFunctions.c:210-274, with
+    scratch reused across records) from paths the kernel source produces:
+    the reference's text bytes (SHA-1 of the golden pairs) and identities."""
+    import hashlib
+    rows = [r for r in G.nw_pairs() if len(r["X"]) * len(r["Y"]) <= 60_000 and r["igap"] == -5 and r["egap"] == -2]
+    rows = [r for r in rows if len(r["Y"]) <= 160][:60]
+    assert len(rows) > 20
+    p = oracle.params(min_coverage=1e-9, min_identity=1e-9)
+    p.want_paths = 1
+    X = [r["X"].encode() for r in rows]
+    Y = [r["Y"].encode() for r in rows]
+    rc, res, paths, flags = emu.nw_pairs(X, Y, p, paths_cap=sum(len(x) + len(y) for x, y in zip(X, Y)) + 16)
+    assert rc == 0 and flags == 0
+    n = 0
+    for k, r in enumerate(rows):
+        if res[k]["status"] != 1:
+            continue
+        pk = paths[res[k]["path_off"]:res[k]["path_off"] + res[k]["path_len"]]
+        txt, ident = imsame_amd.render(X[k], Y[k], res[k], pk)
+        assert hashlib.sha1(txt).hexdigest() == r["text_sha1"], k
+        assert ident == r["identities"]
+        n += 1
+    assert n > 20

@@ -12,6 +12,7 @@ import numpy as np
 import pytest
 
 from tests import golden_io as G
+from imsame_amd import fasta, PARITY_FIELDS
 from tests.oracle_bind import Oracle
 
 
@@ -104,3 +105,28 @@ def test_parallel_index_build_matches_serial(oracle, monkeypatch):
         assert rc == 0
     assert (out["1"]["status"] == 1).sum() > 2_500
     assert np.array_equal(out["1"], out["7"])
+
+
+@pytest.mark.parametrize("name", ["empty_not_head", "borrowed", "edges", "small_c2like"])
+def test_oracle_windows_equal_whole_run(oracle, name):
+    """or_align_windows (reads [a, b) of the whole query, its chunk heads) ==
+    the same reads of or_align over everything: the checker used for windows
+    deep inside large GPU runs (tests/test_gpu.py)."""
+    case = G.e2e_case(name)
+    db, dbs, brk = fasta.load(case["db"], True)
+    q, qs, _ = fasta.load(case["query"])
+    n = len(qs)
+    runs = [int(t) for t in case["meta"]["runs"]]
+    for T in sorted({runs[0], runs[-1]}):
+        rc, exp, er = oracle.align(db, dbs, q, qs, None, T, brk)
+        if rc:
+            continue
+        # one window per call, then disjoint windows in one call
+        calls = [[(0, max(1, n // 2))], [(n // 3, n)], [(1, n - 1)], [(0, n // 3), (n // 2, n // 2 + 1)]]
+        for ws in calls:
+            ws = [w for w in ws if w[1] > w[0]]
+            rc2, got, _ = oracle.align_windows(db, dbs, q, qs, ws, None, T, brk)
+            assert rc2 == 0
+            for (a, b), g in zip(ws, got):
+                for f in PARITY_FIELDS:
+                    assert np.array_equal(g[f], exp[f][a:b]), (name, T, a, b, f)
