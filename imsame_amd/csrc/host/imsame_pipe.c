@@ -368,6 +368,7 @@ int pipe_align_render(pipe_dev *d, int G, const host_seqs *db, const host_seqs *
     }
     for (int g = 0; g < G; ++g)
         if (started[g]) pthread_join(th[g], NULL);
+    if (stop_read < n && !rc) rc = IMSAME_E_READ_TOO_LONG;       /* its batch may start at the read */
     for (k = 0; k < total; ++k) {
         if (B[k].t_done > t_last) t_last = B[k].t_done;
         add_stats(&r->st, &B[k].st);
