@@ -32,7 +32,8 @@
 //
 // Traceback, three dwords per lane per step (0.6 B/cell):
 //   WM  cells 0-7: bit s = NOT-diag(A), 8+s NOT-diag(B), 16+s up(A), 24+s up(B)
-//       -- one v_perm gathers the four sign bits of (d0 - lu, l0 - u0)
+//       -- one v_perm turns the four signs of (d0 - lu, l0 - u0) into 0xFF/0x00
+//          bytes (selectors 8-11 replicate bits 15/31/47/63)
 //   WU  cells 0-7: bit s = U(A), 8+s NOT-L(A), 16+s U(B), 24+s NOT-L(B)
 //   WX  cells 8-9 (s' = s - 8): moves at s', 8+s', 16+s', 24+s';
 //       U(A) 2+s', NOT-L(A) 4+s', U(B) 18+s', NOT-L(B) 20+s'
@@ -223,7 +224,8 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
                 if (s == 0) v = leadc0 ? sc : v;                      // column 0 (:426)
                 cur[s] = pre ? own[s] : v;
                 // move bits: signs of (d0 - lu) [not diagonal] and (l0 - up) [up > left] (:457-472)
-                const uint32_t P2 = wv_perm(pk_sub(l0, up), pk_sub(d0, lu), 0x07050301u);
+                // (sign-replicating selectors 8-11: bytes 0xFF / 0x00, no shift before packing)
+                const uint32_t P2 = wv_perm(pk_sub(l0, up), pk_sub(d0, lu), 0x0B0A0908u);
                 // column max of column j-1 over rows <= i-2, strict > (:476-480)
                 const uint32_t mU = pk_neg_mask(pk_sub(mcS[s], u2));
                 const uint32_t u0n = wv_bfi(mU, pk_add(u2, IG2E), pk_add(u0[s], EG));
@@ -235,12 +237,12 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
                 mfS = wv_bfi(mnL, mfS, d0);
                 if (s == 0) { mfS = leadc0 ? NBIG : mfS; l0 = leadc0 ? NBIG : l0; }   // j = 1: mf = T[i][0]
                 if (s < 8) {
-                    wm = wv_and_or(P2 >> (7 - s), 0x01010101u << s, wm);
+                    wm = wv_and_or(P2, 0x01010101u << s, wm);
                     wu = wv_and_or(mU, 0x00010001u << s, wu);
                     wu = wv_and_or(mnL, 0x01000100u << s, wu);
                 } else {
                     const int q = s - 8;
-                    wx = wv_and_or(P2 >> (7 - q), 0x01010101u << q, wx);
+                    wx = wv_and_or(P2, 0x01010101u << q, wx);
                     wx = wv_and_or(mU, 0x00040004u << q, wx);
                     wx = wv_and_or(mnL, 0x00100010u << q, wx);
                 }
