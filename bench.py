@@ -169,6 +169,7 @@ def main():
     pin = imsame_amd.PinnedArray(len(q))              # page-locked source of the per-step upload
     pin.array[:] = q
     qp = pin.array
+    rpin = imsame_amd.PinnedArray(hi - lo, imsame_amd.RESULT_DTYPE)   # page-locked results, reused
     params = dev.params(max_read_size=cfg["max_rs"]) if cfg["max_rs"] else dev.params()
 
     n_slices = 1
@@ -183,7 +184,7 @@ def main():
             res, paths, st, n_slices = dev.align_sliced(ref, rst, a.slice_bases, n_threads=a.n_threads,
                                                         params=params, read_from=lo, read_to=hi)
             return res, paths, st
-        return dev.align(lo, hi, n_threads=a.n_threads, params=params)
+        return dev.align(lo, hi, n_threads=a.n_threads, params=params, out=rpin.array)
 
     def barrier():
         if dist is not None:
@@ -201,6 +202,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     accepted = int((res["status"] == 1).sum())
+    res = res.copy()
     if dist is not None:
         from imsame_amd.dist import all_reduce     # RCCL: max of the clocks, sum of the counters
         elapsed = all_reduce([elapsed], op="max")[0]
@@ -276,12 +278,14 @@ def main():
                        "nw_cells": last["nw_cells"], "n_nw": last["n_nw"],
                        "ms_seed": round(last["ms_seed"], 3), "ms_nw": round(last["ms_nw"], 3),
                        "ms_align_call": round(last["ms_total"], 3),
+                       "ms_host_setup": round(last["ms_setup"], 3), "ms_d2h_results": round(last["ms_d2h"], 3),
                        "nw_launch_cand": last["launch_cand"],
                        "nw_launch_ms": [round(x, 3) for x in last["launch_ms"]]},
         }
         print(json.dumps(line), flush=True)
     dev.close()
     pin.free()
+    rpin.free()
     if dist is not None:
         dist.destroy_process_group()
 

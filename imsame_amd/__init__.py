@@ -209,15 +209,21 @@ class Device:
         return paths[:used.value]
 
     def align(self, read_from=None, read_to=None, n_threads=4, params=None, want_paths=False, paths_cap=None,
-              allow_too_long=False):
+              allow_too_long=False, out=None):
         """Per-read results (numpy RESULT_DTYPE) for reads [read_from, read_to)
-        (default: the uploaded range)."""
+        (default: the uploaded range).  out: a RESULT_DTYPE array to fill
+        (e.g. a PinnedArray's, reused across calls)."""
         read_from = self.q_range[0] if read_from is None else read_from
         read_to = self.q_range[1] if read_to is None else read_to
         p = params if params is not None else self.params()
         p.want_paths = 1 if want_paths else 0
         n = read_to - read_from
-        res = np.zeros(n, dtype=RESULT_DTYPE)
+        if out is not None:
+            if out.dtype != RESULT_DTYPE or len(out) < n or not out.flags.c_contiguous:
+                raise ImsameError(abi.IMSAME_E_ARG, "align(out=): RESULT_DTYPE array of >= n rows")
+            res = out[:n]
+        else:
+            res = np.zeros(n, dtype=RESULT_DTYPE)
         cap = (paths_cap if paths_cap is not None else 8 * n + 1024) if want_paths else 0
         st = Stats()
         used = C.c_uint64()

@@ -693,6 +693,7 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
                     c->cur_h.as<uint32_t>(), c->nmemo.as<uint8_t>(), c->rstat.as<uint8_t>(), c->act0.as<uint32_t>()};
     init_kernel<<<nblk(n, 256), 256, 0, s>>>(I);
     HIPCHK(hipGetLastError());
+    st.ms_setup = now_ms() - t_start;
 
     const uint32_t short_y = std::min<uint32_t>(ycap, NW_W / 2);
     uint32_t nact = n;
@@ -712,7 +713,7 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
         S.cur_p = c->cur_p.as<uint64_t>(); S.cur_h = c->cur_h.as<uint32_t>(); S.memo = c->memo.as<uint32_t>();
         S.nmemo = c->nmemo.as<uint8_t>(); S.rstat = c->rstat.as<uint8_t>();
         S.minraw = c->minraw.as<uint64_t>(); S.n_minraw = ymax + 1;
-        S.max_rs = p->max_read_size; S.short_ylen = short_y;
+        S.max_rs = p->max_read_size; S.short_ylen = short_y; S.max_rec = c->max_rec;
         S.spec = (st.rounds == 1) ? 1u : std::max<uint32_t>(1u, std::min<uint32_t>(spec_later, n / nact));
         S.budget = seed_budget(budget1, (uint32_t)st.rounds);
         S.next = nxt; S.nnext = (uint32_t *)(ctr + C_NNEXT);
@@ -790,8 +791,11 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
     }
     uint64_t hc[C_NSLOTS];
     HIPCHK(hipMemcpyAsync(hc, ctr, C_NSLOTS * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    const double t_d2h = now_ms();
     HIPCHK(hipMemcpyAsync(res, c->res.p, (uint64_t)n * 64, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    st.ms_d2h = now_ms() - t_d2h;
     st.n_hits = hc[C_HITS];
     st.nw_cells = hc[C_CELLS];
     st.n_accepted = hc[C_NACC];

@@ -27,6 +27,7 @@ struct SeedLaunch {
     uint64_t *cur_p; uint32_t *cur_h; uint32_t *memo; uint8_t *nmemo; uint8_t *rstat;
     const uint64_t *minraw; uint32_t n_minraw;
     uint64_t max_rs; uint32_t short_ylen;
+    uint64_t max_rec;                      // longest database record (a-priori rejection of whole reads)
     uint32_t spec;                         // candidates a read may emit this round (1..SPEC_MAX)
     uint32_t budget;                       // ungapped extensions a read may run this round (0: no limit)
     uint32_t *next, *nnext;                // reads that paused on the budget (next round's active list)
@@ -155,6 +156,19 @@ __device__ __forceinline__ bool nw_cannot_accept(const SeedLaunch &S, uint64_t x
     return mi == 0xFFFFFFFFu || (uint64_t)mi > (xlen < ylen ? xlen : ylen);
 }
 
+// A hit whose record cannot be accepted for this read AND cannot trip the
+// size abort (both lengths within max_read_size) has no observable effect
+// whatever its e-value: the reference would extend it and either fail the
+// e-value test or run an NW it then rejects.  Skipped before the extension.
+__device__ __forceinline__ bool hit_irrelevant(const SeedLaunch &S, uint64_t xlen, uint64_t ylen) {
+    return xlen <= S.max_rs && ylen <= S.max_rs && nw_cannot_accept(S, xlen, ylen);
+}
+// ... and when even the longest record cannot accept the read, nothing the
+// read's scan meets can: its outcome is "not found" without a scan.
+__device__ __forceinline__ bool read_irrelevant(const SeedLaunch &S, uint64_t ylen) {
+    return S.max_rec <= S.max_rs && hit_irrelevant(S, S.max_rec, ylen);
+}
+
 __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint64_t &hits) {
     const uint64_t r = S.active[idx], k = r - S.read_from;
     const uint64_t rs = S.q_start[r], re = S.q_start[r + 1];
@@ -176,6 +190,7 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint
     for (int m = 0; m < MEMO; ++m) memo[m] = (m < (int)nm) ? S.memo[k * MEMO + m] : 0xFFFFFFFFu;
     const uint64_t mraw = ylen < S.n_minraw ? S.minraw[ylen] : ~0ull;
     const int64_t ys = (int64_t)rs, ye = (r == S.n_q - 1) ? (int64_t)S.q_len : (int64_t)re - 1;
+    if (read_irrelevant(S, ylen)) { S.rstat[k] = RS_DONE; return; }      // nothing can be accepted
     // Up to `spec` e-value-passing hits of distinct, not-yet-rejected records,
     // in visiting order.  NW(record, read) is pure (Q18): whichever of them is
     // accepted first in this order is exactly the reference's accepted hit,
@@ -209,6 +224,7 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint
             for (int m = 0; m < MEMO; ++m) skip |= memo[m] == sid;
             for (uint32_t m = 0; m < ne; ++m) skip |= emit[m] == sid;
             if (skip) continue;                 // NW(sid, r) already rejected or pending (Q18)
+            if (hit_irrelevant(S, S.db_start[sid + 1] - S.db_start[sid], ylen)) continue;
             if (budget == 0) {
                 S.cur_p[k] = p; S.cur_h[k] = h;                      // resume at this hit
                 paused = stop = true;
@@ -322,7 +338,8 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
 #pragma unroll
     for (int m = 0; m < SPEC_MAX; ++m) emit[m] = 0xFFFFFFFFu;
     uint32_t ne = 0, perr = 0, used = 0;
-    bool done = !gvalid || p >= up_to, paused = false, exhausted = gvalid && p >= up_to;
+    bool done = !gvalid || p >= up_to || read_irrelevant(S, ylen), paused = false,
+         exhausted = gvalid && p >= up_to;
     while (wv_any(!done)) {
         // ---- every lane scans its window (no wave ops in here)
         const uint64_t pw = p + (uint64_t)wl;
@@ -339,6 +356,7 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
                 for (uint32_t m = 0; m < nm; ++m) skip |= S.memo[k * MEMO + m] == sid;
                 for (uint32_t m = 0; m < nl; ++m) skip |= lst[m].x == sid;
                 if (skip) continue;                       // NW(sid, r) rejected, pending or listed (Q18)
+                if (hit_irrelevant(S, S.db_start[sid + 1] - S.db_start[sid], ylen)) continue;
                 ++ev;
                 const int64_t xs = (int64_t)S.db_start[sid];
                 const int64_t xe = (sid == S.n_db - 1) ? (int64_t)S.db_len : (int64_t)S.db_start[sid + 1] - 1;

@@ -112,6 +112,8 @@ typedef struct imsame_stats {
     double   launch_ms[IMSAME_LAUNCH_STATS];
     uint64_t n_rewalk;      /* accepted reads whose path overflowed the device
                                arena and was re-walked (want_paths)      */
+    double   ms_setup;      /* host: tables, buffers, until the first kernel */
+    double   ms_d2h;        /* results (64 B per read) device -> host        */
 } imsame_stats;
 
 typedef struct imsame_ctx imsame_ctx;

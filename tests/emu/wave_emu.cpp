@@ -205,7 +205,7 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
         S.minraw = mr.data(); S.n_minraw = ymax + 1;
         S.minlen = ml.data(); S.n_minlen = ymax + 1;
         S.minident = mi.data(); S.n_minident = xcap + ymax + 2;
-        S.max_rs = p->max_read_size; S.short_ylen = short_y;
+        S.max_rs = p->max_read_size; S.short_ylen = short_y; S.max_rec = max_rec;
         S.spec = (st.rounds == 1) ? 1u : std::max<uint32_t>(1u, std::min<uint32_t>(spec_later, n / nact));
         S.budget = seed_budget(budget1, (uint32_t)st.rounds);
         S.next = nxt.data(); S.nnext = &nc[2];

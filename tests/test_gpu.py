@@ -540,3 +540,26 @@ def test_cli_multi_device_output_identical(tmp_path):
         outs.append(open(o, "rb").read())
     assert outs[0] == outs[1] == outs[2]
     assert outs[0].count(b" $$$$$$$ \n") > 10_000
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("rec_bp,cap", [(2_000, 10_001), (12_001, 12_001)], ids=["c5_2kbp", "c5w_12kbp"])
+def test_c5_full_50mbp_database(dev, oracle_memo, rec_bp, cap):
+    """BASELINE configs[4] at its real database size (50 Mbp, so the e-value
+    tables use C5's L_DB): 6 ONT-like 10 kbp reads vs 2 kbp records (every
+    read rejected a priori: no record can hold the identities a 10 kbp read
+    needs, seed_kernel.hip:read_irrelevant) and vs 12 kbp records (the
+    long-read NW runs, 120M cells per candidate) -- every field equal to the
+    oracle's, which runs the reference's full scan and NWs."""
+    ref, rst = synth.make_reference_arr(50_004_000 if rec_bp > 10_000 else 50_000_000, rec_bp, seed=42)
+    q, qs = synth.make_long_reads_arr(ref, 6, 10_000, seed=48)
+    dev.index(ref, rst)
+    dev.set_query(q, qs)
+    res, _, st = dev.align(n_threads=3, params=dev.params(max_read_size=cap))
+    rc, exp, _ = oracle_memo.align(ref, rst, q, qs, oracle_memo.params(max_read_size=cap), 3)
+    assert rc == 0
+    assert not _cmp(res, exp), _cmp(res, exp)
+    if rec_bp > 10_000:
+        assert st.n_nw > 0 and (res["status"] == 1).sum() >= 3
+    else:
+        assert st.n_nw == 0 and st.n_hits == 0 and (res["status"] == 1).sum() == 0
