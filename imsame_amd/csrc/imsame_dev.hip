@@ -182,7 +182,7 @@ struct DBuf {
         if (n <= cap) return 0;
         if (p) (void)hipFree(p);
         p = nullptr; cap = 0;
-        size_t want = n + n / 8 + 4096;
+        size_t want = n + std::min<size_t>(n / 8, (size_t)1 << 30) + 4096;   // slack for regrowth, <= 1 GB
         if (hipMalloc(&p, want) != hipSuccess) { p = nullptr; return IMSAME_E_OOM; }
         cap = want;
         return 0;
@@ -501,29 +501,35 @@ static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, 
     const uint64_t waves_needed = (ncand + cpw - 1) / cpw;
     pl->blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)c->ncu * per_cu, (waves_needed + wpb - 1) / wpb));
     // Traceback arena: one slot per resident wave.  Long reads against long
-    // records (C5, 10 kbp x 12 kbp = 60 MB per slot) would ask for more than
+    // records (C5w, 10 kbp x 12 kbp = 99 MB per slot) would ask for more than
     // the card holds at full residency; the kernel pulls candidates from a
-    // queue, so fewer blocks finish the same work.  Budget: half of what is
-    // free (counting the arena already held), at most 64 GB.
+    // queue, so fewer blocks finish the same work.  Budget: what is free
+    // (counting the arena already held) less 8 GB of headroom -- the 288 GB
+    // of HBM are there to keep waves resident.
     const uint64_t per_block = (uint64_t)wpb * (pl->tb_dw * 4 + 3ull * pl->xcap * 4);
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = 0;
     const uint64_t held = c->tb.cap + c->bnd.cap;
-    const uint64_t budget = std::min<uint64_t>(64ull << 30, (fr + held) / 2);
+    const uint64_t avail = fr + held, headroom = 8ull << 30;
+    const uint64_t budget = avail > 2 * headroom ? avail - headroom : avail / 2;
     const uint64_t fit = budget / per_block;
     if (fit < 1) return IMSAME_E_OOM;
     if (pl->blocks > fit) pl->blocks = (unsigned)fit;
     return 0;
 }
 
-static int launch_nw(imsame_ctx *c, const NwPlan &pl, const uint32_t *cread, const uint32_t *csid, uint32_t n,
+static int launch_nw(imsame_ctx *c, NwPlan pl, const uint32_t *cread, const uint32_t *csid, uint32_t n,
                      imsame_read_result *outp, int64_t ig, int64_t eg, const imsame_params *p, uint32_t ymax,
                      uint32_t xmax, uint32_t *work, const uint8_t *dbp, const uint64_t *dbs, const uint8_t *qp,
                      const uint64_t *qs, uint32_t paths_cap, double *ms) {
     hipStream_t s = c->stream;
-    const unsigned slots = pl.blocks * 4;
     const uint64_t tb_dw = pl.tb_dw;
-    if (c->tb.ensure(slots * tb_dw * 4) || c->bnd.ensure((uint64_t)slots * 3 * pl.xcap * 4 + 64)) return IMSAME_E_OOM;
+    // fewer resident waves if the arena cannot be had (the queue still drains)
+    while (c->tb.ensure((uint64_t)pl.blocks * 4 * tb_dw * 4) ||
+           c->bnd.ensure((uint64_t)pl.blocks * 4 * 3 * pl.xcap * 4 + 64)) {
+        if (pl.blocks == 1) return IMSAME_E_OOM;
+        pl.blocks = (pl.blocks + 1) / 2;
+    }
     NwLaunch P;
     memset(&P, 0, sizeof P);
     P.db = dbp; P.db_start = dbs; P.q = qp; P.q_start = qs;
