@@ -216,8 +216,12 @@ struct imsame_ctx {
     DBuf cread, csid, cread2, csid2, cout, cout2;
     // scalars (one block of u64 counters)
     DBuf ctr;
-    // tables
+    // tables (and the inputs they were built for)
     DBuf minraw, minlen, minident;
+    bool tab_valid = false;
+    long double tab_min_e = 0, tab_cov = 0, tab_id = 0;
+    uint64_t tab_L = 0;
+    uint32_t tab_ymax = 0, tab_xmax = 0;
     // NW scratch; the path arena of the last align (device, or host for the
     // sliced form) until imsame_dev_fetch_paths
     DBuf tb, bnd, paths;
@@ -464,6 +468,13 @@ extern "C" void imsame_host_free(void *p) {
 }
 
 static int build_tables(imsame_ctx *c, const imsame_params *p, uint32_t ymax, uint32_t xmax) {
+    // the tables depend on the thresholds, L_DB and the shape only: reuse
+    // them across calls (ymax = 10,000 takes ~0.1 s of x87 expl / divisions)
+    const uint64_t L = c->ev_db_len ? c->ev_db_len : c->db_len;
+    if (c->tab_valid && c->tab_min_e == p->min_e && c->tab_cov == p->min_coverage && c->tab_id == p->min_identity &&
+        c->tab_L == L && c->tab_ymax == ymax && c->tab_xmax == xmax)
+        return 0;
+    c->tab_valid = false;
     std::vector<uint64_t> mr;
     std::vector<uint32_t> ml, mi;
     imsame_build_tables(p, c->ev_db_len ? c->ev_db_len : c->db_len, ymax, xmax, mr, ml, mi);
@@ -473,10 +484,13 @@ static int build_tables(imsame_ctx *c, const imsame_params *p, uint32_t ymax, ui
     HIPCHK(hipMemcpyAsync(c->minlen.p, ml.data(), ml.size() * 4, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(c->minident.p, mi.data(), mi.size() * 4, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));   // host vectors die here
+    c->tab_valid = true;
+    c->tab_min_e = p->min_e; c->tab_cov = p->min_coverage; c->tab_id = p->min_identity;
+    c->tab_L = L; c->tab_ymax = ymax; c->tab_xmax = xmax;
     return 0;
 }
 
-struct NwPlan { int G, GPW, xcap, xstride, steps, nstr; bool pk, last4; size_t lds; unsigned blocks; uint64_t tb_dw; };
+struct NwPlan { int G, GPW, xcap, xstride, steps, nstr; bool pk, last4; size_t lds; unsigned blocks, max_blocks; uint64_t tb_dw; };
 
 // pk: the packed-pair int16 kernel (nw16_kernel.hip) when the launch fits it
 // ylen_mult: every read of the launch has a length that is a multiple of NW16_K
@@ -515,6 +529,11 @@ static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, 
     const uint64_t fit = budget / per_block;
     if (fit < 1) return IMSAME_E_OOM;
     if (pl->blocks > fit) pl->blocks = (unsigned)fit;
+    // the arena is sized for a full-residency launch of this shape, so the
+    // launches of later rounds (fewer or more candidates) reuse it instead of
+    // reallocating up to hundreds of GB each round
+    pl->max_blocks = (unsigned)std::min<uint64_t>((uint64_t)c->ncu * per_cu, fit);
+    if (pl->max_blocks < pl->blocks) pl->max_blocks = pl->blocks;
     return 0;
 }
 
@@ -525,8 +544,10 @@ static int launch_nw(imsame_ctx *c, NwPlan pl, const uint32_t *cread, const uint
     hipStream_t s = c->stream;
     const uint64_t tb_dw = pl.tb_dw;
     // fewer resident waves if the arena cannot be had (the queue still drains)
-    while (c->tb.ensure((uint64_t)pl.blocks * 4 * tb_dw * 4) ||
-           c->bnd.ensure((uint64_t)pl.blocks * 4 * 3 * pl.xcap * 4 + 64)) {
+    const uint64_t per_slot = tb_dw * 4, bnd_slot = 3ull * pl.xcap * 4;
+    if (c->tb.cap < (uint64_t)pl.blocks * 4 * per_slot)       // grow once to this shape's full residency
+        (void)c->tb.ensure((uint64_t)pl.max_blocks * 4 * per_slot);
+    while (c->tb.ensure((uint64_t)pl.blocks * 4 * per_slot) || c->bnd.ensure((uint64_t)pl.blocks * 4 * bnd_slot + 64)) {
         if (pl.blocks == 1) return IMSAME_E_OOM;
         pl.blocks = (pl.blocks + 1) / 2;
     }
