@@ -29,6 +29,8 @@ for s in $STEPS; do
            > gpurun_out/bench_${s}_${TAG}.json 2> gpurun_out/bench_${s}_${TAG}.err; ok_or_stop $? $s ;;
     bud*) B=${s#bud}; IMSAME_SEED_BUDGET=$B timeout -k 10 600 python -u bench.py --cpu-sample 0 --e2e off \
            > gpurun_out/bench_${s}_${TAG}.json 2> gpurun_out/bench_${s}_${TAG}.err; ok_or_stop $? $s ;;
+    c3) timeout -k 10 600 python -u bench.py --config c3 --steps 2 --cpu-sample 0 --e2e off > gpurun_out/bench_c3_${TAG}.json \
+           2> gpurun_out/bench_c3_${TAG}.err; ok_or_stop $? c3 ;;
     c5) timeout -k 10 600 python -u bench.py --config c5 --steps 1 --warmup 0 > gpurun_out/bench_c5_${TAG}.json \
            2> gpurun_out/bench_c5_${TAG}.err; ok_or_stop $? c5 ;;
     c5wprof) timeout -k 10 900 rocprofv3 --kernel-trace --stats -T -d gpurun_out/prof_c5w_${TAG} -o kt --output-format csv \
