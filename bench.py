@@ -100,6 +100,12 @@ def parse():
     ap.add_argument("--e2e", choices=("auto", "on", "off"), default="auto",
                     help="end-to-end imsame CLI run (parse, index, align, render, write) after the timed steps "
                          "(auto: on for c2 at N=1)")
+    ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
+                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo: rehearsal on one card)")
+    ap.add_argument("--device", type=int, default=None,
+                    help="HIP device of this rank (default LOCAL_RANK; a fixed value rehearses N ranks on one card)")
+    ap.add_argument("--shard", default=None, metavar="R/N",
+                    help="diagnostic: on one GPU, time only rank R's shard of an N-GPU strong-scaling run")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "nw_traffic.json"))
     ap.add_argument("--valu-json", default=os.path.join(REPO, "profiles", "nw_valu.json"))
     a = ap.parse_args()
@@ -144,11 +150,15 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    gpu = local if a.device is None else a.device
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.dist_backend == "nccl":
+            torch.cuda.set_device(gpu)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group("gloo")
     import imsame_amd
     from imsame_amd.dist import shard_range
     from tests import synth
@@ -162,7 +172,10 @@ def main():
     strong = a.scaling == "strong"
     q, qs = gen(ref, a.reads, a.read_len, seed=cfg["seeds"][1] + (0 if strong else 1000 * rank))
     lo, hi = shard_range(a.reads, rank, world) if strong else (0, a.reads)
-    dev = imsame_amd.Device(local)
+    if a.shard and world == 1:                        # one rank's work of an N-GPU run, on one GPU
+        sr, sn = (int(x) for x in a.shard.split("/"))
+        lo, hi = shard_range(a.reads, sr, sn)
+    dev = imsame_amd.Device(gpu)
     t0 = time.time()
     dev.index(ref, rst)
     t_index = time.time() - t0
@@ -210,6 +223,8 @@ def main():
     else:
         accepted_all = accepted
     total_reads = (a.reads if strong else world * a.reads) * a.steps
+    if a.shard and world == 1:
+        total_reads = (hi - lo) * a.steps             # the shard's own rate (diagnostic line)
     value = total_reads / elapsed
 
     # dominant kernel: the NW launches.  Algorithmic bytes per NW candidate
@@ -267,7 +282,9 @@ def main():
                           if a.slice_bases else ""),
                        "reads": a.reads, "reads_per_gpu": hi - lo, "read_len": a.read_len, "ref_bp": a.ref_bp,
                        "record_bp": a.record_bp, "n_threads_semantic": a.n_threads,
-                       "parallelism": f"dp{world} (read shards, replicated index)"},
+                       "parallelism": f"dp{world} (read shards, replicated index)"
+                       + ("" if world == 1 or a.dist_backend == "nccl" else
+                          f"; REHEARSAL: {a.dist_backend} collectives, device {gpu} shared by all ranks")},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "e2e": e2e,

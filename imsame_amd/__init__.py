@@ -27,6 +27,7 @@ LIB_DEV = os.environ.get("IMSAME_LIB_DEV") or os.path.join(HERE, "lib", "libimsa
 LIB_HOST = os.path.join(HERE, "lib", "libimsame_host.so")
 CLI = os.path.join(HERE, "bin", "imsame")
 FLAG_NW32 = 1          # imsame_params.flags: force the int32 NW kernel (include/imsame_dev.h)
+FLAG_NW16 = 2          # ... or the packed int16 kernel for every launch it fits, however small
 
 _lib = None
 _host = None

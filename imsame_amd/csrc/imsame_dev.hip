@@ -495,9 +495,17 @@ struct NwPlan { int G, GPW, xcap, xstride, steps, nstr; bool pk, last4; size_t l
 // pk: the packed-pair int16 kernel (nw16_kernel.hip) when the launch fits it
 // ylen_mult: every read of the launch has a length that is a multiple of NW16_K
 static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, const imsame_params *p,
-                   bool ylen_mult, NwPlan *pl) {
+                   bool ylen_mult, NwPlan *pl, bool rounds = true) {
     const int wpb = 4;
-    pl->pk = !(p->flags & IMSAME_FLAG_NW32) && nw16_fits(p->igap, p->egap, xcap, ymax);
+    // Small launches (the last rounds; every round of a small shard) are
+    // latency-bound: one packed task is 8 candidates x all rows with 10
+    // columns per lane (~1.1 ms alone on a SIMD), while the int32 kernel puts
+    // 5 columns on a lane (about a third of the per-row issue) and 2
+    // candidates in a wave.  Results are identical (tests run both kernels).
+    // (IMSAME_FLAG_NW16 and the unit-level nw_pairs keep the packed kernel.)
+    const char *se = getenv("IMSAME_NW_SMALL");
+    const uint32_t small = (p->flags & IMSAME_FLAG_NW16) || !rounds ? 0u : se ? (uint32_t)atoi(se) : 3000u;
+    pl->pk = !(p->flags & IMSAME_FLAG_NW32) && ncand >= small && nw16_fits(p->igap, p->egap, xcap, ymax);
     pl->last4 = pl->pk && ylen_mult;
     const NwShape sh = pl->pk ? nw16_shape(ymax, xcap) : nw_shape(ymax, xcap);
     pl->G = sh.G; pl->GPW = sh.GPW; pl->nstr = sh.nstr; pl->xcap = sh.xcap; pl->xstride = sh.xstride;
@@ -1096,7 +1104,7 @@ extern "C" int imsame_dev_nw_pairs(imsame_ctx *c, const uint8_t *xs, const uint6
     NwPlan pl;
     bool ymult = true;
     for (uint64_t k = 0; k < npairs; ++k) ymult = ymult && (y_start[k + 1] - y_start[k]) % NW16_K == 0;
-    if ((rc = plan_nw(c, ymax, xmax, (uint32_t)npairs, p, ymult, &pl))) return rc;
+    if ((rc = plan_nw(c, ymax, xmax, (uint32_t)npairs, p, ymult, &pl, false))) return rc;
     double ms = 0;
     rc = launch_nw(c, pl, dc.as<uint32_t>(), dc.as<uint32_t>(), (uint32_t)npairs, dout.as<imsame_read_result>(),
                    p->igap, p->egap, p, ymax, xmax, (uint32_t *)(ctr + C_WORK), dx.as<uint8_t>(), dxs.as<uint64_t>(),

@@ -58,9 +58,12 @@ typedef struct imsame_params {
     uint32_t    flags;          /* IMSAME_FLAG_* (0 = defaults)                 */
 } imsame_params;
 
-/* flags: force the int32 NW kernel even where the packed int16 one fits
- * (results are identical; used by the tests to cover both kernels) */
+/* flags: force the int32 NW kernel even where the packed int16 one fits,
+ * or the packed kernel for every launch it fits however few candidates it
+ * has (by default launches of < 3000 candidates take the int32 kernel: lower
+ * latency).  Results are identical; the tests use both to cover both kernels. */
 #define IMSAME_FLAG_NW32 1u
+#define IMSAME_FLAG_NW16 2u
 
 /* Fill the reference defaults: min_e = 1/powl(10,20), cov = id = 0.5,
  * igap = -5, egap = -2, max_read_size = 3000, want_paths = 0. */

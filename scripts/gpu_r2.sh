@@ -31,6 +31,11 @@ for s in $STEPS; do
            > gpurun_out/bench_${s}_${TAG}.json 2> gpurun_out/bench_${s}_${TAG}.err; ok_or_stop $? $s ;;
     c3) timeout -k 10 600 python -u bench.py --config c3 --steps 2 --cpu-sample 0 --e2e off > gpurun_out/bench_c3_${TAG}.json \
            2> gpurun_out/bench_c3_${TAG}.err; ok_or_stop $? c3 ;;
+    shard*) SH=${s#shard}; timeout -k 10 600 python -u bench.py --cpu-sample 0 --e2e off --shard ${SH/_//} --steps 5 \
+           > gpurun_out/bench_${s}_${TAG}.json 2> gpurun_out/bench_${s}_${TAG}.err; ok_or_stop $? $s ;;
+    ranks2) timeout -k 10 600 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+             --master-port 29517 bench.py --gpus 2 --dist-backend gloo --device 0 --cpu-sample 0 --e2e off \
+             > gpurun_out/bench_ranks2_${TAG}.json 2> gpurun_out/bench_ranks2_${TAG}.err; ok_or_stop $? ranks2 ;;
     c5) timeout -k 10 600 python -u bench.py --config c5 --steps 1 --warmup 0 > gpurun_out/bench_c5_${TAG}.json \
            2> gpurun_out/bench_c5_${TAG}.err; ok_or_stop $? c5 ;;
     c5wprof) timeout -k 10 900 rocprofv3 --kernel-trace --stats -T -d gpurun_out/prof_c5w_${TAG} -o kt --output-format csv \

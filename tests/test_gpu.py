@@ -9,7 +9,7 @@ import tempfile
 import numpy as np
 import pytest
 
-from imsame_amd import Device, render, fasta, CLI, PARITY_FIELDS, FLAG_NW32
+from imsame_amd import Device, render, fasta, CLI, PARITY_FIELDS, FLAG_NW32, FLAG_NW16
 from imsame_amd import abi
 from tests import golden_io as G
 from tests import synth
@@ -115,14 +115,17 @@ def test_align_matches_oracle_e2e(dev, oracle, name):
     dev.index(db, dbs, brk)
     dev.set_query(q, qs)
     for T in [int(t) for t in case["meta"]["runs"]]:
-        p = _params_for(dev, case)
-        res, _, st = dev.align(n_threads=T, params=p, allow_too_long=True)
         po = _params_for(oracle, case)        # exact long double defaults on both sides
         rc, ref, er = oracle.align(db, dbs, q, qs, po, T, brk)
         lim = er if rc else None
-        assert not _cmp(res, ref, lim), _cmp(res, ref, lim)
-        if rc:
-            assert st.err_read == er
+        # default (small launches take the int32 kernel) and packed kernel forced
+        for flags in (0, FLAG_NW16):
+            p = _params_for(dev, case)
+            p.flags = flags
+            res, _, st = dev.align(n_threads=T, params=p, allow_too_long=True)
+            assert not _cmp(res, ref, lim), (flags, _cmp(res, ref, lim))
+            if rc:
+                assert st.err_read == er
 
 
 @pytest.mark.parametrize("name", G.e2e_cases())
@@ -174,9 +177,12 @@ def test_synthetic_c2_shape_vs_oracle_all_T(dev, oracle):
         finally:
             del os.environ["IMSAME_SEED_BUDGET"], os.environ["IMSAME_SEED_L"]
         assert not _cmp(resb, res), (b, lanes, _cmp(resb, res))
-    # the int32 kernel gives the same results as the packed-pair one
+    # the int32 kernel gives the same results as the packed-pair one, which
+    # every launch uses when forced (by default launches < 3000 take int32)
     res32, _, _ = dev.align(n_threads=16, params=dev.params(flags=FLAG_NW32))
     assert not _cmp(res32, res), _cmp(res32, res)
+    res16, _, _ = dev.align(n_threads=16, params=dev.params(flags=FLAG_NW16))
+    assert not _cmp(res16, res), _cmp(res16, res)
     # shards with the global chunk-head semantics equal the full run
     full, _, _ = dev.align(n_threads=8)
     parts = [dev.align(a, b, n_threads=8)[0] for a, b in ((0, 3001), (3001, 7777), (7777, 12_000))]
