@@ -230,13 +230,19 @@ def main():
     # dominant kernel: the NW launches.  Algorithmic bytes per NW candidate
     # (SURVEY 8(d)): record + read + 2 B/cell traceback floor; HIP events on
     # the library's own stream bracket every NW launch.
-    nw_ms = sum(s["ms_nw"] for s in stats)
+    nw_ms = sum(s["ms_nw"] for s in stats)                 # summed per-launch HIP-event durations
+    nw_busy = sum(s["ms_nw_busy"] for s in stats)          # union of the launch intervals (lanes overlap)
     nw_launches = sum(s["nw_launches"] for s in stats)
     cells = sum(s["nw_cells"] for s in stats)
     n_nw = sum(s["n_nw"] for s in stats)
     seq_bytes = n_nw * (a.record_bp + a.read_len)
     alg_bytes = 2 * cells + seq_bytes
-    achieved = alg_bytes / (nw_ms / 1e3) / 1e9 if nw_ms else 0.0
+    # achieved: algorithmic bytes / the time the device ran NW launches.  With
+    # two lanes, launches of the two halves overlap: the per-launch average
+    # (avg_launch_ms, what rocprofv3 --stats reports) times the launches
+    # exceeds that time by launch_overlap (scripts/nw_busy.py recomputes the
+    # union from the kernel trace)
+    achieved = alg_bytes / (nw_busy / 1e3) / 1e9 if nw_busy else 0.0
     kernel = nw_kernel_name(a.read_len, a.record_bp) if not stats[-1]["nw_launches"] or a.read_len <= 160 \
         else "nw_kernel"
     per_launch = alg_bytes / max(nw_launches, 1)
@@ -248,12 +254,14 @@ def main():
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-    cells_per_s = cells / (nw_ms / 1e3) if nw_ms else 0.0
+    cells_per_s = cells / (nw_busy / 1e3) if nw_busy else 0.0
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "traffic_over_alg": round(traffic / per_launch, 4) if traffic and per_launch else None,
                 "kernel": kernel, "launches": nw_launches,
                 "avg_launch_ms": round(nw_ms / max(nw_launches, 1), 4),
+                "nw_busy_ms_per_step": round(nw_busy / a.steps, 3),
+                "launch_overlap": round(nw_ms / nw_busy, 3) if nw_busy else None,
                 "alg_bytes_per_launch": int(per_launch),
                 "cells_per_s": round(cells_per_s, 1),
                 "valu": valu_roofline(a.valu_json, kernel, a.config, cells_per_s)}
@@ -293,7 +301,9 @@ def main():
                        "hits_per_read": round(last["n_hits"] / max(hi - lo, 1), 2),
                        "ms_h2d_query": round(1e3 * sum(h2d) / max(len(h2d), 1), 3),
                        "nw_cells": last["nw_cells"], "n_nw": last["n_nw"],
+                       "lanes": last["lanes"],
                        "ms_seed": round(last["ms_seed"], 3), "ms_nw": round(last["ms_nw"], 3),
+                       "ms_nw_busy": round(last["ms_nw_busy"], 3),
                        "ms_align_call": round(last["ms_total"], 3),
                        "ms_host_setup": round(last["ms_setup"], 3), "ms_d2h_results": round(last["ms_d2h"], 3),
                        "nw_launch_cand": last["launch_cand"],

@@ -20,6 +20,7 @@
 #include <time.h>
 #include <vector>
 #include <algorithm>
+#include <thread>
 #include "../../include/imsame_dev.h"
 
 #include "tables.h"
@@ -208,6 +209,7 @@ struct imsame_ctx {
     DBuf q, q_start;
     uint64_t n_q = 0, q_len = 0, q_lo = 0, q_hi = 0, q_base = 0, q_lo_first = 0;
     std::vector<uint64_t> h_q_start;  // starts of reads q_lo .. q_hi
+    const uint64_t *hq = nullptr;     // = h_q_start.data(), or the parent's for a lane
     bool have_query = false;
     bool q_len_mult = false;         // every read length is a multiple of NW16_K
     // per-read state
@@ -236,9 +238,18 @@ struct imsame_ctx {
     uint64_t ev_db_len = 0;          // 0: db_len
     bool use_wcap = false, use_wstart = false;
     DBuf wcap, wout, wstart;
+    // second LANE: a context sharing this one's index and query (aliased
+    // buffers), with its own stream and per-read state, so one call's two
+    // halves run concurrently (see imsame_dev_align)
+    imsame_ctx *sub = nullptr;
+    bool is_sub = false, paths_split = false;
+    uint64_t paths_n_sub = 0;
+    // NW launch intervals (ms since the call's origin event) for the busy time
+    hipEvent_t origin = nullptr;
+    std::vector<std::pair<float, float>> nw_iv;
 };
 
-static inline uint64_t hqs(const imsame_ctx *c, uint64_t r) { return c->h_q_start[r - c->q_lo]; }
+static inline uint64_t hqs(const imsame_ctx *c, uint64_t r) { return c->hq[r - c->q_lo]; }
 // biased views: valid for the uploaded reads (and QPAD bases before them)
 static inline const uint8_t *dev_q(const imsame_ctx *c) { return (const uint8_t *)((uintptr_t)c->q.p - c->q_base); }
 static inline const uint64_t *dev_qs(const imsame_ctx *c) {
@@ -301,8 +312,14 @@ extern "C" int imsame_dev_open(int device, imsame_ctx **out) {
     return IMSAME_OK;
 }
 
+static void lane_unalias(imsame_ctx *l) {
+    DBuf *al[] = {&l->db, &l->db_start, &l->off, &l->ent, &l->q, &l->q_start};
+    for (DBuf *b : al) { b->p = nullptr; b->cap = 0; }
+}
+
 extern "C" void imsame_dev_close(imsame_ctx *c) {
     if (!c) return;
+    if (c->sub) { lane_unalias(c->sub); imsame_dev_close(c->sub); c->sub = nullptr; }
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     DBuf *bufs[] = {&c->db, &c->db_start, &c->off, &c->ent, &c->brk, &c->codes, &c->fill, &c->big, &c->q,
@@ -313,8 +330,29 @@ extern "C" void imsame_dev_close(imsame_ctx *c) {
     for (DBuf *b : bufs) b->release();
     (void)hipEventDestroy(c->ev0);
     (void)hipEventDestroy(c->ev1);
+    if (c->origin && !c->is_sub) (void)hipEventDestroy(c->origin);     // a lane borrows its parent's
     (void)hipStreamDestroy(c->stream);
     delete c;
+}
+
+// The second lane of c, aliasing c's index and query (not owned).
+static int lane_sub(imsame_ctx *c, imsame_ctx **out) {
+    if (!c->sub) {
+        imsame_ctx *l = nullptr;
+        int rc = imsame_dev_open(c->device, &l);
+        if (rc) return rc;
+        l->is_sub = true;
+        c->sub = l;
+    }
+    imsame_ctx *l = c->sub;
+    l->db = c->db; l->db_start = c->db_start; l->off = c->off; l->ent = c->ent; l->q = c->q; l->q_start = c->q_start;
+    l->n_db = c->n_db; l->db_len = c->db_len; l->n_ent = c->n_ent; l->max_rec = c->max_rec;
+    l->have_index = c->have_index;
+    l->n_q = c->n_q; l->q_len = c->q_len; l->q_lo = c->q_lo; l->q_hi = c->q_hi; l->q_base = c->q_base;
+    l->q_lo_first = c->q_lo_first; l->hq = c->hq; l->have_query = c->have_query; l->q_len_mult = c->q_len_mult;
+    l->ev_db_len = 0; l->use_wcap = l->use_wstart = false;
+    *out = l;
+    return 0;
 }
 
 static unsigned nblk(uint64_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
@@ -435,6 +473,7 @@ extern "C" int imsame_dev_set_query_range(imsame_ctx *c, const uint8_t *q_seq, u
     c->n_q = n_q; c->q_len = q_len; c->q_lo = read_from; c->q_hi = read_to;
     c->h_q_start.resize(read_to - read_from + 1);
     for (uint64_t r = read_from; r <= read_to; ++r) c->h_q_start[r - read_from] = qs(r);
+    c->hq = c->h_q_start.data();
     // reads q_lo_first .. read_from-1 are empty (start where read_from starts)
     uint64_t f = read_from;
     while (f > 0 && qs(f - 1) == qs(read_from)) --f;
@@ -587,6 +626,12 @@ static int launch_nw(imsame_ctx *c, NwPlan pl, const uint32_t *cread, const uint
     float f = 0;
     HIPCHK(hipEventElapsedTime(&f, c->ev0, c->ev1));
     *ms = f;
+    if (c->origin) {                             // interval on the call's common clock
+        float a = 0, b = 0;
+        if (hipEventElapsedTime(&a, c->origin, c->ev0) == hipSuccess &&
+            hipEventElapsedTime(&b, c->origin, c->ev1) == hipSuccess)
+            c->nw_iv.push_back({a, b});
+    }
     return 0;
 }
 
@@ -672,14 +717,11 @@ static int rewalk_lost(imsame_ctx *c, const imsame_params *p, uint64_t read_from
     return 0;
 }
 
-extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64_t n_threads_semantic,
-                                const imsame_params *p, imsame_read_result *res, uint32_t *paths, uint64_t paths_cap,
-                                uint64_t *paths_used, imsame_stats *stats) {
+// one lane's alignment of reads [read_from, read_to) (arguments checked)
+static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64_t n_threads_semantic,
+                     const imsame_params *p, imsame_read_result *res, uint32_t *paths, uint64_t paths_cap,
+                     uint64_t *paths_used, imsame_stats *stats) {
     const double t_start = now_ms();
-    if (!c || !p || (!res && read_to > read_from)) return IMSAME_E_ARG;
-    if (!c->have_index || !c->have_query) return IMSAME_E_STATE;
-    if (read_from < c->q_lo || read_to > c->q_hi || read_from > read_to) return IMSAME_E_ARG;
-    if (p->want_paths && !paths && paths_cap) return IMSAME_E_ARG;
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     const uint32_t n = (uint32_t)(read_to - read_from);
@@ -687,6 +729,7 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
     memset(&st, 0, sizeof st);
     st.n_reads = n;
     st.err_read = ~0ull;
+    st.lanes = 1;
     if (paths_used) *paths_used = 0;
     c->paths_n = 0; c->paths_on_host = false;
     // shapes
@@ -861,18 +904,121 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
     return ret;
 }
 
+// total length of the union of [a, b) intervals
+static double union_ms(std::vector<std::pair<float, float>> v) {
+    std::sort(v.begin(), v.end());
+    double tot = 0, a = 0, b = -1;
+    for (const auto &x : v) {
+        if (x.first > b) { if (b > a) tot += b - a; a = x.first; b = x.second; }
+        else b = std::max<double>(b, x.second);
+    }
+    if (b > a) tot += b - a;
+    return tot;
+}
+
+// Reads per lane below which a call is not split (a lane must fill the chip)
+#define LANE_MIN 32768
+
+extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64_t n_threads_semantic,
+                                const imsame_params *p, imsame_read_result *res, uint32_t *paths, uint64_t paths_cap,
+                                uint64_t *paths_used, imsame_stats *stats) {
+    const double t_start = now_ms();
+    if (!c || !p || (!res && read_to > read_from)) return IMSAME_E_ARG;
+    if (!c->have_index || !c->have_query) return IMSAME_E_STATE;
+    if (read_from < c->q_lo || read_to > c->q_hi || read_from > read_to) return IMSAME_E_ARG;
+    if (p->want_paths && !paths && paths_cap) return IMSAME_E_ARG;
+    HIPCHK(hipSetDevice(c->device));
+    if (!c->origin) HIPCHK(hipEventCreate(&c->origin));
+    HIPCHK(hipEventRecord(c->origin, c->stream));          // common clock of both lanes' NW launches
+    c->nw_iv.clear();
+    c->paths_split = false;
+    const uint64_t n = read_to - read_from;
+    uint64_t ymax = 0;
+    for (uint64_t r = read_from; r < read_to; ++r) ymax = std::max<uint64_t>(ymax, hqs(c, r + 1) - hqs(c, r));
+    // Two LANES: the halves of the range run concurrently on two streams
+    // (this context and c->sub, which shares the index and the query), so
+    // one half's latency-bound phases -- seed scans, the last small NW
+    // launches, host round trips -- overlap the other half's VALU-bound NW
+    // sweep.  Per-read results do not depend on the split (reads are
+    // independent given the chunk heads).  Short reads only: a long-read
+    // lane's traceback arena takes most of HBM.
+    const char *le = getenv("IMSAME_LANES");
+    const bool split = (le ? atoi(le) : 2) >= 2 && !c->is_sub && !c->use_wcap && n >= 2ull * LANE_MIN &&
+                       ymax <= (uint64_t)NW_W / 2;
+    if (!split) {
+        const int rc = align_one(c, read_from, read_to, n_threads_semantic, p, res, paths, paths_cap, paths_used,
+                                 stats);
+        if (stats) stats->ms_nw_busy = union_ms(c->nw_iv);
+        return rc;
+    }
+    imsame_ctx *l = nullptr;
+    int rc = lane_sub(c, &l);
+    if (rc) return rc;
+    l->origin = c->origin;
+    l->nw_iv.clear();
+    const uint64_t mid = read_from + n / 2, n0 = mid - read_from;
+    imsame_stats s0, s1;
+    memset(&s0, 0, sizeof s0); memset(&s1, 0, sizeof s1);
+    uint64_t u0 = 0, u1 = 0;
+    int r1 = 0;
+    std::thread th([&] {
+        r1 = align_one(l, mid, read_to, n_threads_semantic, p, res + n0, nullptr, 0, &u1, &s1);
+    });
+    const int r0 = align_one(c, read_from, mid, n_threads_semantic, p, res, nullptr, 0, &u0, &s0);
+    th.join();
+    l->origin = nullptr;
+    for (int r : {r0, r1})
+        if (r && r != IMSAME_E_PATHS && r != IMSAME_E_READ_TOO_LONG) return r;
+    int ret = (r0 == IMSAME_E_READ_TOO_LONG || r1 == IMSAME_E_READ_TOO_LONG) ? IMSAME_E_READ_TOO_LONG : IMSAME_OK;
+    // one result set: lane 1's paths follow lane 0's
+    if (p->want_paths)
+        for (uint64_t k = n0; k < n; ++k)
+            if (res[k].status == 1 && res[k].path_len) res[k].path_off += (uint32_t)u0;
+    imsame_stats st = s0;
+    st.n_reads += s1.n_reads; st.n_accepted += s1.n_accepted; st.n_nw += s1.n_nw; st.nw_cells += s1.nw_cells;
+    st.n_hits += s1.n_hits; st.rounds = std::max(s0.rounds, s1.rounds);
+    if (s1.err_read < st.err_read) { st.err_read = s1.err_read; st.err_dbseq = s1.err_dbseq; }
+    st.ms_seed += s1.ms_seed; st.ms_nw += s1.ms_nw; st.nw_bytes += s1.nw_bytes; st.n_rewalk += s1.n_rewalk;
+    for (uint64_t k = 0; k < s1.nw_launches && st.nw_launches < IMSAME_LAUNCH_STATS; ++k) {
+        st.launch_cand[st.nw_launches] = s1.launch_cand[k]; st.launch_ms[st.nw_launches] = s1.launch_ms[k];
+        st.nw_launches++;
+    }
+    st.nw_launches = s0.nw_launches + s1.nw_launches;
+    st.nw_launch_ms = st.nw_launches ? st.ms_nw / st.nw_launches : 0;
+    st.ms_setup = std::max(s0.ms_setup, s1.ms_setup); st.ms_d2h = s0.ms_d2h + s1.ms_d2h;
+    std::vector<std::pair<float, float>> iv = c->nw_iv;
+    iv.insert(iv.end(), l->nw_iv.begin(), l->nw_iv.end());
+    st.ms_nw_busy = union_ms(iv);
+    st.lanes = 2;
+    const uint64_t used = u0 + u1;
+    c->paths_split = true; c->paths_n = u0; c->paths_n_sub = u1; c->paths_on_host = false;
+    if (paths_used) *paths_used = used;
+    if (p->want_paths && used) {
+        if (used > paths_cap || !paths) { if (ret == IMSAME_OK) ret = IMSAME_E_PATHS; }
+        else {
+            uint64_t got = 0;
+            if ((rc = imsame_dev_fetch_paths(c, paths, paths_cap, &got))) return rc;
+        }
+    }
+    st.ms_total = now_ms() - t_start;
+    if (stats) *stats = st;
+    return ret;
+}
+
 extern "C" int imsame_dev_fetch_paths(imsame_ctx *c, uint32_t *paths, uint64_t paths_cap, uint64_t *paths_used) {
     if (!c) return IMSAME_E_ARG;
-    if (paths_used) *paths_used = c->paths_n;
-    if (c->paths_n > paths_cap) return IMSAME_E_PATHS;
-    if (!c->paths_n) return IMSAME_OK;
+    const uint64_t n1 = c->paths_split ? c->paths_n_sub : 0, total = c->paths_n + n1;
+    if (paths_used) *paths_used = total;
+    if (total > paths_cap) return IMSAME_E_PATHS;
+    if (!total) return IMSAME_OK;
     if (!paths) return IMSAME_E_ARG;
     if (c->paths_on_host) {
         memcpy(paths, c->paths_host.data(), c->paths_n * 4);
         return IMSAME_OK;
     }
     HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipMemcpyAsync(paths, c->paths.p, c->paths_n * 4, hipMemcpyDeviceToHost, c->stream));
+    if (c->paths_n) HIPCHK(hipMemcpyAsync(paths, c->paths.p, c->paths_n * 4, hipMemcpyDeviceToHost, c->stream));
+    if (n1) HIPCHK(hipMemcpyAsync(paths + c->paths_n, c->sub->paths.p, n1 * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return IMSAME_OK;
 }

@@ -117,6 +117,9 @@ typedef struct imsame_stats {
                                arena and was re-walked (want_paths)      */
     double   ms_setup;      /* host: tables, buffers, until the first kernel */
     double   ms_d2h;        /* results (64 B per read) device -> host        */
+    double   ms_nw_busy;    /* wall time the device ran NW launches (union of
+                               the launch intervals of all lanes)        */
+    uint64_t lanes;         /* concurrent lanes the call ran (1 or 2)   */
 } imsame_stats;
 
 typedef struct imsame_ctx imsame_ctx;
@@ -175,7 +178,10 @@ int imsame_dev_set_query_range(imsame_ctx *ctx, const uint8_t *q_seq, uint64_t q
  * overflow it are re-walked for exactly the reads concerned, never the whole
  * call); if paths_cap is smaller than *paths_used the call returns
  * IMSAME_E_PATHS with res[] complete and the paths still on the device:
- * grow the host arena and call imsame_dev_fetch_paths. */
+ * grow the host arena and call imsame_dev_fetch_paths.
+ * A call over >= 65,536 short reads runs its two halves concurrently on two
+ * streams of the device (a second internal lane sharing the index and the
+ * query); results do not depend on it (IMSAME_LANES=1 turns it off). */
 int imsame_dev_align(imsame_ctx *ctx, uint64_t read_from, uint64_t read_to,
                      uint64_t n_threads_semantic, const imsame_params *prm,
                      imsame_read_result *res, uint32_t *paths, uint64_t paths_cap,

@@ -17,7 +17,7 @@ for s in $STEPS; do
     tests) timeout -k 10 1200 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
              > gpurun_out/pytest_gpu_${TAG}.log 2>&1; ok_or_stop $? tests ;;
     newtests) timeout -k 10 900 python -u -m pytest tests/test_gpu.py -m gpu -v --timeout 300 --timeout-method thread \
-             -k "query_shards or path_arena or cli_devices or multi_device or full_c2 or c3_" \
+             -k "query_shards or path_arena or cli_devices or multi_device or full_c2 or lanes or c2_shape or e2e" \
              > gpurun_out/pytest_new_${TAG}.log 2>&1; ok_or_stop $? newtests ;;
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_${TAG}.log 2>&1
            ok_or_stop $? smoke ;;
@@ -36,6 +36,8 @@ for s in $STEPS; do
     ranks2) timeout -k 10 600 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
              --master-port 29517 bench.py --gpus 2 --dist-backend gloo --device 0 --cpu-sample 0 --e2e off \
              > gpurun_out/bench_ranks2_${TAG}.json 2> gpurun_out/bench_ranks2_${TAG}.err; ok_or_stop $? ranks2 ;;
+    lanes1) IMSAME_LANES=1 timeout -k 10 600 python -u bench.py --cpu-sample 0 --e2e off \
+           > gpurun_out/bench_lanes1_${TAG}.json 2> gpurun_out/bench_lanes1_${TAG}.err; ok_or_stop $? lanes1 ;;
     c5) timeout -k 10 600 python -u bench.py --config c5 --steps 1 --warmup 0 > gpurun_out/bench_c5_${TAG}.json \
            2> gpurun_out/bench_c5_${TAG}.err; ok_or_stop $? c5 ;;
     c5wprof) timeout -k 10 900 rocprofv3 --kernel-trace --stats -T -d gpurun_out/prof_c5w_${TAG} -o kt --output-format csv \

@@ -235,10 +235,12 @@ def test_full_c2_reference_properties(dev, oracle):
     dev.index(ref, rst)
     dev.set_query(q, qs)
     res, paths, st = dev.align(n_threads=16, want_paths=True)
+    assert st.lanes == 2                      # both halves ran concurrently
     acc = res["status"] == 1
     assert acc.mean() > 0.85
-    # every accepted path re-renders to the device's own identity count
-    for k in np.flatnonzero(acc)[:2000]:
+    # every accepted path re-renders to the device's own identity count (both lanes)
+    ka = np.flatnonzero(acc)
+    for k in np.concatenate([ka[:1000], ka[ka >= len(qs) // 2][:1000]]):
         r = res[k]
         s = int(r["db_seq"])
         X = ref[int(rst[s]):int(rst[s + 1]) if s + 1 < len(rst) else len(ref)]
@@ -569,3 +571,28 @@ def test_c5_full_50mbp_database(dev, oracle_memo, rec_bp, cap):
         assert st.n_nw > 0 and (res["status"] == 1).sum() >= 3
     else:
         assert st.n_nw == 0 and st.n_hits == 0 and (res["status"] == 1).sum() == 0
+
+
+def test_lanes_equal_one_lane(dev, monkeypatch):
+    """Two concurrent lanes (the halves of a call on two streams) against one
+    lane: identical per-read rows and identical .align text for every
+    accepted read (lane 1's paths follow lane 0's in the arena)."""
+    ref, rst = synth.make_reference_arr(4_000_000, 2_000, seed=61)
+    q, qs = synth.make_reads_arr(ref, 140_000, 150, seed=62, ins=0.003, dele=0.003)
+    dev.index(ref, rst)
+    dev.set_query(q, qs)
+    two, p2, s2 = dev.align(n_threads=7, want_paths=True, paths_cap=64)     # small host arena: fetch path
+    monkeypatch.setenv("IMSAME_LANES", "1")
+    one, p1, s1 = dev.align(n_threads=7, want_paths=True)
+    monkeypatch.delenv("IMSAME_LANES")
+    assert s2.lanes == 2 and s1.lanes == 1
+    assert not _cmp(two, one)
+    assert s2.n_nw == s1.n_nw and s2.n_accepted == s1.n_accepted and s2.ms_nw_busy > 0
+    for k in np.flatnonzero(two["status"] == 1)[::53]:
+        r2, r1 = two[k], one[k]
+        s = int(r2["db_seq"])
+        X = ref[int(rst[s]):int(rst[s]) + 2_000].tobytes()
+        Y = q[int(qs[k]):int(qs[k]) + 150].tobytes()
+        t2, _ = render(X, Y, r2, p2[r2["path_off"]:r2["path_off"] + r2["path_len"]])
+        t1, _ = render(X, Y, r1, p1[r1["path_off"]:r1["path_off"] + r1["path_len"]])
+        assert t2 == t1, k
