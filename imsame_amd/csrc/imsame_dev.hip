@@ -241,9 +241,9 @@ struct imsame_ctx {
     // second LANE: a context sharing this one's index and query (aliased
     // buffers), with its own stream and per-read state, so one call's two
     // halves run concurrently (see imsame_dev_align)
-    imsame_ctx *sub = nullptr;
+    std::vector<imsame_ctx *> subs;   // lanes 1, 2, ...
     bool is_sub = false, paths_split = false;
-    uint64_t paths_n_sub = 0;
+    std::vector<uint64_t> lane_paths; // path entries of lanes 1, 2, ... after a split call
     // NW launch intervals (ms since the call's origin event) for the busy time
     hipEvent_t origin = nullptr;
     std::vector<std::pair<float, float>> nw_iv;
@@ -319,7 +319,8 @@ static void lane_unalias(imsame_ctx *l) {
 
 extern "C" void imsame_dev_close(imsame_ctx *c) {
     if (!c) return;
-    if (c->sub) { lane_unalias(c->sub); imsame_dev_close(c->sub); c->sub = nullptr; }
+    for (imsame_ctx *l : c->subs) { lane_unalias(l); imsame_dev_close(l); }
+    c->subs.clear();
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     DBuf *bufs[] = {&c->db, &c->db_start, &c->off, &c->ent, &c->brk, &c->codes, &c->fill, &c->big, &c->q,
@@ -335,16 +336,16 @@ extern "C" void imsame_dev_close(imsame_ctx *c) {
     delete c;
 }
 
-// The second lane of c, aliasing c's index and query (not owned).
-static int lane_sub(imsame_ctx *c, imsame_ctx **out) {
-    if (!c->sub) {
+// Lane k >= 1 of c, aliasing c's index and query (not owned).
+static int lane_sub(imsame_ctx *c, int k, imsame_ctx **out) {
+    while ((int)c->subs.size() < k) {
         imsame_ctx *l = nullptr;
         int rc = imsame_dev_open(c->device, &l);
         if (rc) return rc;
         l->is_sub = true;
-        c->sub = l;
+        c->subs.push_back(l);
     }
-    imsame_ctx *l = c->sub;
+    imsame_ctx *l = c->subs[k - 1];
     l->db = c->db; l->db_start = c->db_start; l->off = c->off; l->ent = c->ent; l->q = c->q; l->q_start = c->q_start;
     l->n_db = c->n_db; l->db_len = c->db_len; l->n_ent = c->n_ent; l->max_rec = c->max_rec;
     l->have_index = c->have_index;
@@ -935,69 +936,89 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
     const uint64_t n = read_to - read_from;
     uint64_t ymax = 0;
     for (uint64_t r = read_from; r < read_to; ++r) ymax = std::max<uint64_t>(ymax, hqs(c, r + 1) - hqs(c, r));
-    // Two LANES: the halves of the range run concurrently on two streams
-    // (this context and c->sub, which shares the index and the query), so
-    // one half's latency-bound phases -- seed scans, the last small NW
-    // launches, host round trips -- overlap the other half's VALU-bound NW
-    // sweep.  Per-read results do not depend on the split (reads are
+    // LANES: the range is cut into `nl` parts that run concurrently on nl
+    // streams (this context and c->subs, which share the index and the
+    // query), so one part's latency-bound phases -- seed scans, the last
+    // small NW launches, host round trips -- overlap the others' VALU-bound
+    // NW sweeps.  Per-read results do not depend on the cut (reads are
     // independent given the chunk heads).  Short reads only: a long-read
     // lane's traceback arena takes most of HBM.
     const char *le = getenv("IMSAME_LANES");
-    const bool split = (le ? atoi(le) : 2) >= 2 && !c->is_sub && !c->use_wcap && n >= 2ull * LANE_MIN &&
-                       ymax <= (uint64_t)NW_W / 2;
-    if (!split) {
+    int nl = le ? std::max(1, std::min(8, atoi(le))) : 2;
+    while (nl > 1 && n < (uint64_t)nl * LANE_MIN) --nl;
+    if (c->is_sub || c->use_wcap || ymax > (uint64_t)NW_W / 2) nl = 1;
+    if (nl == 1) {
         const int rc = align_one(c, read_from, read_to, n_threads_semantic, p, res, paths, paths_cap, paths_used,
                                  stats);
         if (stats) stats->ms_nw_busy = union_ms(c->nw_iv);
         return rc;
     }
-    imsame_ctx *l = nullptr;
-    int rc = lane_sub(c, &l);
-    if (rc) return rc;
-    l->origin = c->origin;
-    l->nw_iv.clear();
-    const uint64_t mid = read_from + n / 2, n0 = mid - read_from;
-    imsame_stats s0, s1;
-    memset(&s0, 0, sizeof s0); memset(&s1, 0, sizeof s1);
-    uint64_t u0 = 0, u1 = 0;
-    int r1 = 0;
-    std::thread th([&] {
-        r1 = align_one(l, mid, read_to, n_threads_semantic, p, res + n0, nullptr, 0, &u1, &s1);
-    });
-    const int r0 = align_one(c, read_from, mid, n_threads_semantic, p, res, nullptr, 0, &u0, &s0);
-    th.join();
-    l->origin = nullptr;
-    for (int r : {r0, r1})
-        if (r && r != IMSAME_E_PATHS && r != IMSAME_E_READ_TOO_LONG) return r;
-    int ret = (r0 == IMSAME_E_READ_TOO_LONG || r1 == IMSAME_E_READ_TOO_LONG) ? IMSAME_E_READ_TOO_LONG : IMSAME_OK;
-    // one result set: lane 1's paths follow lane 0's
-    if (p->want_paths)
-        for (uint64_t k = n0; k < n; ++k)
-            if (res[k].status == 1 && res[k].path_len) res[k].path_off += (uint32_t)u0;
-    imsame_stats st = s0;
-    st.n_reads += s1.n_reads; st.n_accepted += s1.n_accepted; st.n_nw += s1.n_nw; st.nw_cells += s1.nw_cells;
-    st.n_hits += s1.n_hits; st.rounds = std::max(s0.rounds, s1.rounds);
-    if (s1.err_read < st.err_read) { st.err_read = s1.err_read; st.err_dbseq = s1.err_dbseq; }
-    st.ms_seed += s1.ms_seed; st.ms_nw += s1.ms_nw; st.nw_bytes += s1.nw_bytes; st.n_rewalk += s1.n_rewalk;
-    for (uint64_t k = 0; k < s1.nw_launches && st.nw_launches < IMSAME_LAUNCH_STATS; ++k) {
-        st.launch_cand[st.nw_launches] = s1.launch_cand[k]; st.launch_ms[st.nw_launches] = s1.launch_ms[k];
-        st.nw_launches++;
+    std::vector<imsame_ctx *> L(nl, c);
+    for (int k = 1; k < nl; ++k) {
+        int rc = lane_sub(c, k, &L[k]);
+        if (rc) return rc;
+        L[k]->origin = c->origin;
+        L[k]->nw_iv.clear();
     }
-    st.nw_launches = s0.nw_launches + s1.nw_launches;
-    st.nw_launch_ms = st.nw_launches ? st.ms_nw / st.nw_launches : 0;
-    st.ms_setup = std::max(s0.ms_setup, s1.ms_setup); st.ms_d2h = s0.ms_d2h + s1.ms_d2h;
+    std::vector<uint64_t> cut(nl + 1), used(nl, 0);
+    for (int k = 0; k <= nl; ++k) cut[k] = read_from + n * (uint64_t)k / (uint64_t)nl;
+    std::vector<imsame_stats> S(nl);
+    std::vector<int> R(nl, 0);
+    std::vector<std::thread> th;
+    for (int k = 1; k < nl; ++k)
+        th.emplace_back([&, k] {
+            R[k] = align_one(L[k], cut[k], cut[k + 1], n_threads_semantic, p, res + (cut[k] - read_from), nullptr, 0,
+                             &used[k], &S[k]);
+        });
+    R[0] = align_one(c, cut[0], cut[1], n_threads_semantic, p, res, nullptr, 0, &used[0], &S[0]);
+    for (auto &t : th) t.join();
+    for (int k = 1; k < nl; ++k) L[k]->origin = nullptr;
+    for (int r : R)
+        if (r && r != IMSAME_E_PATHS && r != IMSAME_E_READ_TOO_LONG) return r;
+    int ret = IMSAME_OK;
+    for (int r : R)
+        if (r == IMSAME_E_READ_TOO_LONG) ret = IMSAME_E_READ_TOO_LONG;
+    // one result set: each lane's paths follow the previous lanes'
+    uint64_t base = 0;
+    for (int k = 0; k < nl; ++k) {
+        if (p->want_paths && k)
+            for (uint64_t r = cut[k]; r < cut[k + 1]; ++r) {
+                imsame_read_result &x = res[r - read_from];
+                if (x.status == 1 && x.path_len) x.path_off += (uint32_t)base;
+            }
+        base += used[k];
+    }
+    imsame_stats st = S[0];
     std::vector<std::pair<float, float>> iv = c->nw_iv;
-    iv.insert(iv.end(), l->nw_iv.begin(), l->nw_iv.end());
+    st.nw_launches = 0;
+    for (int k = 0; k < nl; ++k) {
+        const imsame_stats &x = S[k];
+        if (k) {
+            st.n_reads += x.n_reads; st.n_accepted += x.n_accepted; st.n_nw += x.n_nw; st.nw_cells += x.nw_cells;
+            st.n_hits += x.n_hits; st.rounds = std::max(st.rounds, x.rounds);
+            if (x.err_read < st.err_read) { st.err_read = x.err_read; st.err_dbseq = x.err_dbseq; }
+            st.ms_seed += x.ms_seed; st.ms_nw += x.ms_nw; st.nw_bytes += x.nw_bytes; st.n_rewalk += x.n_rewalk;
+            st.ms_setup = std::max(st.ms_setup, x.ms_setup); st.ms_d2h += x.ms_d2h;
+            iv.insert(iv.end(), L[k]->nw_iv.begin(), L[k]->nw_iv.end());
+        }
+        for (uint64_t j = 0; j < std::min<uint64_t>(x.nw_launches, IMSAME_LAUNCH_STATS); ++j) {
+            if (st.nw_launches + j >= IMSAME_LAUNCH_STATS) break;
+            st.launch_cand[st.nw_launches + j] = x.launch_cand[j]; st.launch_ms[st.nw_launches + j] = x.launch_ms[j];
+        }
+        st.nw_launches += x.nw_launches;
+    }
+    st.nw_launch_ms = st.nw_launches ? st.ms_nw / st.nw_launches : 0;
     st.ms_nw_busy = union_ms(iv);
-    st.lanes = 2;
-    const uint64_t used = u0 + u1;
-    c->paths_split = true; c->paths_n = u0; c->paths_n_sub = u1; c->paths_on_host = false;
-    if (paths_used) *paths_used = used;
-    if (p->want_paths && used) {
-        if (used > paths_cap || !paths) { if (ret == IMSAME_OK) ret = IMSAME_E_PATHS; }
+    st.lanes = (uint64_t)nl;
+    c->paths_split = true; c->paths_n = used[0]; c->paths_on_host = false;
+    c->lane_paths.assign(used.begin() + 1, used.end());
+    if (paths_used) *paths_used = base;
+    if (p->want_paths && base) {
+        if (base > paths_cap || !paths) { if (ret == IMSAME_OK) ret = IMSAME_E_PATHS; }
         else {
             uint64_t got = 0;
-            if ((rc = imsame_dev_fetch_paths(c, paths, paths_cap, &got))) return rc;
+            int rc = imsame_dev_fetch_paths(c, paths, paths_cap, &got);
+            if (rc) return rc;
         }
     }
     st.ms_total = now_ms() - t_start;
@@ -1007,7 +1028,9 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
 
 extern "C" int imsame_dev_fetch_paths(imsame_ctx *c, uint32_t *paths, uint64_t paths_cap, uint64_t *paths_used) {
     if (!c) return IMSAME_E_ARG;
-    const uint64_t n1 = c->paths_split ? c->paths_n_sub : 0, total = c->paths_n + n1;
+    uint64_t total = c->paths_n;
+    if (c->paths_split)
+        for (uint64_t u : c->lane_paths) total += u;
     if (paths_used) *paths_used = total;
     if (total > paths_cap) return IMSAME_E_PATHS;
     if (!total) return IMSAME_OK;
@@ -1018,7 +1041,13 @@ extern "C" int imsame_dev_fetch_paths(imsame_ctx *c, uint32_t *paths, uint64_t p
     }
     HIPCHK(hipSetDevice(c->device));
     if (c->paths_n) HIPCHK(hipMemcpyAsync(paths, c->paths.p, c->paths_n * 4, hipMemcpyDeviceToHost, c->stream));
-    if (n1) HIPCHK(hipMemcpyAsync(paths + c->paths_n, c->sub->paths.p, n1 * 4, hipMemcpyDeviceToHost, c->stream));
+    uint64_t off = c->paths_n;
+    if (c->paths_split)
+        for (size_t k = 0; k < c->lane_paths.size(); ++k) {
+            const uint64_t u = c->lane_paths[k];
+            if (u) HIPCHK(hipMemcpyAsync(paths + off, c->subs[k]->paths.p, u * 4, hipMemcpyDeviceToHost, c->stream));
+            off += u;
+        }
     HIPCHK(hipStreamSynchronize(c->stream));
     return IMSAME_OK;
 }

@@ -36,8 +36,9 @@ for s in $STEPS; do
     ranks2) timeout -k 10 600 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
              --master-port 29517 bench.py --gpus 2 --dist-backend gloo --device 0 --cpu-sample 0 --e2e off \
              > gpurun_out/bench_ranks2_${TAG}.json 2> gpurun_out/bench_ranks2_${TAG}.err; ok_or_stop $? ranks2 ;;
-    lanes1) IMSAME_LANES=1 timeout -k 10 600 python -u bench.py --cpu-sample 0 --e2e off \
-           > gpurun_out/bench_lanes1_${TAG}.json 2> gpurun_out/bench_lanes1_${TAG}.err; ok_or_stop $? lanes1 ;;
+    lanes*) LN=${s#lanes}; LN=${LN%%_*}; SH=${s#lanes${LN}}; SH=${SH#_}
+           IMSAME_LANES=$LN timeout -k 10 600 python -u bench.py --cpu-sample 0 --e2e off --steps 5 ${SH:+--shard ${SH/_//}} \
+           > gpurun_out/bench_${s}_${TAG}.json 2> gpurun_out/bench_${s}_${TAG}.err; ok_or_stop $? $s ;;
     c5) timeout -k 10 600 python -u bench.py --config c5 --steps 1 --warmup 0 > gpurun_out/bench_c5_${TAG}.json \
            2> gpurun_out/bench_c5_${TAG}.err; ok_or_stop $? c5 ;;
     c5wprof) timeout -k 10 900 rocprofv3 --kernel-trace --stats -T -d gpurun_out/prof_c5w_${TAG} -o kt --output-format csv \
