@@ -944,7 +944,9 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
     // independent given the chunk heads).  Short reads only: a long-read
     // lane's traceback arena takes most of HBM.
     const char *le = getenv("IMSAME_LANES");
-    int nl = le ? std::max(1, std::min(8, atoi(le))) : 2;
+    // default: 2 lanes, 4 from 1M reads on (profiles/r2h_*: 1M reads 6.81 /
+    // 6.86 / 6.91 M reads/s with 2 / 3 / 4 lanes; a 125k-read shard is best at 2)
+    int nl = le ? std::max(1, std::min(8, atoi(le))) : (n >= 1000000 ? 4 : 2);
     while (nl > 1 && n < (uint64_t)nl * LANE_MIN) --nl;
     if (c->is_sub || c->use_wcap || ymax > (uint64_t)NW_W / 2) nl = 1;
     if (nl == 1) {
