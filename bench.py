@@ -251,7 +251,10 @@ def main():
         try:
             tj = json.load(open(a.traffic_json))
             if tj.get("kernel") == kernel and tj.get("config", "c2") == a.config:   # PMC pass of THIS kernel
-                traffic = tj.get("hbm_bytes_per_launch")
+                # bytes per DP cell of the PMC pass x this run's cells per launch
+                # (launch sizes depend on the lane count; the per-cell rate does not)
+                bpc = tj.get("hbm_bytes_per_cell")
+                traffic = int(bpc * cells / max(nw_launches, 1)) if bpc else None
         except Exception:
             traffic = None
     cells_per_s = cells / (nw_busy / 1e3) if nw_busy else 0.0

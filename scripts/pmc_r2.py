@@ -70,9 +70,14 @@ def main():
     config = "c2" if cfg.get("ref_bp") == 50_000_000 and cfg.get("read_len") == 150 else "other"
     if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
         fetch2, write = 2 * v["FETCH_SIZE"] * 1024, v["WRITE_SIZE"] * 1024
+        cells = (bench or {}).get("detail", {}).get("nw_cells")
         with open(os.path.join(prof, "nw_traffic.json"), "w") as f:
             json.dump({"tag": tag, "kernel": kname, "config": config, "launches": n,
                        "hbm_bytes_per_launch": round((fetch2 + write) / n),
+                       # per DP cell: bench.py scales it by the cells of ITS launches
+                       # (launch sizes change with the lane count)
+                       "nw_cells": cells,
+                       "hbm_bytes_per_cell": round((fetch2 + write) / cells, 5) if cells else None,
                        "fetch_bytes_x2_per_launch": round(fetch2 / n), "write_bytes_per_launch": round(write / n),
                        "note": "one bench step (--steps 1 --warmup 0); FETCH_SIZE doubled per MI355X_MICROARCH.md "
                                "gfx950; KiB -> bytes"}, f, indent=1)
