@@ -304,7 +304,7 @@ def main():
                        "hits_per_read": round(last["n_hits"] / max(hi - lo, 1), 2),
                        "ms_h2d_query": round(1e3 * sum(h2d) / max(len(h2d), 1), 3),
                        "nw_cells": last["nw_cells"], "n_nw": last["n_nw"],
-                       "lanes": last["lanes"],
+                       "lanes": last["lanes"], "nw_redo_waves": last.get("nw_redo"),
                        "ms_seed": round(last["ms_seed"], 3), "ms_nw": round(last["ms_nw"], 3),
                        "ms_nw_busy": round(last["ms_nw_busy"], 3),
                        "ms_align_call": round(last["ms_total"], 3),

@@ -28,6 +28,7 @@ LIB_HOST = os.path.join(HERE, "lib", "libimsame_host.so")
 CLI = os.path.join(HERE, "bin", "imsame")
 FLAG_NW32 = 1          # imsame_params.flags: force the int32 NW kernel (include/imsame_dev.h)
 FLAG_NW16 = 2          # ... or the packed int16 kernel for every launch it fits, however small
+FLAG_NW16_ONEPASS = 4  # ... the packed kernel in one pass (default: score sweep + traceback band)
 
 _lib = None
 _host = None

@@ -74,7 +74,7 @@ class Stats(C.Structure):
         ("nw_launch_ms", C.c_double), ("nw_launches", C.c_uint64), ("nw_bytes", C.c_uint64),
         ("launch_cand", C.c_uint64 * LAUNCH_STATS), ("launch_ms", C.c_double * LAUNCH_STATS),
         ("n_rewalk", C.c_uint64), ("ms_setup", C.c_double), ("ms_d2h", C.c_double),
-        ("ms_nw_busy", C.c_double), ("lanes", C.c_uint64),
+        ("ms_nw_busy", C.c_double), ("lanes", C.c_uint64), ("nw_redo", C.c_uint64),
     ]
 
     def as_dict(self):

@@ -226,7 +226,7 @@ struct imsame_ctx {
     uint32_t tab_ymax = 0, tab_xmax = 0;
     // NW scratch; the path arena of the last align (device, or host for the
     // sliced form) until imsame_dev_fetch_paths
-    DBuf tb, bnd, paths;
+    DBuf tb, bnd, paths, ck;
     uint64_t paths_cap_dev = 0, paths_n = 0;
     double paths_hint = 0;     // path entries per read of the last call
     std::vector<uint32_t> paths_host;
@@ -260,7 +260,8 @@ static inline const uint64_t *dev_qs(const imsame_ctx *c) {
 #define QPAD 64
 
 // counters block layout (u64 slots)
-enum { C_NCAND = 0, C_NCAND2, C_NNEXT, C_WORK, C_WORK2, C_PATHS, C_FLAGS, C_ERR, C_HITS, C_CELLS, C_NACC, C_NSLOTS };
+enum { C_NCAND = 0, C_NCAND2, C_NNEXT, C_WORK, C_WORK2, C_PATHS, C_FLAGS, C_ERR, C_HITS, C_CELLS, C_NACC, C_REDO,
+       C_PROF, C_NSLOTS = C_PROF + 5 };
 
 static double now_ms() {
     struct timespec ts; clock_gettime(CLOCK_MONOTONIC, &ts);
@@ -326,7 +327,7 @@ extern "C" void imsame_dev_close(imsame_ctx *c) {
     DBuf *bufs[] = {&c->db, &c->db_start, &c->off, &c->ent, &c->brk, &c->codes, &c->fill, &c->big, &c->q,
                     &c->q_start, &c->res, &c->cur_p, &c->cur_h, &c->memo, &c->nmemo, &c->rstat, &c->act0,
                     &c->act1, &c->cread, &c->csid, &c->cread2, &c->csid2, &c->cout, &c->cout2, &c->ctr,
-                    &c->minraw, &c->minlen, &c->minident, &c->tb, &c->bnd, &c->paths, &c->rc_in, &c->rc_out,
+                    &c->minraw, &c->minlen, &c->minident, &c->tb, &c->bnd, &c->paths, &c->ck, &c->rc_in, &c->rc_out,
                     &c->rc_a, &c->rc_b, &c->rc_c, &c->cbase, &c->ccnt, &c->perr, &c->wcap, &c->wout, &c->wstart};
     for (DBuf *b : bufs) b->release();
     (void)hipEventDestroy(c->ev0);
@@ -530,7 +531,17 @@ static int build_tables(imsame_ctx *c, const imsame_params *p, uint32_t ymax, ui
     return 0;
 }
 
-struct NwPlan { int G, GPW, xcap, xstride, steps, nstr; bool pk, last4; size_t lds; unsigned blocks, max_blocks; uint64_t tb_dw; };
+struct NwPlan { int G, GPW, xcap, xstride, steps, nstr; bool pk, last4, two; size_t lds; unsigned blocks, max_blocks;
+                uint64_t tb_dw, ck_dw; int band_w; };
+
+// Rows above its best cell the second nw16 sweep keeps (nw16_kernel.hip).  A
+// path longer than that (rare: C2 paths span <= 209 rows) makes its wave redo
+// the sweep from row 1.  IMSAME_NW_BAND overrides (tests use tiny bands to
+// drive the redo path).
+static int nw16_band_rows() {
+    const char *e = getenv("IMSAME_NW_BAND");
+    return e ? std::max(0, atoi(e)) : 200;
+}
 
 // pk: the packed-pair int16 kernel (nw16_kernel.hip) when the launch fits it
 // ylen_mult: every read of the launch has a length that is a multiple of NW16_K
@@ -547,13 +558,18 @@ static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, 
     const uint32_t small = (p->flags & IMSAME_FLAG_NW16) || !rounds ? 0u : se ? (uint32_t)atoi(se) : 3000u;
     pl->pk = !(p->flags & IMSAME_FLAG_NW32) && ncand >= small && nw16_fits(p->igap, p->egap, xcap, ymax);
     pl->last4 = pl->pk && ylen_mult;
+    const char *op = getenv("IMSAME_NW_ONEPASS");
+    pl->two = pl->pk && !(p->flags & IMSAME_FLAG_NW16_ONEPASS) && !(op && atoi(op));
+    pl->band_w = nw16_band_rows();
     const NwShape sh = pl->pk ? nw16_shape(ymax, xcap) : nw_shape(ymax, xcap);
     pl->G = sh.G; pl->GPW = sh.GPW; pl->nstr = sh.nstr; pl->xcap = sh.xcap; pl->xstride = sh.xstride;
     pl->steps = sh.steps;
     pl->tb_dw = pl->pk ? nw16_tb_words(sh) : nw_tb_words(sh);
+    pl->ck_dw = pl->two ? nw16_ck_words(sh) : 0;
     pl->lds = (size_t)wpb * (pl->pk ? nw16_wave_lds(pl->GPW, pl->xstride) : nw_wave_lds(pl->GPW, pl->xstride));
     int per_cu = 0;
-    hipError_t oe = pl->pk ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw16_kernel<false>, wpb * 64, pl->lds)
+    hipError_t oe = pl->two ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw16_kernel<false, true>, wpb * 64, pl->lds)
+                  : pl->pk ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw16_kernel<false, false>, wpb * 64, pl->lds)
                   : (pl->nstr > 1)
                       ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw_kernel<true>, wpb * 64, pl->lds)
                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw_kernel<false>, wpb * 64, pl->lds);
@@ -568,10 +584,10 @@ static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, 
     // queue, so fewer blocks finish the same work.  Budget: what is free
     // (counting the arena already held) less 8 GB of headroom -- the 288 GB
     // of HBM are there to keep waves resident.
-    const uint64_t per_block = (uint64_t)wpb * (pl->tb_dw * 4 + 3ull * pl->xcap * 4);
+    const uint64_t per_block = (uint64_t)wpb * (pl->tb_dw * 4 + pl->ck_dw * 4 + 3ull * pl->xcap * 4);
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = 0;
-    const uint64_t held = c->tb.cap + c->bnd.cap;
+    const uint64_t held = c->tb.cap + c->bnd.cap + c->ck.cap;
     const uint64_t avail = fr + held, headroom = 8ull << 30;
     const uint64_t budget = avail > 2 * headroom ? avail - headroom : avail / 2;
     const uint64_t fit = budget / per_block;
@@ -592,10 +608,13 @@ static int launch_nw(imsame_ctx *c, NwPlan pl, const uint32_t *cread, const uint
     hipStream_t s = c->stream;
     const uint64_t tb_dw = pl.tb_dw;
     // fewer resident waves if the arena cannot be had (the queue still drains)
-    const uint64_t per_slot = tb_dw * 4, bnd_slot = 3ull * pl.xcap * 4;
+    const uint64_t per_slot = tb_dw * 4, bnd_slot = 3ull * pl.xcap * 4, ck_slot = pl.ck_dw * 4;
     if (c->tb.cap < (uint64_t)pl.blocks * 4 * per_slot)       // grow once to this shape's full residency
         (void)c->tb.ensure((uint64_t)pl.max_blocks * 4 * per_slot);
-    while (c->tb.ensure((uint64_t)pl.blocks * 4 * per_slot) || c->bnd.ensure((uint64_t)pl.blocks * 4 * bnd_slot + 64)) {
+    if (ck_slot && c->ck.cap < (uint64_t)pl.blocks * 4 * ck_slot)
+        (void)c->ck.ensure((uint64_t)pl.max_blocks * 4 * ck_slot);
+    while (c->tb.ensure((uint64_t)pl.blocks * 4 * per_slot) || c->bnd.ensure((uint64_t)pl.blocks * 4 * bnd_slot + 64) ||
+           (ck_slot && c->ck.ensure((uint64_t)pl.blocks * 4 * ck_slot))) {
         if (pl.blocks == 1) return IMSAME_E_OOM;
         pl.blocks = (pl.blocks + 1) / 2;
     }
@@ -615,10 +634,15 @@ static int launch_nw(imsame_ctx *c, NwPlan pl, const uint32_t *cread, const uint
     P.paths = c->paths.as<uint32_t>(); P.paths_cap = paths_cap;
     P.paths_used = (uint32_t *)(ctr + C_PATHS); P.want_paths = p->want_paths;
     P.flags = (uint32_t *)(ctr + C_FLAGS);
+    P.ck = pl.two ? c->ck.as<uint32_t>() : nullptr; P.ck_wave_dw = pl.ck_dw;
+    P.band_w = pl.band_w; P.redo = (uint32_t *)(ctr + C_REDO);
+    P.prof = getenv("IMSAME_NW_PROF") ? (unsigned long long *)(ctr + C_PROF) : nullptr;
     HIPCHK(hipMemsetAsync(work, 0, 4, s));
     HIPCHK(hipEventRecord(c->ev0, s));
-    if (pl.pk && pl.last4) nw16_kernel<true><<<pl.blocks, 256, pl.lds, s>>>(P);
-    else if (pl.pk)       nw16_kernel<false><<<pl.blocks, 256, pl.lds, s>>>(P);
+    if (pl.two && pl.last4)     nw16_kernel<true, true><<<pl.blocks, 256, pl.lds, s>>>(P);
+    else if (pl.two)            nw16_kernel<false, true><<<pl.blocks, 256, pl.lds, s>>>(P);
+    else if (pl.pk && pl.last4) nw16_kernel<true, false><<<pl.blocks, 256, pl.lds, s>>>(P);
+    else if (pl.pk)             nw16_kernel<false, false><<<pl.blocks, 256, pl.lds, s>>>(P);
     else if (pl.nstr > 1) nw_kernel<true><<<pl.blocks, 256, pl.lds, s>>>(P);
     else                  nw_kernel<false><<<pl.blocks, 256, pl.lds, s>>>(P);
     HIPCHK(hipEventRecord(c->ev1, s));
@@ -878,6 +902,12 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     st.n_hits = hc[C_HITS];
     st.nw_cells = hc[C_CELLS];
     st.n_accepted = hc[C_NACC];
+    st.nw_redo = (uint32_t)hc[C_REDO];
+    if (getenv("IMSAME_NW_PROF")) {           // diagnostics: nw16 phase cycles (summed over waves)
+        const double tot = (double)(hc[C_PROF] + hc[C_PROF + 1] + hc[C_PROF + 2] + hc[C_PROF + 3] + hc[C_PROF + 4]);
+        fprintf(stderr, "[nwprof] setup %.3f sweep1 %.3f reduce %.3f sweep2 %.3f walk %.3f (fractions of %.4g wave-cycles)\n",
+                hc[C_PROF] / tot, hc[C_PROF + 1] / tot, hc[C_PROF + 2] / tot, hc[C_PROF + 3] / tot, hc[C_PROF + 4] / tot, tot);
+    }
     st.nw_launch_ms = st.nw_launches ? st.ms_nw / st.nw_launches : 0;
     st.nw_bytes = 2 * st.nw_cells;       // 2 B/cell traceback floor; bench.py adds xlen + ylen per NW
     int ret = IMSAME_OK;
@@ -1000,6 +1030,7 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
             st.n_hits += x.n_hits; st.rounds = std::max(st.rounds, x.rounds);
             if (x.err_read < st.err_read) { st.err_read = x.err_read; st.err_dbseq = x.err_dbseq; }
             st.ms_seed += x.ms_seed; st.ms_nw += x.ms_nw; st.nw_bytes += x.nw_bytes; st.n_rewalk += x.n_rewalk;
+            st.nw_redo += x.nw_redo;
             st.ms_setup = std::max(st.ms_setup, x.ms_setup); st.ms_d2h += x.ms_d2h;
             iv.insert(iv.end(), L[k]->nw_iv.begin(), L[k]->nw_iv.end());
         }
@@ -1212,7 +1243,7 @@ extern "C" int imsame_dev_align_sliced(imsame_ctx *c, const uint8_t *db_seq, uin
                 rc = imsame_dev_fetch_paths(c, acc.data() + used, pu, &pu);
             }
             if (rc) { ret = rc; break; }
-            tot.n_rewalk += st.n_rewalk;
+            tot.n_rewalk += st.n_rewalk; tot.nw_redo += st.nw_redo;
             tot.n_nw += st.n_nw; tot.nw_cells += st.nw_cells; tot.n_hits += st.n_hits; tot.rounds += st.rounds;
             tot.ms_seed += st.ms_seed; tot.ms_nw += st.ms_nw; tot.nw_launches += st.nw_launches;
             tot.nw_bytes += st.nw_bytes;

@@ -41,6 +41,19 @@
 // (T[i-1][j-1], col j-1) after it, as nw_kernel.hip; TbAcc16 hands the walk
 // that kernel's nibble.
 //
+// Two passes (TWO, the default): the full sweep writes no traceback -- it
+// keeps the DP values, the best cell and, every NW16_CK steps, a checkpoint of
+// the wave's whole register state (56 dwords per lane) -- and a second sweep
+// restarts each half from the last checkpoint at least band_w rows above its
+// best cell, per half (its own rows: two LDS row reads and per-half row masks),
+// and writes the traceback of those ~band_w + NW16_CK + G steps only.  The
+// walk reads only rows the second sweep wrote (TbAcc16::has); a path that
+// leaves them is LOST and the wave redoes the second sweep from row 1 for it
+// (same values: the state restored is the state the first sweep had).  The
+// move bits and their packing are 6 of the 23 instructions per cell pair, so
+// the first sweep issues ~190 VALU per step instead of 250, and ~90 % of the
+// steps are first-sweep steps at C2 (2000-row records, 150-column reads).
+//
 // Range: scores are int16.  The host picks this kernel only when every value
 // of the launch (including the garbage rows/columns a lockstep group computes
 // past a shorter candidate, which are DP values of an extended problem) stays
@@ -49,6 +62,8 @@
 
 #define NW16_K   10               // columns per lane
 #define NW16_BIG 16384
+#define NW16_CK  24               // checkpoint interval of the first sweep (steps, a multiple of 3)
+#define NW16_NST (5 * NW16_K + 6) // dwords of wave state per lane in a checkpoint
 
 // does the launch fit the int16 path?  (all gap terms non-positive)
 __host__ static inline bool nw16_fits(int64_t ig, int64_t eg, uint64_t xcap, uint64_t ymax) {
@@ -57,7 +72,8 @@ __host__ static inline bool nw16_fits(int64_t ig, int64_t eg, uint64_t xcap, uin
     const uint64_t aig = (uint64_t)(-ig), aeg = (uint64_t)(-eg);
     if (aig > 8191 || aeg > 8191) return false;
     // |T| <= 4*ycols; l0 >= -T - |ig| - |eg|*ycols; u0 drifts at most over
-    // xcap + 64 rows (lockstep garbage rows included) and takes u2 + ig + 2eg
+    // xcap + 64 rows (lockstep garbage rows included -- a second sweep runs at
+    // most NW16_CK + G <= 40 rows past the first one) and takes u2 + ig + 2eg
     const uint64_t R = 4 * ycols + aig + aeg * (xcap + 64 + ycols + 2) + 16;
     return R <= 8191;
 }
@@ -73,11 +89,14 @@ WV_DEVICE uint32_t base_code(uint8_t b) { return (b >> 1) & 3u; }          // A0
 #define NW16_TBL_HI 0xFFFFFF00u
 
 // traceback of half h of group g (layout above) -> nw_kernel.hip's nibble
+// t0: step of the sweep that wrote record 0 (0: one pass, steps indexed by t;
+// two passes: the half's restart step, cells before it were not written)
 struct TbAcc16 {
-    const uint32_t *tb; const uint8_t *X; const uint8_t *Y; int g, G, h;
+    const uint32_t *tb; const uint8_t *X; const uint8_t *Y; int g, G, h, t0;
+    __device__ bool has(int i, int j) const { return i + j / NW16_K >= t0; }
     __device__ uint32_t nib(int i, int j) const {
         const int l = j / NW16_K, s = j - l * NW16_K;
-        const uint32_t *w = tb + ((uint32_t)(i + l) * 64u + (uint32_t)(g * G + l)) * 3u;
+        const uint32_t *w = tb + ((uint32_t)(i + l - t0) * 64u + (uint32_t)(g * G + l)) * 3u;
         uint32_t nd, up, U, nL;
         if (s < 8) {
             const uint32_t wm = w[0], wu = w[1];
@@ -99,7 +118,8 @@ __host__ __device__ static inline size_t nw16_wave_lds(int GPW, int xstride) {
 
 // LAST: every read length of the launch is a multiple of NW16_K, so each
 // candidate's last column is slot NW16_K-1 of its owner lane (no select).
-template <bool LAST>
+// TWO: score-only sweep + checkpoints, then the traceback band (header).
+template <bool LAST, bool TWO>
 __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const uint32_t slot) {
     constexpr int K = NW16_K;
     const int G = P.G, GPW = P.GPW;
@@ -108,8 +128,15 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
     const int gg = in_group ? g : 0;
     int *red = (int *)(wsm + (size_t)GPW * P.xstride);                // 64 lanes x 8 ints
     uint32_t *tbw = P.tb + (uint64_t)slot * P.tb_wave_dw;
+    uint32_t *ckw = TWO ? P.ck + (uint64_t)slot * P.ck_wave_dw + lane : nullptr;
     const int ig = P.igap, eg = P.egap;
 
+    // phase profile (P.prof): 0 fetch + staging + setup, 1 first sweep, 2 best-cell
+    // reduction, 3 second sweep(s) incl. restore, 4 walks + results
+    unsigned long long ph[5] = {0, 0, 0, 0, 0}, tq = P.prof ? wv_clock() : 0;
+    auto mark = [&](const int k) {
+        if (P.prof) { const unsigned long long n = wv_clock(); ph[k] += n - tq; tq = n; }
+    };
     for (;;) {
         uint32_t base = 0;
         if (lane == 0) base = wv_atomic_add(P.counter, (uint32_t)(2 * GPW));
@@ -201,7 +228,7 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
         const uint32_t limp = pk2(xl[0] - 2, xl[1] - 2);
         uint8_t *tb3 = (uint8_t *)tbw;
 
-        auto step = [&](const bool PRE, const bool CAREFUL, const int t, uint32_t (&cur)[K],
+        auto step = [&](const bool PRE, const bool CAREFUL, const bool TB, const int t, uint32_t (&cur)[K],
                         const uint32_t (&own)[K], const uint32_t (&own2)[K], uint32_t &in0, const uint32_t in1,
                         const uint32_t in2) {
             const uint32_t sN = (uint32_t)wv_shr1((int)outT), mS = (uint32_t)wv_shr1((int)outMS),
@@ -225,7 +252,7 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
                 cur[s] = pre ? own[s] : v;
                 // move bits: signs of (d0 - lu) [not diagonal] and (l0 - up) [up > left] (:457-472)
                 // (sign-replicating selectors 8-11: bytes 0xFF / 0x00, no shift before packing)
-                const uint32_t P2 = wv_perm(pk_sub(l0, up), pk_sub(d0, lu), 0x0B0A0908u);
+                const uint32_t P2 = TB ? wv_perm(pk_sub(l0, up), pk_sub(d0, lu), 0x0B0A0908u) : 0u;
                 // column max of column j-1 over rows <= i-2, strict > (:476-480)
                 const uint32_t mU = pk_neg_mask(pk_sub(mcS[s], u2));
                 const uint32_t u0n = wv_bfi(mU, pk_add(u2, IG2E), pk_add(u0[s], EG));
@@ -236,7 +263,8 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
                 l0 = wv_bfi(mnL, pk_add(l0, EG), pk_add(d0, IGE));
                 mfS = wv_bfi(mnL, mfS, d0);
                 if (s == 0) { mfS = leadc0 ? NBIG : mfS; l0 = leadc0 ? NBIG : l0; }   // j = 1: mf = T[i][0]
-                if (s < 8) {
+                if (!TB) {
+                } else if (s < 8) {
                     wm = wv_and_or(P2, 0x01010101u << s, wm);
                     wu = wv_and_or(mU, 0x00010001u << s, wu);
                     wu = wv_and_or(mnL, 0x01000100u << s, wu);
@@ -249,8 +277,10 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
             }
             // rows outside [1, xlen) are never read; 32-bit byte offset from the
             // wave-uniform slot base (global_store saddr form)
-            uint32_t *rec = (uint32_t *)(tb3 + ((uint32_t)t * 768u + (uint32_t)lane * 12u));
-            rec[0] = wm; rec[1] = wu; rec[2] = wx;
+            if (TB) {
+                uint32_t *rec = (uint32_t *)(tb3 + ((uint32_t)t * 768u + (uint32_t)lane * 12u));
+                rec[0] = wm; rec[1] = wu; rec[2] = wx;
+            }
             // last column (rows 1 .. xlen-2) and last row (:481-484)
             uint32_t vl = cur[LAST ? K - 1 : 0];
             if (!LAST)
@@ -276,27 +306,49 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
             in0 = pre ? in1 : sN;
             outT = cur[K - 1]; outMS = mfS; outL = l0;
         };
+        // Checkpoint m = the state before step 1 + m*NW16_CK, where the roles
+        // are (cur, own, own2) = (A, B, C), (in0, in1, in2) = (I3, I1, I2);
+        // register r of lane l at ckw[(m*NW16_NST + r)*64] (coalesced).
+        constexpr bool TB1 = !TWO;                // the first sweep writes traceback only in one-pass mode
+        auto save = [&](const int m) {
+            uint32_t *p = ckw + (uint32_t)m * (NW16_NST * 64u);
+#pragma unroll
+            for (int s = 0; s < K; ++s) {
+                p[s * 64] = A[s]; p[(K + s) * 64] = B[s]; p[(2 * K + s) * 64] = C[s];
+                p[(3 * K + s) * 64] = mcS[s]; p[(4 * K + s) * 64] = u0[s];
+            }
+            p[5 * K * 64] = I1; p[(5 * K + 1) * 64] = I2; p[(5 * K + 2) * 64] = I3;
+            p[(5 * K + 3) * 64] = outT; p[(5 * K + 4) * 64] = outMS; p[(5 * K + 5) * 64] = outL;
+        };
+        int nextck = 1 + NW16_CK, mck = 1;
+        auto ck = [&](const int t) { if (TWO && t == nextck) { save(mck); ++mck; nextck += NW16_CK; } };
+        if (TWO) save(0);
+        mark(0);
         // (cur, own, own2) and (in0, in1, in2) rotate every step; every loop
         // advances t by 3 so the rotation phase carries over
         int t = 1;
         for (; t + 2 < tend && t <= G + 1; t += 3) {             // skewed start: lanes may be at row <= 1
-            step(true, true, t, A, B, C, I3, I1, I2);
-            step(true, true, t + 1, C, A, B, I2, I3, I1);
-            step(true, true, t + 2, B, C, A, I1, I2, I3);
+            ck(t);
+            step(true, true, TB1, t, A, B, C, I3, I1, I2);
+            step(true, true, TB1, t + 1, C, A, B, I2, I3, I1);
+            step(true, true, TB1, t + 2, B, C, A, I1, I2, I3);
         }
         for (; t + 2 <= xmin - 2; t += 3) {                      // every lane inside every record, row >= 2
-            step(false, false, t, A, B, C, I3, I1, I2);
-            step(false, false, t + 1, C, A, B, I2, I3, I1);
-            step(false, false, t + 2, B, C, A, I1, I2, I3);
+            ck(t);
+            step(false, false, TB1, t, A, B, C, I3, I1, I2);
+            step(false, false, TB1, t + 1, C, A, B, I2, I3, I1);
+            step(false, false, TB1, t + 2, B, C, A, I1, I2, I3);
         }
         for (; t + 2 < tend; t += 3) {
-            step(false, true, t, A, B, C, I3, I1, I2);
-            step(false, true, t + 1, C, A, B, I2, I3, I1);
-            step(false, true, t + 2, B, C, A, I1, I2, I3);
+            ck(t);
+            step(false, true, TB1, t, A, B, C, I3, I1, I2);
+            step(false, true, TB1, t + 1, C, A, B, I2, I3, I1);
+            step(false, true, TB1, t + 2, B, C, A, I1, I2, I3);
         }
-        if (t < tend) step(true, true, t, A, B, C, I3, I1, I2);
-        if (t + 1 < tend) step(true, true, t + 1, C, A, B, I2, I3, I1);
-        wv_mem_sync();                            // traceback written by all lanes, read by the walkers
+        if (t < tend) step(true, true, TB1, t, A, B, C, I3, I1, I2);
+        if (t + 1 < tend) step(true, true, TB1, t + 1, C, A, B, I2, I3, I1);
+        wv_mem_sync();                            // traceback / checkpoints written by all lanes
+        mark(1);
 
         // best cell per half: row-major order, ">=" -> last visited wins
         for (int h = 0; h < 2; ++h) {
@@ -319,12 +371,127 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
             else          { bscore[h] = bC; bx[h] = bCi; by[h] = yl[h] - 1; }
         }
         wv_lds_sync();
-        for (int h = 0; h < 2; ++h) {
-            const TbAcc16 acc16 = {tbw, X8, Yp[h], gg, G, h};
-            nw_finish(P, acc16, xl[h], yl[h], valid[h], gg, gl, G, bscore[h], bx[h], by[h], cidx[h], sid[h]);
+        mark(2);
+        if (!TWO) {
+            for (int h = 0; h < 2; ++h) {
+                const TbAcc16 acc16 = {tbw, X8, Yp[h], gg, G, h, 0};
+                nw_finish(P, acc16, xl[h], yl[h], valid[h], gg, gl, G, bscore[h], bx[h], by[h], cidx[h], sid[h]);
+            }
+            wv_lds_sync();
+            mark(4);
+            continue;
+        }
+
+        // ------------------------------------------- second sweep: the band
+        // Half h restarts at step t0h[h] (a checkpoint at least band_w rows
+        // above its best cell; 1 = the start) and runs until every lane of its
+        // group has passed row bx[h]; per-half rows i_h = t0h[h] + tau - gl.
+        bool todo[2] = {valid[0], valid[1]};
+        int t0h[2] = {1, 1};
+        // MASK: some half may be at row <= 1 (it restarted at step 1)
+        auto step2 = [&](const bool MASK, const int tau, uint32_t (&cur)[K], const uint32_t (&own)[K],
+                         const uint32_t (&own2)[K], uint32_t &in0, const uint32_t in1, const uint32_t in2) {
+            const uint32_t sN = (uint32_t)wv_shr1((int)outT), mS = (uint32_t)wv_shr1((int)outMS),
+                           mL0 = (uint32_t)wv_shr1((int)outL);
+            const int iA = t0h[0] + tau - gl, iB = t0h[1] + tau - gl;
+            const uint32_t xsel = xsel_of(xrow);
+            xrow = (X8[min(max(iA + 1, 0), xcl)] & 3u) | (X8[min(max(iB + 1, 0), xcl)] & 0xCu);
+            // per-half forms of pass 1's `pre` (i < 1: row 0 repeats) and `row1` (i <= 1)
+            const uint32_t pm = !MASK ? 0u : (iA < 1 ? 0x0000FFFFu : 0u) | (iB < 1 ? 0xFFFF0000u : 0u);
+            const uint32_t r1 = !MASK ? 0u : (iA <= 1 ? 0x0000FFFFu : 0u) | (iB <= 1 ? 0xFFFF0000u : 0u);
+            uint32_t mfS = mS, l0 = mL0, wm = 0, wu = 0, wx = 0;
+#pragma unroll
+            for (int s = 0; s < K; ++s) {
+                const uint32_t d0 = (s == 0) ? in1 : own[s - 1];
+                const uint32_t u2 = (s == 0) ? in2 : own2[s - 1];
+                const uint32_t tl = (s == 0) ? sN : cur[s - 1];
+                const uint32_t sc = wv_perm(NW16_TBL_HI, NW16_TBL_LO, xsel ^ yreg[s]);
+                const uint32_t up = MASK ? wv_bfi(r1, NBIG, u0[s]) : u0[s];
+                const uint32_t lu = pk_max(l0, up);
+                uint32_t v = pk_add(pk_max(d0, lu), sc);
+                if (s == 0) v = leadc0 ? sc : v;
+                cur[s] = MASK ? wv_bfi(pm, own[s], v) : v;
+                const uint32_t P2 = wv_perm(pk_sub(l0, up), pk_sub(d0, lu), 0x0B0A0908u);
+                const uint32_t mU = pk_neg_mask(pk_sub(mcS[s], u2));
+                const uint32_t u0n = wv_bfi(mU, pk_add(u2, IG2E), pk_add(u0[s], EG));
+                u0[s] = MASK ? wv_bfi(r1, u0[s], u0n) : u0n;
+                mcS[s] = pk_max(mcS[s], u2);
+                const uint32_t mnL = pk_neg_mask(pk_sub(tl, mfS));
+                l0 = wv_bfi(mnL, pk_add(l0, EG), pk_add(d0, IGE));
+                mfS = wv_bfi(mnL, mfS, d0);
+                if (s == 0) { mfS = leadc0 ? NBIG : mfS; l0 = leadc0 ? NBIG : l0; }
+                if (s < 8) {
+                    wm = wv_and_or(P2, 0x01010101u << s, wm);
+                    wu = wv_and_or(mU, 0x00010001u << s, wu);
+                    wu = wv_and_or(mnL, 0x01000100u << s, wu);
+                } else {
+                    const int q = s - 8;
+                    wx = wv_and_or(P2, 0x01010101u << q, wx);
+                    wx = wv_and_or(mU, 0x00040004u << q, wx);
+                    wx = wv_and_or(mnL, 0x00100010u << q, wx);
+                }
+            }
+            uint32_t *rec = (uint32_t *)(tb3 + ((uint32_t)tau * 768u + (uint32_t)lane * 12u));
+            rec[0] = wm; rec[1] = wu; rec[2] = wx;
+            in0 = MASK ? wv_bfi(pm, in1, sN) : sN;
+            outT = cur[K - 1]; outMS = mfS; outL = l0;
+        };
+        for (int att = 0; att < 2; ++att) {
+            // attempt 0: the band; attempt 1 (a path left it): every half from the start
+            int n2 = 0;
+            for (int h = 0; h < 2; ++h) {
+                const int lo = bx[h] - P.band_w - 1;
+                t0h[h] = (att == 0 && lo >= 0) ? 1 + NW16_CK * (lo / NW16_CK) : 1;
+                if (todo[h]) n2 = max(n2, bx[h] + G - t0h[h]);
+            }
+            for (int o = 32; o > 0; o >>= 1) n2 = max(n2, wv_shfl_xor(n2, o));
+            {   // restore: half A from its checkpoint, half B from its own
+                const uint32_t *pa = ckw + (uint32_t)((t0h[0] - 1) / NW16_CK) * (NW16_NST * 64u);
+                const uint32_t *pb = ckw + (uint32_t)((t0h[1] - 1) / NW16_CK) * (NW16_NST * 64u);
+                auto ld = [&](const int r) { return wv_bfi(0x0000FFFFu, pa[r * 64], pb[r * 64]); };
+#pragma unroll
+                for (int s = 0; s < K; ++s) {
+                    A[s] = ld(s); B[s] = ld(K + s); C[s] = ld(2 * K + s);
+                    mcS[s] = ld(3 * K + s); u0[s] = ld(4 * K + s);
+                }
+                I1 = ld(5 * K); I2 = ld(5 * K + 1); I3 = ld(5 * K + 2);
+                outT = ld(5 * K + 3); outMS = ld(5 * K + 4); outL = ld(5 * K + 5);
+                xrow = (X8[min(max(t0h[0] - gl, 0), xcl)] & 3u) | (X8[min(max(t0h[1] - gl, 0), xcl)] & 0xCu);
+            }
+            // rows <= 1 need the masked step: while tau <= G - min(t0h) (wave-uniform bound)
+            // (every half counts: one that is done still computes, and stays a bounded DP)
+            int tmin = min(t0h[0], t0h[1]);
+            for (int o = 32; o > 0; o >>= 1) tmin = min(tmin, wv_shfl_xor(tmin, o));
+            const int tau_m = G + 1 - tmin;          // rows t0h + tau - gl > 1 for every lane from here on
+            int tau = 0;
+            for (; tau + 2 < n2 && tau < tau_m; tau += 3) {
+                step2(true, tau, A, B, C, I3, I1, I2);
+                step2(true, tau + 1, C, A, B, I2, I3, I1);
+                step2(true, tau + 2, B, C, A, I1, I2, I3);
+            }
+            for (; tau + 2 < n2; tau += 3) {
+                step2(false, tau, A, B, C, I3, I1, I2);
+                step2(false, tau + 1, C, A, B, I2, I3, I1);
+                step2(false, tau + 2, B, C, A, I1, I2, I3);
+            }
+            if (tau < n2) step2(true, tau, A, B, C, I3, I1, I2);
+            if (tau + 1 < n2) step2(true, tau + 1, C, A, B, I2, I3, I1);
+            wv_mem_sync();                        // band traceback written by all lanes, read by the walkers
+            mark(3);
+            for (int h = 0; h < 2; ++h) {
+                const TbAcc16 acc16 = {tbw, X8, Yp[h], gg, G, h, t0h[h]};
+                todo[h] = nw_finish(P, acc16, xl[h], yl[h], todo[h], gg, gl, G, bscore[h], bx[h], by[h], cidx[h],
+                                    sid[h]);
+            }
+            mark(4);
+            if (!wv_any(todo[0] || todo[1])) break;
+            if (lane == 0 && P.redo) wv_atomic_add(P.redo, 1u);
+            wv_mem_sync();                        // walkers done before the redo overwrites the band
         }
         wv_lds_sync();
     }
+    if (P.prof && lane == 0)
+        for (int k = 0; k < 5; ++k) wv_atomic_add64(P.prof + k, ph[k]);
 }
 
 // Launch shape: G lanes per group, GPW groups (2*GPW candidates) per wave
@@ -341,17 +508,21 @@ __host__ static inline NwShape nw16_shape(uint32_t ymax, uint32_t xcap) {
 }
 // traceback dwords per wave slot (three per lane per step)
 __host__ static inline uint64_t nw16_tb_words(const NwShape &s) { return (uint64_t)s.steps * 64 * 3; }
+// checkpoint dwords per wave slot (two-pass mode): one per NW16_CK steps + the start
+__host__ static inline uint64_t nw16_ck_words(const NwShape &s) {
+    return (uint64_t)((s.steps + NW16_CK - 1) / NW16_CK + 1) * NW16_NST * 64;
+}
 
 #ifndef IMSAME_WAVE_EMU
 #ifndef NW16_WAVES_PER_EU
 #define NW16_WAVES_PER_EU 4
 #endif
-template <bool LAST>
+template <bool LAST, bool TWO>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NW16_WAVES_PER_EU)))
 void nw16_kernel(NwLaunch P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
     const uint32_t slot = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + wib);   // wave-uniform
-    nw16_wave<LAST>(P, smem + wib * nw16_wave_lds(P.GPW, P.xstride), lane, slot);
+    nw16_wave<LAST, TWO>(P, smem + wib * nw16_wave_lds(P.GPW, P.xstride), lane, slot);
 }
 #endif

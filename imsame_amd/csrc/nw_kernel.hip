@@ -56,6 +56,13 @@ struct NwLaunch {
     imsame_read_result *out;     // per candidate
     uint32_t *paths; uint32_t paths_cap; uint32_t *paths_used; uint32_t want_paths;
     uint32_t *flags;             // bit0: path arena overflow, bit1: walk guard tripped
+    // nw16 two-pass mode (nw16_kernel.hip): checkpoints of the first sweep,
+    // one slot per resident wave; rows above a best cell the band keeps;
+    // count of waves whose band missed a path (second sweep redone from row 1)
+    uint32_t *ck; uint64_t ck_wave_dw;
+    int32_t  band_w;
+    uint32_t *redo;
+    unsigned long long *prof;    // optional (IMSAME_NW_PROF): shader cycles per phase, summed over waves
 };
 
 // LDS bytes one wave needs
@@ -212,10 +219,13 @@ __device__ __forceinline__ void nw_sweep(const NwLaunch &P, const NwCand &cd, ui
 // Returns path statistics; emits runs into `path` when emit (lane gl == 0).
 // TB gives nib(i, j) -- the cell's nibble in the layout above -- and
 // match(i, j) = X[i] == Y[j]; one accessor per traceback layout.
-struct WalkOut { int len, idn, ig, eg, cx, cy, nent; bool bad; };
+// lost: the path needs a cell the traceback does not hold (TB::has false --
+// the nw16 second sweep's band); the caller recomputes and walks again.
+struct WalkOut { int len, idn, ig, eg, cx, cy, nent; bool bad, lost; };
 
 struct TbAcc32 {                       // this file's layout: one candidate per group
     const uint32_t *tb; const NwCand *cd; int g, G, steps;
+    __device__ bool has(int, int) const { return true; }
     __device__ uint32_t nib(int i, int j) const { return tb_cell(tb, i, j, g, G, steps); }
     __device__ bool match(int i, int j) const { return cd->X[i] == cd->Y[j]; }
 };
@@ -223,7 +233,7 @@ struct TbAcc32 {                       // this file's layout: one candidate per 
 template <class TB>
 __device__ WalkOut nw_walk(const TB &tbk, int xlen, int ylen, int px, int py, bool walking, int g, int gl,
                            int G, uint32_t *path, bool emit) {
-    WalkOut w = {0, 0, 0, 0, px, py, 0, false};
+    WalkOut w = {0, 0, 0, 0, px, py, 0, false, false};
     const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1);
     int run = 0;                       // pending diagonal run (emit) / in-run flag
     int guard = 4 * (xlen + ylen) + 8;
@@ -232,14 +242,16 @@ __device__ WalkOut nw_walk(const TB &tbk, int xlen, int ylen, int px, int py, bo
         // G diagonal cells at once; the first non-diagonal one stops the run
         const int cx = px - gl, cy = py - gl;
         const bool valid = walking && cx >= 1 && cy >= 1;
+        const bool av = valid && tbk.has(cx, cy);
         uint32_t nib = 0xFu;
         bool match = false;
-        if (valid) {
+        if (av) {
             nib = tbk.nib(cx, cy);
             match = tbk.match(cx, cy);
         }
-        const bool stop = !valid || (nib & 3u) != 0;
-        const unsigned long long bs = wv_ballot(stop), bm = wv_ballot(valid && match);
+        const bool stop = !av || (nib & 3u) != 0;
+        const unsigned long long bs = wv_ballot(stop), bm = wv_ballot(av && match);
+        const unsigned long long bl = (wv_ballot(valid && !av) >> (g * G)) & gmask;
         const unsigned long long gs = (bs >> (g * G)) & gmask;
         const int first = gs ? __builtin_ctzll(gs) : G;
         const unsigned long long below = (first >= 64) ? ~0ull : ((1ull << first) - 1);
@@ -251,6 +263,7 @@ __device__ WalkOut nw_walk(const TB &tbk, int xlen, int ylen, int px, int py, bo
                 if (emit) run += first; else run = 1;
                 w.len += first; w.idn += nm; px -= first; py -= first;
             }
+            if (first < G && ((bl >> first) & 1ull)) { w.lost = true; walking = false; }   // stopped at a missing cell
         }
         const bool jump = walking && first < G && px > 0 && py > 0;
         if (walking && jump && (mvj == 0u || mvj == 3u)) { w.bad = true; walking = false; }
@@ -266,10 +279,14 @@ __device__ WalkOut nw_walk(const TB &tbk, int xlen, int ylen, int px, int py, bo
             while (wv_any(searching)) {
                 const int r = base - gl;
                 const bool ok = searching && r >= 1;
-                const bool u = ok && ((tbk.nib(r, py) >> 2) & 1u);
+                const bool av = ok && tbk.has(r, py);
+                const bool u = av && ((tbk.nib(r, py) >> 2) & 1u);
                 const unsigned long long gb = (wv_ballot(u) >> (g * G)) & gmask;
+                const unsigned long long gm = (wv_ballot(ok && !av) >> (g * G)) & gmask;
                 if (searching) {
-                    if (gb) { src = base - __builtin_ctzll(gb) - 2; searching = false; }
+                    // a missing row above (before) the first U found: the U may be there
+                    if (gm && (!gb || __builtin_ctzll(gm) < __builtin_ctzll(gb))) { w.lost = true; searching = false; }
+                    else if (gb) { src = base - __builtin_ctzll(gb) - 2; searching = false; }
                     else if (base - G < 1) { src = 0; searching = false; }
                     else base -= G;
                 }
@@ -282,16 +299,20 @@ __device__ WalkOut nw_walk(const TB &tbk, int xlen, int ylen, int px, int py, bo
             while (wv_any(searching)) {
                 const int c = base - gl;
                 const bool ok = searching && c >= 1;
-                const bool l = ok && ((tbk.nib(px, c) >> 3) & 1u);
+                const bool av = ok && tbk.has(px, c);
+                const bool l = av && ((tbk.nib(px, c) >> 3) & 1u);
                 const unsigned long long gb = (wv_ballot(l) >> (g * G)) & gmask;
+                const unsigned long long gm = (wv_ballot(ok && !av) >> (g * G)) & gmask;
                 if (searching) {
-                    if (gb) { lsrc = base - __builtin_ctzll(gb) - 1; searching = false; }
+                    if (gm && (!gb || __builtin_ctzll(gm) < __builtin_ctzll(gb))) { w.lost = true; searching = false; }
+                    else if (gb) { lsrc = base - __builtin_ctzll(gb) - 1; searching = false; }
                     else if (base - G < 1) { w.bad = true; searching = false; }   // L(i,1) always set
                     else base -= G;
                 }
             }
             if (is_left) src = lsrc;
         }
+        if (w.lost) walking = false;
         if (walking && jump && !w.bad) {
             int n;
             if (is_up) { n = px - src; px = src; py -= 1; }     // X run vs '-'  (:520-530)
@@ -311,18 +332,21 @@ __device__ WalkOut nw_walk(const TB &tbk, int xlen, int ylen, int px, int py, bo
             if (--guard < 0) { w.bad = true; walking = false; }
         }
     }
-    if (emit && gl == 0 && run && !w.bad) path[w.nent - 1] = (IMSAME_MOVE_DIAG << 30) | (uint32_t)run;
+    if (emit && gl == 0 && run && !w.bad && !w.lost) path[w.nent - 1] = (IMSAME_MOVE_DIAG << 30) | (uint32_t)run;
     w.cx = px; w.cy = py;
     return w;
 }
 
 // Backtrack + acceptance + result of one candidate per group (all lanes of
 // the wave call it; lanes with !cvalid only take part in the wave votes).
+// Returns true (and writes nothing) where the path left the traceback held.
 template <class TB>
-__device__ void nw_finish(const NwLaunch &P, const TB &acc32, const int xlen, const int ylen, const bool cvalid,
+__device__ bool nw_finish(const NwLaunch &P, const TB &acc32, const int xlen, const int ylen, const bool cvalid0,
                           const int gg, const int gl, const int G, const int bscore, const int bx, const int by,
                           const uint32_t c, const uint32_t sid) {
-        WalkOut w = nw_walk(acc32, xlen, ylen, bx, by, cvalid, gg, gl, G, nullptr, false);
+        WalkOut w = nw_walk(acc32, xlen, ylen, bx, by, cvalid0, gg, gl, G, nullptr, false);
+        const bool lost = cvalid0 && w.lost;
+        const bool cvalid = cvalid0 && !w.lost;
         bool acc = false;
         if (cvalid && !w.bad) {
             acc = (uint32_t)ylen < P.n_minlen && (uint32_t)w.len >= P.minlen[ylen] &&
@@ -358,6 +382,7 @@ __device__ void nw_finish(const NwLaunch &P, const TB &acc32, const int xlen, co
             r.path_off = poff; r.path_len = plen;
             P.out[c] = r;
         }
+        return lost;
 }
 
 // One wave's share of a launch: pulls groups of GPW candidates from the work

@@ -28,6 +28,9 @@ WV_DEVICE uint32_t wv_first(uint32_t v) { return __builtin_amdgcn_readfirstlane(
 WV_DEVICE uint32_t wv_atomic_add(uint32_t *p, uint32_t v) { return atomicAdd(p, v); }
 WV_DEVICE void wv_atomic_or(uint32_t *p, uint32_t v) { atomicOr(p, v); }
 WV_DEVICE void wv_atomic_min64(unsigned long long *p, unsigned long long v) { atomicMin(p, v); }
+WV_DEVICE void wv_atomic_add64(unsigned long long *p, unsigned long long v) { atomicAdd(p, v); }
+// shader clock (phase profiling only)
+WV_DEVICE unsigned long long wv_clock() { return (unsigned long long)clock64(); }
 // LDS written by some lanes, read by others of the SAME wave
 WV_DEVICE void wv_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -137,6 +140,8 @@ inline void wv_atomic_min64(unsigned long long *p, unsigned long long v) {
     unsigned long long cur = __atomic_load_n(p, __ATOMIC_SEQ_CST);
     while (v < cur && !__atomic_compare_exchange_n(p, &cur, v, false, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST)) {}
 }
+inline void wv_atomic_add64(unsigned long long *p, unsigned long long v) { __atomic_fetch_add(p, v, __ATOMIC_SEQ_CST); }
+inline unsigned long long wv_clock() { return 0; }
 inline void wv_lds_sync() { wvemu::sync(); }
 inline void wv_mem_sync() { wvemu::sync(); }
 

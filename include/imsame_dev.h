@@ -64,6 +64,10 @@ typedef struct imsame_params {
  * latency).  Results are identical; the tests use both to cover both kernels. */
 #define IMSAME_FLAG_NW32 1u
 #define IMSAME_FLAG_NW16 2u
+/* the packed kernel in ONE pass (traceback of every row) instead of its
+ * default two passes (score-only sweep + a traceback band under the best
+ * cell, nw16_kernel.hip).  Results are identical. */
+#define IMSAME_FLAG_NW16_ONEPASS 4u
 
 /* Fill the reference defaults: min_e = 1/powl(10,20), cov = id = 0.5,
  * igap = -5, egap = -2, max_read_size = 3000, want_paths = 0. */
@@ -120,6 +124,8 @@ typedef struct imsame_stats {
     double   ms_nw_busy;    /* wall time the device ran NW launches (union of
                                the launch intervals of all lanes)        */
     uint64_t lanes;         /* concurrent lanes the call ran (1 or 2)   */
+    uint64_t nw_redo;       /* two-pass NW: waves whose traceback band missed a
+                               path and redid their second sweep from row 1 */
 } imsame_stats;
 
 typedef struct imsame_ctx imsame_ctx;

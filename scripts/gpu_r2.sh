@@ -39,6 +39,21 @@ for s in $STEPS; do
     lanes*) LN=${s#lanes}; LN=${LN%%_*}; SH=${s#lanes${LN}}; SH=${SH#_}
            IMSAME_LANES=$LN timeout -k 10 600 python -u bench.py --cpu-sample 0 --e2e off --steps 5 ${SH:+--shard ${SH/_//}} \
            > gpurun_out/bench_${s}_${TAG}.json 2> gpurun_out/bench_${s}_${TAG}.err; ok_or_stop $? $s ;;
+    onepass) IMSAME_NW_ONEPASS=1 timeout -k 10 600 python -u bench.py --cpu-sample 0 --e2e off --steps 5 \
+           > gpurun_out/bench_onepass_${TAG}.json 2> gpurun_out/bench_onepass_${TAG}.err; ok_or_stop $? onepass ;;
+    band*) BW=${s#band}; IMSAME_NW_BAND=$BW timeout -k 10 600 python -u bench.py --cpu-sample 0 --e2e off --steps 5 \
+           > gpurun_out/bench_${s}_${TAG}.json 2> gpurun_out/bench_${s}_${TAG}.err; ok_or_stop $? $s ;;
+    nwprof) IMSAME_NW_PROF=1 IMSAME_LANES=1 timeout -k 10 600 python -u bench.py --cpu-sample 0 --e2e off --steps 1 --warmup 1 \
+           > gpurun_out/bench_nwprof_${TAG}.json 2> gpurun_out/bench_nwprof_${TAG}.err; ok_or_stop $? nwprof ;;
+    nwprof1) IMSAME_NW_ONEPASS=1 IMSAME_NW_PROF=1 IMSAME_LANES=1 timeout -k 10 600 python -u bench.py --cpu-sample 0 --e2e off \
+           --steps 1 --warmup 1 > gpurun_out/bench_nwprof1_${TAG}.json 2> gpurun_out/bench_nwprof1_${TAG}.err; ok_or_stop $? nwprof1 ;;
+    pmcsq) timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_BUSY_CYCLES \
+             --kernel-include-regex 'nw16_kernel|seed_' -T -d gpurun_out/pmc_${TAG}_p1 -o pmc --output-format csv \
+             -- python3 bench.py --steps 1 --warmup 0 --cpu-sample 0 --e2e off > gpurun_out/pmc_${TAG}_p1.json \
+             2> gpurun_out/pmc_${TAG}_p1.err; ok_or_stop $? pmcsq ;;
+    nwtests) timeout -k 10 900 python -u -m pytest tests/test_gpu.py -m gpu -v --timeout 300 --timeout-method thread \
+             -k "two_pass or nw_pairs or nw_packed or c2_shape or e2e or lanes or path_arena" \
+             > gpurun_out/pytest_nw_${TAG}.log 2>&1; ok_or_stop $? nwtests ;;
     c5) timeout -k 10 600 python -u bench.py --config c5 --steps 1 --warmup 0 > gpurun_out/bench_c5_${TAG}.json \
            2> gpurun_out/bench_c5_${TAG}.err; ok_or_stop $? c5 ;;
     c5wprof) timeout -k 10 900 rocprofv3 --kernel-trace --stats -T -d gpurun_out/prof_c5w_${TAG} -o kt --output-format csv \

@@ -43,14 +43,22 @@ static void run_wave(const std::function<void(int)> &f) {
     for (auto &t : th) t.join();
 }
 
+// waves whose nw16 traceback band missed a path (NwLaunch::redo), since the last emu_redo_count()
+static uint32_t g_redo;
+extern "C" uint32_t emu_redo_count(void) { const uint32_t r = g_redo; g_redo = 0; return r; }
+
 static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, const uint64_t *qs,
                   const uint32_t *cread, const uint32_t *csid, uint32_t n, const imsame_params *p, uint32_t ymax,
                   uint32_t xmax, const std::vector<uint32_t> &ml, const std::vector<uint32_t> &mi,
                   imsame_read_result *out, uint32_t *paths, uint32_t pcap, uint32_t *pused, uint32_t *flags) {
     // same kernel choice as imsame_dev.hip:plan_nw
     const bool pk = !(p->flags & IMSAME_FLAG_NW32) && nw16_fits(p->igap, p->egap, xmax, ymax);
+    const char *op = getenv("IMSAME_NW_ONEPASS");
+    const bool two = pk && !(p->flags & IMSAME_FLAG_NW16_ONEPASS) && !(op && atoi(op));
     const NwShape sh = pk ? nw16_shape(ymax, xmax) : nw_shape(ymax, xmax);
     std::vector<uint32_t> tb((pk ? nw16_tb_words(sh) : nw_tb_words(sh)) + 64, 0xABABABABu);
+    std::vector<uint32_t> ck(two ? nw16_ck_words(sh) : 1, 0xCDCDCDCDu);
+    const char *be = getenv("IMSAME_NW_BAND");
     std::vector<int32_t> bnd((size_t)3 * sh.xcap + 64);
     std::vector<uint8_t> lds((pk ? nw16_wave_lds(sh.GPW, sh.xstride) : nw_wave_lds(sh.GPW, sh.xstride)) + 64, 0xA5);
     uint32_t counter = 0;
@@ -67,10 +75,15 @@ static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, cons
     P.counter = &counter; P.out = out;
     P.paths = paths; P.paths_cap = pcap; P.paths_used = pused; P.want_paths = p->want_paths;
     P.flags = flags;
+    P.ck = ck.data(); P.ck_wave_dw = ck.size();
+    P.band_w = be ? std::max(0, atoi(be)) : 200;        // imsame_dev.hip:nw16_band_rows
+    P.redo = &g_redo;
     bool ymult = true;        // every read length a multiple of NW16_K (imsame_dev.hip: q_len_mult)
     for (uint32_t k = 0; k < n; ++k) ymult = ymult && (qs[cread[k] + 1] - qs[cread[k]]) % NW16_K == 0;
-    if (pk && ymult)      run_wave([&](int lane) { nw16_wave<true>(P, lds.data(), lane, 0); });
-    else if (pk)          run_wave([&](int lane) { nw16_wave<false>(P, lds.data(), lane, 0); });
+    if (two && ymult)     run_wave([&](int lane) { nw16_wave<true, true>(P, lds.data(), lane, 0); });
+    else if (two)         run_wave([&](int lane) { nw16_wave<false, true>(P, lds.data(), lane, 0); });
+    else if (pk && ymult) run_wave([&](int lane) { nw16_wave<true, false>(P, lds.data(), lane, 0); });
+    else if (pk)          run_wave([&](int lane) { nw16_wave<false, false>(P, lds.data(), lane, 0); });
     else if (sh.nstr > 1) run_wave([&](int lane) { nw_wave<true>(P, lds.data(), lane, 0); });
     else             run_wave([&](int lane) { nw_wave<false>(P, lds.data(), lane, 0); });
     return 0;

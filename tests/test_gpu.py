@@ -9,7 +9,7 @@ import tempfile
 import numpy as np
 import pytest
 
-from imsame_amd import Device, render, fasta, CLI, PARITY_FIELDS, FLAG_NW32, FLAG_NW16
+from imsame_amd import Device, render, fasta, CLI, PARITY_FIELDS, FLAG_NW32, FLAG_NW16, FLAG_NW16_ONEPASS
 from imsame_amd import abi
 from tests import golden_io as G
 from tests import synth
@@ -187,6 +187,38 @@ def test_synthetic_c2_shape_vs_oracle_all_T(dev, oracle):
     full, _, _ = dev.align(n_threads=8)
     parts = [dev.align(a, b, n_threads=8)[0] for a, b in ((0, 3001), (3001, 7777), (7777, 12_000))]
     assert not _cmp(np.concatenate(parts), full)
+
+
+def test_nw16_two_pass_equals_one_pass(dev, oracle):
+    """The packed kernel's two passes (score-only sweep + checkpoints, then a
+    traceback band restored from the checkpoint above each best cell) give
+    the one-pass kernel's rows AND paths; bands too small to hold a path make
+    the waves redo their second sweep from row 1, with the same results."""
+    ref, rst = synth.make_reference_arr(2_000_000, 2_000, seed=44)
+    q, qs = synth.make_reads_arr(ref, 12_000, 150, seed=45)
+    dev.index(ref, rst)
+    dev.set_query(q, qs)
+    p1 = dev.params(flags=FLAG_NW16 | FLAG_NW16_ONEPASS)
+    one, paths1, st1 = dev.align(n_threads=16, params=p1, want_paths=True)
+    assert st1.nw_redo == 0 and (one["status"] == 1).sum() > 10_000
+
+    def path(res, paths, k):
+        return paths[res["path_off"][k]:res["path_off"][k] + res["path_len"][k]].tolist()
+
+    for band in (None, "40", "0"):
+        if band is not None:
+            os.environ["IMSAME_NW_BAND"] = band
+        try:
+            two, paths2, st2 = dev.align(n_threads=16, params=dev.params(flags=FLAG_NW16), want_paths=True)
+        finally:
+            os.environ.pop("IMSAME_NW_BAND", None)
+        assert not _cmp(two, one), (band, _cmp(two, one))
+        acc = np.flatnonzero(one["status"] == 1)
+        assert all(path(two, paths2, k) == path(one, paths1, k) for k in acc[::7]), band
+        if band == "0":
+            assert st2.nw_redo > 0
+    rc, exp, _ = oracle.align(ref, rst, q, qs, None, 16)
+    assert rc == 0 and not _cmp(one, exp)
 
 
 def test_c1_shape_vs_oracle(dev, oracle):

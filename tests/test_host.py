@@ -133,6 +133,56 @@ def test_emulated_packed_nw_mixed_shapes(emu, oracle):
                 assert int(res[k][f]) == int(o[f]), (f, k, ig, eg, len(X[k]), len(Y[k]))
 
 
+@pytest.mark.parametrize("band", ["200", "40", "0"])
+def test_emulated_two_pass_band(emu, oracle, band, monkeypatch):
+    """nw16_kernel.hip's two passes (emulated): the score-only sweep with
+    checkpoints, then the traceback band restored per half from its own
+    checkpoint.  Records long enough that the band starts past row 1; small
+    bands make paths leave it, so the waves redo the second sweep from row 1.
+    Every field and every path equals the one-pass kernel and the oracle."""
+    rng = np.random.default_rng(int(band) + 5)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    X, Y = [], []
+    for k in range(9):
+        xl = int(rng.integers(250, 700))
+        yl = int(rng.choice([150, 149, 60, int(rng.integers(20, 161))]))
+        x = acgt[rng.integers(0, 4, xl)]
+        if k % 3 != 2:              # true hits at varied depths (best cells spread over the rows)
+            o = int(rng.integers(0, xl - yl))
+            y = x[o:o + yl].copy()
+            mut = rng.random(yl) < 0.04
+            y[mut] = acgt[rng.integers(0, 4, int(mut.sum()))]
+            if rng.random() < 0.5:  # an indel run: up / left jumps on the path
+                c = int(rng.integers(10, yl - 10))
+                y = np.concatenate([y[:c], acgt[rng.integers(0, 4, 3)], y[c:]])[:yl]
+        else:
+            y = acgt[rng.integers(0, 4, yl)]
+        X.append(x.tobytes()); Y.append(y.tobytes())
+    monkeypatch.setenv("IMSAME_NW_BAND", band)
+    redo = emu.lib.emu_redo_count
+    redo.restype = C.c_uint32
+    redo()
+    p2 = oracle.params(want_paths=1)
+    rc, res2, paths2, fl = emu.nw_pairs(X, Y, p2, paths_cap=4096)
+    assert rc == 0 and fl == 0
+    n_redo = redo()
+    p1 = oracle.params(want_paths=1, flags=imsame_amd.FLAG_NW16_ONEPASS)
+    rc, res1, paths1, fl = emu.nw_pairs(X, Y, p1, paths_cap=4096)
+    assert rc == 0 and fl == 0 and redo() == 0
+    for k in range(len(X)):
+        o = oracle.nw(X[k], Y[k], text=False)
+        for f in ("score", "bx", "by", "length", "identities", "igaps", "egaps", "head_x", "head_y"):
+            assert int(res2[k][f]) == int(o[f]) == int(res1[k][f]), (f, k, band, len(X[k]), len(Y[k]))
+        if res2[k]["status"] == 1:
+            a, b = res2[k], res1[k]
+            assert paths2[a["path_off"]:a["path_off"] + a["path_len"]].tolist() == \
+                paths1[b["path_off"]:b["path_off"] + b["path_len"]].tolist()
+    if band == "0":
+        assert n_redo > 0           # a zero band cannot hold a path: the redo path ran
+    if band == "200":
+        assert n_redo == 0
+
+
 def _emu_ungapped(emu, db, dbs, q, qs, pd0, pq0, read, sid):
     f = emu.lib.emu_ungapped
     f.restype = C.c_uint64
