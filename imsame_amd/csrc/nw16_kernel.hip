@@ -165,9 +165,35 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
         // an idle group (no candidate) reads group 0's record, so its lockstep
         // garbage stays a bounded DP like everyone else's
         uint8_t *X8 = wsm + (size_t)(valid[0] ? g : 0) * P.xstride;
-        if (valid[0])
-            for (int k = gl; k < xlp; k += G)
-                X8[k] = (uint8_t)(base_code(Xg[0][min(k, xl[0] - 1)]) | (base_code(Xg[1][min(k, xl[1] - 1)]) << 2));
+        if (valid[0]) {
+            // 16 rows per lane and iteration: one unaligned 16-byte load per record
+            // where the chunk lies inside it (else bytes clamped to its last base),
+            // codes packed four per dword, one 16-byte LDS store (xstride is a
+            // multiple of 16, so the chunk past xlp stays inside the group's area)
+            const int nch = (xlp + 15) >> 4;
+            for (int c = gl; c < nch; c += G) {
+                const int k0 = c << 4;
+                uint32_t w[2][4];
+                for (int h = 0; h < 2; ++h) {
+                    if (k0 + 16 <= xl[h]) {
+                        __builtin_memcpy(w[h], Xg[h] + k0, 16);
+                    } else {
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            uint32_t v = 0;
+#pragma unroll
+                            for (int b = 0; b < 4; ++b) v |= (uint32_t)Xg[h][min(k0 + 4 * q + b, xl[h] - 1)] << (8 * b);
+                            w[h][q] = v;
+                        }
+                    }
+                }
+                uint32_t o[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q)   // base_code per byte: (b >> 1) & 3; B's code at bits 2-3
+                    o[q] = ((w[0][q] >> 1) & 0x03030303u) | ((w[1][q] << 1) & 0x0C0C0C0Cu);
+                __builtin_memcpy(X8 + k0, o, 16);
+            }
+        }
         wv_lds_sync();
 
         int xmax = valid[0] ? xlp : 0, xmin = valid[0] ? min(xl[0], xl[1]) : INT_MAX;

@@ -51,6 +51,8 @@ for s in $STEPS; do
              --kernel-include-regex 'nw16_kernel|seed_' -T -d gpurun_out/pmc_${TAG}_p1 -o pmc --output-format csv \
              -- python3 bench.py --steps 1 --warmup 0 --cpu-sample 0 --e2e off > gpurun_out/pmc_${TAG}_p1.json \
              2> gpurun_out/pmc_${TAG}_p1.err; ok_or_stop $? pmcsq ;;
+    w5) IMSAME_LIB_DEV=$PWD/imsame_amd/lib/alt/libimsame_dev_w5.so timeout -k 10 600 python -u bench.py --cpu-sample 0 \
+           --e2e off --steps 5 > gpurun_out/bench_w5_${TAG}.json 2> gpurun_out/bench_w5_${TAG}.err; ok_or_stop $? w5 ;;
     nwtests) timeout -k 10 900 python -u -m pytest tests/test_gpu.py -m gpu -v --timeout 300 --timeout-method thread \
              -k "two_pass or nw_pairs or nw_packed or c2_shape or e2e or lanes or path_arena" \
              > gpurun_out/pytest_nw_${TAG}.log 2>&1; ok_or_stop $? nwtests ;;
