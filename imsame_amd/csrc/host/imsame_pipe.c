@@ -186,27 +186,34 @@ static void run_pool(rtask *t, int n, void *(*fn)(void *)) {
     }
 }
 
-/* render reads [from, to) with the task buffers t[0..nt), write at *off */
-static int render_batch(rtask *t, int nt, const host_seqs *db, const host_seqs *q, const imsame_read_result *res,
-                        const uint32_t *paths, uint64_t from, uint64_t to, int fd, int seekable, uint64_t *off,
-                        pipe_result *r) {
-    if (to <= from) return 0;
+/* render reads [from, to) into the task buffers t[0..*nt) and give each its
+ * file offset from *off (advanced past the batch); *nt = tasks used */
+static int render_part(rtask *t, int *nt, const host_seqs *db, const host_seqs *q, const imsame_read_result *res,
+                       const uint32_t *paths, uint64_t from, uint64_t to, int fd, uint64_t *off, pipe_result *r) {
+    if (to <= from) { *nt = 0; return 0; }
     const uint64_t n = to - from;
-    if ((uint64_t)nt > n) nt = (int)n;
-    for (int k = 0; k < nt; ++k) {
+    if ((uint64_t)*nt > n) *nt = (int)n;
+    for (int k = 0; k < *nt; ++k) {
         t[k].db = db; t[k].q = q; t[k].res = res; t[k].paths = paths; t[k].fd = fd; t[k].err = 0;
-        t[k].from = from + n * (uint64_t)k / (uint64_t)nt;
-        t[k].to = from + n * (uint64_t)(k + 1) / (uint64_t)nt;
+        t[k].from = from + n * (uint64_t)k / (uint64_t)*nt;
+        t[k].to = from + n * (uint64_t)(k + 1) / (uint64_t)*nt;
     }
-    double t0 = pipe_now();
-    run_pool(t, nt, render_task);
+    const double t0 = pipe_now();
+    run_pool(t, *nt, render_task);
     r->t_render += pipe_now() - t0;
-    for (int k = 0; k < nt; ++k) {
+    for (int k = 0; k < *nt; ++k) {
         if (t[k].err) return t[k].err;
         t[k].off = *off;
         *off += t[k].text.len;
     }
-    t0 = pipe_now();
+    r->bytes_out = *off;
+    return 0;
+}
+
+/* write what render_part left in t[0..nt): parallel pwrite at the offsets, or
+ * ordered write() for pipes; returns an errno and the wall time in *secs */
+static int write_part(rtask *t, int nt, int fd, int seekable, double *secs) {
+    const double t0 = pipe_now();
     int err = 0;
     if (seekable) {
         run_pool(t, nt, write_task);
@@ -214,9 +221,47 @@ static int render_batch(rtask *t, int nt, const host_seqs *db, const host_seqs *
     } else {
         for (int k = 0; k < nt && !err; ++k) err = write_all(fd, t[k].text.buf, t[k].text.len, 0, 0);
     }
-    r->t_write += pipe_now() - t0;
-    r->bytes_out = *off;
+    *secs = pipe_now() - t0;
     return err;
+}
+
+static int render_batch(rtask *t, int nt, const host_seqs *db, const host_seqs *q, const imsame_read_result *res,
+                        const uint32_t *paths, uint64_t from, uint64_t to, int fd, int seekable, uint64_t *off,
+                        pipe_result *r) {
+    int err = render_part(t, &nt, db, q, res, paths, from, to, fd, off, r);
+    if (err || !nt) return err;
+    double w = 0;
+    err = write_part(t, nt, fd, seekable, &w);
+    r->t_write += w;
+    return err;
+}
+
+/* Output of batch k is written by a writer thread while the main thread
+ * renders batch k+1 into the other buffer set (the kernel copies one file's
+ * writes into the page cache one at a time, so writing -- not rendering --
+ * sets the output rate; overlapping the two hides the rendering). */
+typedef struct { rtask *t; int nt, fd, seekable, err, running; double secs; pthread_t th; } writer;
+
+static void *writer_run(void *a) {
+    writer *w = a;
+    w->err = write_part(w->t, w->nt, w->fd, w->seekable, &w->secs);
+    return NULL;
+}
+
+static int writer_join(writer *w, pipe_result *r) {
+    if (!w->running) return 0;
+    pthread_join(w->th, NULL);
+    w->running = 0;
+    r->t_write += w->secs;
+    return w->err;
+}
+
+static int writer_start(writer *w, rtask *t, int nt, int fd, int seekable) {
+    *w = (writer){.t = t, .nt = nt, .fd = fd, .seekable = seekable};
+    if (!nt) return 0;
+    if (pthread_create(&w->th, NULL, writer_run, w) != 0) return writer_run(w), w->err;
+    w->running = 1;
+    return 0;
 }
 
 static int render_threads(int want) {
@@ -346,10 +391,11 @@ int pipe_align_render(pipe_dev *d, int G, const host_seqs *db, const host_seqs *
         if (!started[g]) align_worker(&W[g]);
     /* walk the batches in read order: render each as it completes */
     const int nt = render_threads(o->render_threads);
-    rtask *rt = prm.want_paths ? calloc((size_t)nt, sizeof *rt) : NULL;
+    rtask *rt = prm.want_paths ? calloc(2 * (size_t)nt, sizeof *rt) : NULL;       /* two buffer sets */
     const int seekable = prm.want_paths && lseek(o->out_fd, 0, SEEK_CUR) >= 0;
     uint64_t off = seekable ? (uint64_t)lseek(o->out_fd, 0, SEEK_CUR) : 0;
-    int rc = 0, werr = 0;
+    int rc = 0, werr = 0, nrend = 0;
+    writer wr = {0};
     double t_last = t0;
     for (k = 0; k < total; ++k) {
         pthread_mutex_lock(&mu);
@@ -361,10 +407,23 @@ int pipe_align_render(pipe_dev *d, int G, const host_seqs *db, const host_seqs *
         if (B[k].rc && B[k].rc != IMSAME_E_READ_TOO_LONG) { if (!rc) rc = B[k].rc; continue; }
         if (B[k].rc == IMSAME_E_READ_TOO_LONG && !rc) rc = IMSAME_E_READ_TOO_LONG;
         const uint64_t hi = B[k].to < sr ? B[k].to : sr;
-        if (rt && !werr && (rc == 0 || rc == IMSAME_E_READ_TOO_LONG))
-            werr = render_batch(rt, nt, db, q, res, B[k].paths, B[k].from, hi, o->out_fd, seekable, &off, r);
+        if (rt && !werr && (rc == 0 || rc == IMSAME_E_READ_TOO_LONG)) {
+            /* set nrend & 1 was last written two batches ago: that writer is joined */
+            rtask *set = rt + (size_t)(nrend & 1) * nt;
+            int used = nt;
+            werr = render_part(set, &used, db, q, res, B[k].paths, B[k].from, hi, o->out_fd, &off, r);
+            const int e = writer_join(&wr, r);              /* batch k-1's output is out */
+            if (!werr) werr = e;
+            if (!werr) werr = writer_start(&wr, set, used, o->out_fd, seekable);
+            nrend++;
+        }
+        /* its paths are no longer needed once rendered (the text is in the set) */
         free(B[k].paths);
         B[k].paths = NULL;
+    }
+    {
+        const int e = writer_join(&wr, r);
+        if (!werr) werr = e;
     }
     for (int g = 0; g < G; ++g)
         if (started[g]) pthread_join(th[g], NULL);
@@ -385,7 +444,7 @@ int pipe_align_render(pipe_dev *d, int G, const host_seqs *db, const host_seqs *
     r->st.err_read = stop_read < n ? stop_read : ~0ull;
     for (uint64_t x = 0; x < stop_read; ++x) r->accepted += res[x].status == 1;
     if (rt) {
-        for (int j = 0; j < nt; ++j) { free(rt[j].text.buf); free(rt[j].scratch.buf); }
+        for (int j = 0; j < 2 * nt; ++j) { free(rt[j].text.buf); free(rt[j].scratch.buf); }
         free(rt);
     }
     free(B);

@@ -23,6 +23,8 @@ for s in $STEPS; do
            ok_or_stop $? smoke ;;
     bench) timeout -k 10 900 python -u bench.py > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err
            ok_or_stop $? bench ;;
+    e2e) timeout -k 10 900 python -u bench.py --cpu-sample 0 --steps 1 > gpurun_out/bench_e2e_${TAG}.json \
+           2> gpurun_out/bench_e2e_${TAG}.err; ok_or_stop $? e2e ;;
     benchq) timeout -k 10 600 python -u bench.py --cpu-sample 0 --e2e off > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err
            ok_or_stop $? benchq ;;
     seedl*) L=${s#seedl}; IMSAME_SEED_L1=$L timeout -k 10 600 python -u bench.py --cpu-sample 0 --e2e off \
@@ -53,6 +55,8 @@ for s in $STEPS; do
              2> gpurun_out/pmc_${TAG}_p1.err; ok_or_stop $? pmcsq ;;
     w5) IMSAME_LIB_DEV=$PWD/imsame_amd/lib/alt/libimsame_dev_w5.so timeout -k 10 600 python -u bench.py --cpu-sample 0 \
            --e2e off --steps 5 > gpurun_out/bench_w5_${TAG}.json 2> gpurun_out/bench_w5_${TAG}.err; ok_or_stop $? w5 ;;
+    clitests) timeout -k 10 900 python -u -m pytest tests/test_gpu.py tests/test_avav.py -m gpu -v --timeout 300 --timeout-method thread \
+             -k "cli or driver or multi_device" > gpurun_out/pytest_cli_${TAG}.log 2>&1; ok_or_stop $? clitests ;;
     nwtests) timeout -k 10 900 python -u -m pytest tests/test_gpu.py -m gpu -v --timeout 300 --timeout-method thread \
              -k "two_pass or nw_pairs or nw_packed or c2_shape or e2e or lanes or path_arena" \
              > gpurun_out/pytest_nw_${TAG}.log 2>&1; ok_or_stop $? nwtests ;;
