@@ -62,8 +62,8 @@
 
 #define NW16_K   10               // columns per lane
 #define NW16_BIG 16384
-#define NW16_CK  24               // checkpoint interval of the first sweep (steps, a multiple of 3)
-#define NW16_NST (5 * NW16_K + 6) // dwords of wave state per lane in a checkpoint
+#define NW16_CK  24               // checkpoint interval of the first sweep (steps, even: the rotation period)
+#define NW16_NST (5 * NW16_K + 5) // dwords of wave state per lane in a checkpoint
 
 // does the launch fit the int16 path?  (all gap terms non-positive)
 __host__ static inline bool nw16_fits(int64_t ig, int64_t eg, uint64_t xcap, uint64_t ymax) {
@@ -206,7 +206,7 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
         const int j0 = gl * K;
         const bool leadc0 = gl == 0;
         const int xcl = max(xlp - 1, 0);
-        const uint32_t NBIG = pk1(-NW16_BIG), EG = pk1(eg), IGE = pk1(ig + eg), IG2E = pk1(ig + 2 * eg);
+        const uint32_t NBIG = pk1(-NW16_BIG), EG = pk1(eg), IGE = pk1(ig + eg);
         uint32_t yreg[K], lastm[K];
         bool ownC[2], lact[2];
         for (int h = 0; h < 2; ++h) {
@@ -233,19 +233,26 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
             yprev = ya | ((ya | 4u) << 8) | (yb << 16) | ((yb | 4u) << 24);
         }
         const uint32_t t0prev = wv_perm(NW16_TBL_HI, NW16_TBL_LO, xsel0 ^ yprev);
-        uint32_t A[K], B[K], C[K], mcS[K], u0[K];
+        // The column state keeps mc's score in a frame shifted by ig + eg: dI[s]
+        // = T[i-2][j-1] + ig + eg is the previous row's d0 + ig + eg of this
+        // slot (the left take computes it anyway), so the column max compares
+        // and takes it directly, and the up term re-based on a take is
+        // dI + eg (= T[i-2][j-1] + ig + 2eg, :450) -- no row i-2 array.
+        uint32_t A[K], B[K], dI[K], mcS[K], u0[K];
 #pragma unroll
         for (int s = 0; s < K; ++s) {
             A[s] = wv_perm(NW16_TBL_HI, NW16_TBL_LO, xsel0 ^ yreg[s]);
-            B[s] = A[s]; C[s] = A[s];
+            B[s] = A[s];
         }
 #pragma unroll
         for (int s = 0; s < K; ++s) {
-            mcS[s] = (s == 0) ? t0prev : A[s - 1];                // mc[j-1] = (T[0][j-1], row 0)
-            u0[s] = pk_add(mcS[s], IGE);                          // its up term at row 2
+            // mc[j-1] = (T[0][j-1], row 0); row 0 stands in for rows -1 and -2
+            dI[s] = pk_add((s == 0) ? t0prev : A[s - 1], IGE);
+            mcS[s] = dI[s];
+            u0[s] = dI[s];                                        // its up term at row 2
             if (j0 + s == 1) mcS[s] = pk1(NW16_BIG);             // mc[0] is never updated (:476)
         }
-        uint32_t I1 = t0prev, I2 = t0prev, I3 = t0prev;
+        uint32_t I1 = t0prev, I2 = t0prev;
         uint32_t outT = A[K - 1], outMS = 0, outL = 0;
         const int tend = xmax - 1 + G;
         xrow = valid[0] ? X8[min(max(1 - gl, 0), xcl)] : 0u;
@@ -255,8 +262,7 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
         uint8_t *tb3 = (uint8_t *)tbw;
 
         auto step = [&](const bool PRE, const bool CAREFUL, const bool TB, const int t, uint32_t (&cur)[K],
-                        const uint32_t (&own)[K], const uint32_t (&own2)[K], uint32_t &in0, const uint32_t in1,
-                        const uint32_t in2) {
+                        const uint32_t (&own)[K], uint32_t &in0, const uint32_t in1) {
             const uint32_t sN = (uint32_t)wv_shr1((int)outT), mS = (uint32_t)wv_shr1((int)outMS),
                            mL0 = (uint32_t)wv_shr1((int)outL);
             const int i = t - gl;
@@ -268,7 +274,6 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
 #pragma unroll
             for (int s = 0; s < K; ++s) {
                 const uint32_t d0 = (s == 0) ? in1 : own[s - 1];     // T[i-1][j-1]
-                const uint32_t u2 = (s == 0) ? in2 : own2[s - 1];    // T[i-2][j-1]
                 const uint32_t tl = (s == 0) ? sN : cur[s - 1];      // T[i][j-1]
                 const uint32_t sc = wv_perm(NW16_TBL_HI, NW16_TBL_LO, xsel ^ yreg[s]);
                 const uint32_t up = row1 ? NBIG : u0[s];
@@ -279,14 +284,16 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
                 // move bits: signs of (d0 - lu) [not diagonal] and (l0 - up) [up > left] (:457-472)
                 // (sign-replicating selectors 8-11: bytes 0xFF / 0x00, no shift before packing)
                 const uint32_t P2 = TB ? wv_perm(pk_sub(l0, up), pk_sub(d0, lu), 0x0B0A0908u) : 0u;
-                // column max of column j-1 over rows <= i-2, strict > (:476-480)
-                const uint32_t mU = pk_neg_mask(pk_sub(mcS[s], u2));
-                const uint32_t u0n = wv_bfi(mU, pk_add(u2, IG2E), pk_add(u0[s], EG));
+                // column max of column j-1 over rows <= i-2, strict > (:476-480), in the
+                // +ig+eg frame: dI[s] = T[i-2][j-1] + ig + eg; the max is the select
+                const uint32_t mU = pk_neg_mask(pk_sub(mcS[s], dI[s]));
+                const uint32_t u0n = pk_add(wv_bfi(mU, dI[s], u0[s]), EG);
                 u0[s] = row1 ? u0[s] : u0n;
-                mcS[s] = pk_max(mcS[s], u2);
+                mcS[s] = wv_bfi(mU, dI[s], mcS[s]);
                 // row state for column j+1: tested on row i, taken from row i-1 (:434-438)
                 const uint32_t mnL = pk_neg_mask(pk_sub(tl, mfS));   // 0xFFFF: mf kept (not L)
-                l0 = wv_bfi(mnL, pk_add(l0, EG), pk_add(d0, IGE));
+                dI[s] = pk_add(d0, IGE);                              // this row's; the next row's u2 + ig + eg
+                l0 = wv_bfi(mnL, pk_add(l0, EG), dI[s]);
                 mfS = wv_bfi(mnL, mfS, d0);
                 if (s == 0) { mfS = leadc0 ? NBIG : mfS; l0 = leadc0 ? NBIG : l0; }   // j = 1: mf = T[i][0]
                 if (!TB) {
@@ -333,46 +340,42 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
             outT = cur[K - 1]; outMS = mfS; outL = l0;
         };
         // Checkpoint m = the state before step 1 + m*NW16_CK, where the roles
-        // are (cur, own, own2) = (A, B, C), (in0, in1, in2) = (I3, I1, I2);
-        // register r of lane l at ckw[(m*NW16_NST + r)*64] (coalesced).
+        // are (cur, own) = (A, B), (in0, in1) = (I2, I1); register r of lane l
+        // at ckw[(m*NW16_NST + r)*64] (coalesced).
         constexpr bool TB1 = !TWO;                // the first sweep writes traceback only in one-pass mode
         auto save = [&](const int m) {
             uint32_t *p = ckw + (uint32_t)m * (NW16_NST * 64u);
 #pragma unroll
             for (int s = 0; s < K; ++s) {
-                p[s * 64] = A[s]; p[(K + s) * 64] = B[s]; p[(2 * K + s) * 64] = C[s];
+                p[s * 64] = A[s]; p[(K + s) * 64] = B[s]; p[(2 * K + s) * 64] = dI[s];
                 p[(3 * K + s) * 64] = mcS[s]; p[(4 * K + s) * 64] = u0[s];
             }
-            p[5 * K * 64] = I1; p[(5 * K + 1) * 64] = I2; p[(5 * K + 2) * 64] = I3;
-            p[(5 * K + 3) * 64] = outT; p[(5 * K + 4) * 64] = outMS; p[(5 * K + 5) * 64] = outL;
+            p[5 * K * 64] = I1; p[(5 * K + 1) * 64] = I2;
+            p[(5 * K + 2) * 64] = outT; p[(5 * K + 3) * 64] = outMS; p[(5 * K + 4) * 64] = outL;
         };
         int nextck = 1 + NW16_CK, mck = 1;
         auto ck = [&](const int t) { if (TWO && t == nextck) { save(mck); ++mck; nextck += NW16_CK; } };
         if (TWO) save(0);
         mark(0);
-        // (cur, own, own2) and (in0, in1, in2) rotate every step; every loop
-        // advances t by 3 so the rotation phase carries over
+        // (cur, own) and (in0, in1) swap every step; every loop advances t by 2
+        // so the phase carries over
         int t = 1;
-        for (; t + 2 < tend && t <= G + 1; t += 3) {             // skewed start: lanes may be at row <= 1
+        for (; t + 1 < tend && t <= G + 1; t += 2) {             // skewed start: lanes may be at row <= 1
             ck(t);
-            step(true, true, TB1, t, A, B, C, I3, I1, I2);
-            step(true, true, TB1, t + 1, C, A, B, I2, I3, I1);
-            step(true, true, TB1, t + 2, B, C, A, I1, I2, I3);
+            step(true, true, TB1, t, A, B, I2, I1);
+            step(true, true, TB1, t + 1, B, A, I1, I2);
         }
-        for (; t + 2 <= xmin - 2; t += 3) {                      // every lane inside every record, row >= 2
+        for (; t + 1 <= xmin - 2; t += 2) {                      // every lane inside every record, row >= 2
             ck(t);
-            step(false, false, TB1, t, A, B, C, I3, I1, I2);
-            step(false, false, TB1, t + 1, C, A, B, I2, I3, I1);
-            step(false, false, TB1, t + 2, B, C, A, I1, I2, I3);
+            step(false, false, TB1, t, A, B, I2, I1);
+            step(false, false, TB1, t + 1, B, A, I1, I2);
         }
-        for (; t + 2 < tend; t += 3) {
+        for (; t + 1 < tend; t += 2) {
             ck(t);
-            step(false, true, TB1, t, A, B, C, I3, I1, I2);
-            step(false, true, TB1, t + 1, C, A, B, I2, I3, I1);
-            step(false, true, TB1, t + 2, B, C, A, I1, I2, I3);
+            step(false, true, TB1, t, A, B, I2, I1);
+            step(false, true, TB1, t + 1, B, A, I1, I2);
         }
-        if (t < tend) step(true, true, TB1, t, A, B, C, I3, I1, I2);
-        if (t + 1 < tend) step(true, true, TB1, t + 1, C, A, B, I2, I3, I1);
+        if (t < tend) step(true, true, TB1, t, A, B, I2, I1);
         wv_mem_sync();                            // traceback / checkpoints written by all lanes
         mark(1);
 
@@ -416,7 +419,7 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
         int t0h[2] = {1, 1};
         // MASK: some half may be at row <= 1 (it restarted at step 1)
         auto step2 = [&](const bool MASK, const int tau, uint32_t (&cur)[K], const uint32_t (&own)[K],
-                         const uint32_t (&own2)[K], uint32_t &in0, const uint32_t in1, const uint32_t in2) {
+                         uint32_t &in0, const uint32_t in1) {
             const uint32_t sN = (uint32_t)wv_shr1((int)outT), mS = (uint32_t)wv_shr1((int)outMS),
                            mL0 = (uint32_t)wv_shr1((int)outL);
             const int iA = t0h[0] + tau - gl, iB = t0h[1] + tau - gl;
@@ -429,7 +432,6 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
 #pragma unroll
             for (int s = 0; s < K; ++s) {
                 const uint32_t d0 = (s == 0) ? in1 : own[s - 1];
-                const uint32_t u2 = (s == 0) ? in2 : own2[s - 1];
                 const uint32_t tl = (s == 0) ? sN : cur[s - 1];
                 const uint32_t sc = wv_perm(NW16_TBL_HI, NW16_TBL_LO, xsel ^ yreg[s]);
                 const uint32_t up = MASK ? wv_bfi(r1, NBIG, u0[s]) : u0[s];
@@ -438,12 +440,13 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
                 if (s == 0) v = leadc0 ? sc : v;
                 cur[s] = MASK ? wv_bfi(pm, own[s], v) : v;
                 const uint32_t P2 = wv_perm(pk_sub(l0, up), pk_sub(d0, lu), 0x0B0A0908u);
-                const uint32_t mU = pk_neg_mask(pk_sub(mcS[s], u2));
-                const uint32_t u0n = wv_bfi(mU, pk_add(u2, IG2E), pk_add(u0[s], EG));
+                const uint32_t mU = pk_neg_mask(pk_sub(mcS[s], dI[s]));
+                const uint32_t u0n = pk_add(wv_bfi(mU, dI[s], u0[s]), EG);
                 u0[s] = MASK ? wv_bfi(r1, u0[s], u0n) : u0n;
-                mcS[s] = pk_max(mcS[s], u2);
+                mcS[s] = wv_bfi(mU, dI[s], mcS[s]);
                 const uint32_t mnL = pk_neg_mask(pk_sub(tl, mfS));
-                l0 = wv_bfi(mnL, pk_add(l0, EG), pk_add(d0, IGE));
+                dI[s] = pk_add(d0, IGE);
+                l0 = wv_bfi(mnL, pk_add(l0, EG), dI[s]);
                 mfS = wv_bfi(mnL, mfS, d0);
                 if (s == 0) { mfS = leadc0 ? NBIG : mfS; l0 = leadc0 ? NBIG : l0; }
                 if (s < 8) {
@@ -477,11 +480,11 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
                 auto ld = [&](const int r) { return wv_bfi(0x0000FFFFu, pa[r * 64], pb[r * 64]); };
 #pragma unroll
                 for (int s = 0; s < K; ++s) {
-                    A[s] = ld(s); B[s] = ld(K + s); C[s] = ld(2 * K + s);
+                    A[s] = ld(s); B[s] = ld(K + s); dI[s] = ld(2 * K + s);
                     mcS[s] = ld(3 * K + s); u0[s] = ld(4 * K + s);
                 }
-                I1 = ld(5 * K); I2 = ld(5 * K + 1); I3 = ld(5 * K + 2);
-                outT = ld(5 * K + 3); outMS = ld(5 * K + 4); outL = ld(5 * K + 5);
+                I1 = ld(5 * K); I2 = ld(5 * K + 1);
+                outT = ld(5 * K + 2); outMS = ld(5 * K + 3); outL = ld(5 * K + 4);
                 xrow = (X8[min(max(t0h[0] - gl, 0), xcl)] & 3u) | (X8[min(max(t0h[1] - gl, 0), xcl)] & 0xCu);
             }
             // rows <= 1 need the masked step: while tau <= G - min(t0h) (wave-uniform bound)
@@ -490,18 +493,15 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
             for (int o = 32; o > 0; o >>= 1) tmin = min(tmin, wv_shfl_xor(tmin, o));
             const int tau_m = G + 1 - tmin;          // rows t0h + tau - gl > 1 for every lane from here on
             int tau = 0;
-            for (; tau + 2 < n2 && tau < tau_m; tau += 3) {
-                step2(true, tau, A, B, C, I3, I1, I2);
-                step2(true, tau + 1, C, A, B, I2, I3, I1);
-                step2(true, tau + 2, B, C, A, I1, I2, I3);
+            for (; tau + 1 < n2 && tau < tau_m; tau += 2) {
+                step2(true, tau, A, B, I2, I1);
+                step2(true, tau + 1, B, A, I1, I2);
             }
-            for (; tau + 2 < n2; tau += 3) {
-                step2(false, tau, A, B, C, I3, I1, I2);
-                step2(false, tau + 1, C, A, B, I2, I3, I1);
-                step2(false, tau + 2, B, C, A, I1, I2, I3);
+            for (; tau + 1 < n2; tau += 2) {
+                step2(false, tau, A, B, I2, I1);
+                step2(false, tau + 1, B, A, I1, I2);
             }
-            if (tau < n2) step2(true, tau, A, B, C, I3, I1, I2);
-            if (tau + 1 < n2) step2(true, tau + 1, C, A, B, I2, I3, I1);
+            if (tau < n2) step2(true, tau, A, B, I2, I1);
             wv_mem_sync();                        // band traceback written by all lanes, read by the walkers
             mark(3);
             for (int h = 0; h < 2; ++h) {
