@@ -106,6 +106,9 @@ def parse():
                     help="HIP device of this rank (default LOCAL_RANK; a fixed value rehearses N ranks on one card)")
     ap.add_argument("--shard", default=None, metavar="R/N",
                     help="diagnostic: on one GPU, time only rank R's shard of an N-GPU strong-scaling run")
+    ap.add_argument("--upload", choices=("async", "sync"), default="async",
+                    help="query H2D per step: queued in parts that each lane waits for (async) or waited for "
+                         "before the alignment (sync); inside the timed step either way")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "nw_traffic.json"))
     ap.add_argument("--valu-json", default=os.path.join(REPO, "profiles", "nw_valu.json"))
     a = ap.parse_args()
@@ -191,7 +194,9 @@ def main():
     def step():
         nonlocal n_slices
         t = time.perf_counter()
-        dev.set_query(qp, qs, lo, hi)                   # H2D of this rank's shard: inside the step
+        # H2D of this rank's shard, inside the step: queued in parts, each lane
+        # of the alignment starts when its reads are in HBM (--upload async)
+        dev.set_query(qp, qs, lo, hi, wait=a.upload == "sync")
         h2d.append(time.perf_counter() - t)
         if a.slice_bases:
             res, paths, st, n_slices = dev.align_sliced(ref, rst, a.slice_bases, n_threads=a.n_threads,
@@ -258,11 +263,18 @@ def main():
         except Exception:
             traffic = None
     cells_per_s = cells / (nw_busy / 1e3) if nw_busy else 0.0
+    # launches of the dominant kernel alone (imsame_stats.launch_pk: packed
+    # nw16_kernel vs the int32 nw_kernel that takes the small last launches),
+    # the average rocprofv3 --stats reports for that kernel name
+    pk_ms = [m for s_ in stats for j, m in enumerate(s_["launch_ms"])
+             if ((s_["launch_pk"] >> j) & 1) == (1 if kernel == "nw16_kernel" else 0)]
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "traffic_over_alg": round(traffic / per_launch, 4) if traffic and per_launch else None,
                 "kernel": kernel, "launches": nw_launches,
                 "avg_launch_ms": round(nw_ms / max(nw_launches, 1), 4),
+                "kernel_launches": len(pk_ms),
+                "kernel_avg_launch_ms": round(sum(pk_ms) / max(len(pk_ms), 1), 4),
                 "nw_busy_ms_per_step": round(nw_busy / a.steps, 3),
                 "launch_overlap": round(nw_ms / nw_busy, 3) if nw_busy else None,
                 "alg_bytes_per_launch": int(per_launch),
@@ -302,9 +314,10 @@ def main():
             "detail": {"accepted_reads": accepted_all, "index_build_s": round(t_index, 3),
                        "rounds": last["rounds"], "nw_per_read": round(last["n_nw"] / max(hi - lo, 1), 4),
                        "hits_per_read": round(last["n_hits"] / max(hi - lo, 1), 2),
-                       "ms_h2d_query": round(1e3 * sum(h2d) / max(len(h2d), 1), 3),
+                       "ms_h2d_query": round(1e3 * sum(h2d) / max(len(h2d), 1), 3), "upload": a.upload,
                        "nw_cells": last["nw_cells"], "n_nw": last["n_nw"],
                        "lanes": last["lanes"], "nw_redo_waves": last.get("nw_redo"),
+                       "nw_window_walks": last.get("nw_win"),
                        "ms_seed": round(last["ms_seed"], 3), "ms_nw": round(last["ms_nw"], 3),
                        "ms_nw_busy": round(last["ms_nw_busy"], 3),
                        "ms_align_call": round(last["ms_total"], 3),

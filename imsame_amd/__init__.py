@@ -61,6 +61,8 @@ def lib():
         L.imsame_dev_index.argtypes = [vp, vp, u64, vp, u64, vp]
         L.imsame_dev_set_query.argtypes = [vp, vp, u64, vp, u64]
         L.imsame_dev_set_query_range.argtypes = [vp, vp, u64, vp, u64, u64, u64]
+        L.imsame_dev_set_query_range_async.argtypes = [vp, vp, u64, vp, u64, u64, u64]
+        L.imsame_dev_sync.argtypes = [vp]
         L.imsame_dev_fetch_paths.argtypes = [vp, vp, u64, C.POINTER(u64)]
         L.imsame_host_alloc.restype = vp
         L.imsame_host_alloc.argtypes = [u64]
@@ -187,19 +189,28 @@ class Device:
         if rc:
             raise ImsameError(rc, "imsame_dev_index")
 
-    def set_query(self, q_seq, q_starts, read_from=None, read_to=None):
+    def set_query(self, q_seq, q_starts, read_from=None, read_to=None, wait=True):
         """Upload the query; with read_from/read_to only that shard's reads
         go to HBM (imsame_dev_set_query_range; chunk heads stay the whole
-        query's)."""
+        query's).  wait=False queues the copies (imsame_dev_set_query_range_async):
+        the next align's lanes start as their reads arrive; the arrays must
+        be page-locked (PinnedArray) and stay unchanged until that call."""
         q_seq, q_starts = _arr(q_seq, np.uint8), _arr(q_starts, np.uint64)
         a = 0 if read_from is None else read_from
         b = len(q_starts) if read_to is None else read_to
-        rc = lib().imsame_dev_set_query_range(self._h, q_seq.ctypes.data, len(q_seq), q_starts.ctypes.data,
-                                              len(q_starts), a, b)
+        fn = lib().imsame_dev_set_query_range if wait else lib().imsame_dev_set_query_range_async
+        rc = fn(self._h, q_seq.ctypes.data, len(q_seq), q_starts.ctypes.data, len(q_starts), a, b)
         if rc:
             raise ImsameError(rc, "imsame_dev_set_query_range")
         self.n_q = len(q_starts)
         self.q_range = (a, b)
+        self._q_keep = None if wait else (q_seq, q_starts)   # alive until the copies are done
+
+    def sync(self):
+        """Wait for queued work (an asynchronous query upload)."""
+        rc = lib().imsame_dev_sync(self._h)
+        if rc:
+            raise ImsameError(rc, "imsame_dev_sync")
 
     def fetch_paths(self, cap):
         """Paths of the last align call (after IMSAME_E_PATHS)."""

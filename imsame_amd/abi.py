@@ -75,13 +75,14 @@ class Stats(C.Structure):
         ("launch_cand", C.c_uint64 * LAUNCH_STATS), ("launch_ms", C.c_double * LAUNCH_STATS),
         ("n_rewalk", C.c_uint64), ("ms_setup", C.c_double), ("ms_d2h", C.c_double),
         ("ms_nw_busy", C.c_double), ("lanes", C.c_uint64), ("nw_redo", C.c_uint64),
+        ("launch_pk", C.c_uint64), ("nw_win", C.c_uint64),
     ]
 
     def as_dict(self):
         d = {}
         for k, _ in self._fields_:
             v = getattr(self, k)
-            d[k] = list(v) if k.startswith("launch_") else v
+            d[k] = list(v) if k in ("launch_cand", "launch_ms") else v
         k = min(self.nw_launches, LAUNCH_STATS)
         d["launch_cand"], d["launch_ms"] = d["launch_cand"][:k], d["launch_ms"][:k]
         return d

@@ -170,6 +170,41 @@ __global__ void scan_add(T *out, const T *bpre, uint64_t n) {
 }
 
 // ---------------------------------------------------------------------------
+// Launch order of a packed NW queue: candidates by the predicted first row of
+// their read (SeedLaunch::crow) in 8-row buckets, unpredicted ones last, so
+// the candidates a wave takes share one traceback window (nw16_kernel.hip).
+// Counting sort: histogram, one-block exclusive scan, scatter.
+__device__ __forceinline__ uint32_t row_bucket(int32_t r, uint32_t nb) {
+    if (r == INT32_MIN) return nb - 1;
+    const int64_t b = ((int64_t)r + 256) >> 3;
+    return (uint32_t)(b < 0 ? 0 : b > (int64_t)nb - 2 ? (int64_t)nb - 2 : b);
+}
+__global__ void row_hist_kernel(const int32_t *row, uint32_t n, uint32_t nb, uint32_t *hist) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) atomicAdd(&hist[row_bucket(row[i], nb)], 1u);
+}
+__global__ __launch_bounds__(1024) void row_scan_kernel(const uint32_t *hist, uint32_t nb, uint32_t *cur) {
+    __shared__ uint32_t sm[1024];
+    const uint32_t t = threadIdx.x, per = (nb + 1023) / 1024, a = t * per;
+    uint32_t sum = 0;
+    for (uint32_t k = 0; k < per; ++k) if (a + k < nb) sum += hist[a + k];
+    sm[t] = sum;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024; o <<= 1) {
+        const uint32_t v = t >= o ? sm[t - o] : 0u;
+        __syncthreads();
+        sm[t] += v;
+        __syncthreads();
+    }
+    uint32_t run = sm[t] - sum;
+    for (uint32_t k = 0; k < per; ++k) if (a + k < nb) { cur[a + k] = run; run += hist[a + k]; }
+}
+__global__ void row_scatter_kernel(const int32_t *row, uint32_t n, uint32_t nb, uint32_t *cur, uint32_t *perm) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) perm[atomicAdd(&cur[row_bucket(row[i], nb)], 1u)] = i;
+}
+
+// ---------------------------------------------------------------------------
 // reverse complement (replaces reverseComplement.c:21-118)
 // ---------------------------------------------------------------------------
 #include "revcomp_kernel.hip"
@@ -211,11 +246,17 @@ struct imsame_ctx {
     std::vector<uint64_t> h_q_start;  // starts of reads q_lo .. q_hi
     const uint64_t *hq = nullptr;     // = h_q_start.data(), or the parent's for a lane
     bool have_query = false;
+    // the upload in parts (imsame_dev_set_query_range_async): part k holds the
+    // bases below q_part_end[k] and is complete when q_part_ev[k] fires (the
+    // starts go first, with part 0); a lane borrows its parent's events
+    std::vector<hipEvent_t> q_part_ev;
+    std::vector<uint64_t> q_part_end;
     bool q_len_mult = false;         // every read length is a multiple of NW16_K
     // per-read state
     DBuf res, cur_p, cur_h, memo, nmemo, rstat, act0, act1, cbase, ccnt, perr;
     // candidates
     DBuf cread, csid, cread2, csid2, cout, cout2;
+    DBuf crow, cperm, rhist;          // predicted rows of class-0 candidates, their launch order
     // scalars (one block of u64 counters)
     DBuf ctr;
     // tables (and the inputs they were built for)
@@ -261,7 +302,7 @@ static inline const uint64_t *dev_qs(const imsame_ctx *c) {
 
 // counters block layout (u64 slots)
 enum { C_NCAND = 0, C_NCAND2, C_NNEXT, C_WORK, C_WORK2, C_PATHS, C_FLAGS, C_ERR, C_HITS, C_CELLS, C_NACC, C_REDO,
-       C_PROF, C_NSLOTS = C_PROF + 5 };
+       C_PROF, C_WIN = C_PROF + 5, C_NSLOTS };
 
 static double now_ms() {
     struct timespec ts; clock_gettime(CLOCK_MONOTONIC, &ts);
@@ -316,6 +357,7 @@ extern "C" int imsame_dev_open(int device, imsame_ctx **out) {
 static void lane_unalias(imsame_ctx *l) {
     DBuf *al[] = {&l->db, &l->db_start, &l->off, &l->ent, &l->q, &l->q_start};
     for (DBuf *b : al) { b->p = nullptr; b->cap = 0; }
+    l->q_part_ev.clear(); l->q_part_end.clear();
 }
 
 extern "C" void imsame_dev_close(imsame_ctx *c) {
@@ -328,11 +370,14 @@ extern "C" void imsame_dev_close(imsame_ctx *c) {
                     &c->q_start, &c->res, &c->cur_p, &c->cur_h, &c->memo, &c->nmemo, &c->rstat, &c->act0,
                     &c->act1, &c->cread, &c->csid, &c->cread2, &c->csid2, &c->cout, &c->cout2, &c->ctr,
                     &c->minraw, &c->minlen, &c->minident, &c->tb, &c->bnd, &c->paths, &c->ck, &c->rc_in, &c->rc_out,
-                    &c->rc_a, &c->rc_b, &c->rc_c, &c->cbase, &c->ccnt, &c->perr, &c->wcap, &c->wout, &c->wstart};
+                    &c->rc_a, &c->rc_b, &c->rc_c, &c->cbase, &c->ccnt, &c->perr, &c->wcap, &c->wout, &c->wstart,
+                    &c->crow, &c->cperm, &c->rhist};
     for (DBuf *b : bufs) b->release();
     (void)hipEventDestroy(c->ev0);
     (void)hipEventDestroy(c->ev1);
     if (c->origin && !c->is_sub) (void)hipEventDestroy(c->origin);     // a lane borrows its parent's
+    if (!c->is_sub)
+        for (hipEvent_t e : c->q_part_ev) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -352,6 +397,7 @@ static int lane_sub(imsame_ctx *c, int k, imsame_ctx **out) {
     l->have_index = c->have_index;
     l->n_q = c->n_q; l->q_len = c->q_len; l->q_lo = c->q_lo; l->q_hi = c->q_hi; l->q_base = c->q_base;
     l->q_lo_first = c->q_lo_first; l->hq = c->hq; l->have_query = c->have_query; l->q_len_mult = c->q_len_mult;
+    l->q_part_ev = c->q_part_ev; l->q_part_end = c->q_part_end;
     l->ev_db_len = 0; l->use_wcap = l->use_wstart = false;
     *out = l;
     return 0;
@@ -462,12 +508,17 @@ extern "C" int imsame_dev_index(imsame_ctx *c, const uint8_t *db_seq, uint64_t d
     return IMSAME_OK;
 }
 
-extern "C" int imsame_dev_set_query_range(imsame_ctx *c, const uint8_t *q_seq, uint64_t q_len,
-                                          const uint64_t *q_start, uint64_t n_q, uint64_t read_from,
-                                          uint64_t read_to) {
-    if (!c || (q_len && !q_seq) || (n_q && !q_start) || read_from > read_to || read_to > n_q) return IMSAME_E_ARG;
+// parts of an asynchronous query upload (each a few tens of MB at C2)
+#define Q_PARTS 8
+
+extern "C" int imsame_dev_set_query_range_async(imsame_ctx *c, const uint8_t *q_seq, uint64_t q_len,
+                                                const uint64_t *q_start, uint64_t n_q, uint64_t read_from,
+                                                uint64_t read_to) {
+    if (!c || c->is_sub || (q_len && !q_seq) || (n_q && !q_start) || read_from > read_to || read_to > n_q)
+        return IMSAME_E_ARG;
     if (n_q >= 0xFFFFFFF0ull) return IMSAME_E_ARG;
     HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));     // a previous upload may still read h_q_start / fill q
     c->have_query = false;
     auto qs = [&](uint64_t r) { return r < n_q ? q_start[r] : q_len; };
     for (uint64_t r = read_from; r < read_to; ++r)
@@ -486,12 +537,48 @@ extern "C" int imsame_dev_set_query_range(imsame_ctx *c, const uint8_t *q_seq, u
     c->q_len_mult = true;
     for (uint64_t r = read_from; r < read_to; ++r) c->q_len_mult = c->q_len_mult && (qs(r + 1) - qs(r)) % NW16_K == 0;
     if (c->q.ensure(nb + 64) || c->q_start.ensure(ns * 8)) return IMSAME_E_OOM;
-    if (nb) HIPCHK(hipMemcpyAsync(c->q.p, q_seq + c->q_base, nb, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemsetAsync((uint8_t *)c->q.p + nb, 0, 64, c->stream));
+    while (c->q_part_ev.size() < Q_PARTS) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        c->q_part_ev.push_back(e);
+    }
+    c->q_part_end.assign(Q_PARTS, 0);
     HIPCHK(hipMemcpyAsync(c->q_start.p, c->h_q_start.data(), ns * 8, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipMemsetAsync((uint8_t *)c->q.p + nb, 0, 64, c->stream));
+    for (uint64_t k = 0, a = 0; k < Q_PARTS; ++k) {      // bases [q_base + a, q_base + b)
+        const uint64_t b = nb * (k + 1) / Q_PARTS;
+        if (b > a) HIPCHK(hipMemcpyAsync((uint8_t *)c->q.p + a, q_seq + c->q_base + a, b - a, hipMemcpyHostToDevice,
+                                         c->stream));
+        HIPCHK(hipEventRecord(c->q_part_ev[k], c->stream));
+        c->q_part_end[k] = c->q_base + b;
+        a = b;
+    }
     c->have_query = true;
     return IMSAME_OK;
+}
+
+// stream s waits until the uploaded bases below `end` are in HBM
+static int query_wait(imsame_ctx *c, hipStream_t s, uint64_t end) {
+    for (size_t k = 0; k < c->q_part_end.size(); ++k)
+        if (k + 1 == c->q_part_end.size() || c->q_part_end[k] >= end) {
+            HIPCHK(hipStreamWaitEvent(s, c->q_part_ev[k], 0));
+            break;
+        }
+    return 0;
+}
+
+extern "C" int imsame_dev_sync(imsame_ctx *c) {
+    if (!c) return IMSAME_E_ARG;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return IMSAME_OK;
+}
+
+extern "C" int imsame_dev_set_query_range(imsame_ctx *c, const uint8_t *q_seq, uint64_t q_len,
+                                          const uint64_t *q_start, uint64_t n_q, uint64_t read_from,
+                                          uint64_t read_to) {
+    const int rc = imsame_dev_set_query_range_async(c, q_seq, q_len, q_start, n_q, read_from, read_to);
+    return rc ? rc : imsame_dev_sync(c);
 }
 
 extern "C" int imsame_dev_set_query(imsame_ctx *c, const uint8_t *q_seq, uint64_t q_len, const uint64_t *q_start,
@@ -604,7 +691,7 @@ static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, 
 static int launch_nw(imsame_ctx *c, NwPlan pl, const uint32_t *cread, const uint32_t *csid, uint32_t n,
                      imsame_read_result *outp, int64_t ig, int64_t eg, const imsame_params *p, uint32_t ymax,
                      uint32_t xmax, uint32_t *work, const uint8_t *dbp, const uint64_t *dbs, const uint8_t *qp,
-                     const uint64_t *qs, uint32_t paths_cap, double *ms) {
+                     const uint64_t *qs, uint32_t paths_cap, double *ms, const int32_t *crow = nullptr) {
     hipStream_t s = c->stream;
     const uint64_t tb_dw = pl.tb_dw;
     // fewer resident waves if the arena cannot be had (the queue still drains)
@@ -635,10 +722,24 @@ static int launch_nw(imsame_ctx *c, NwPlan pl, const uint32_t *cread, const uint
     P.paths_used = (uint32_t *)(ctr + C_PATHS); P.want_paths = p->want_paths;
     P.flags = (uint32_t *)(ctr + C_FLAGS);
     P.ck = pl.two ? c->ck.as<uint32_t>() : nullptr; P.ck_wave_dw = pl.ck_dw;
-    P.band_w = pl.band_w; P.redo = (uint32_t *)(ctr + C_REDO);
+    P.band_w = pl.band_w; P.redo = (uint32_t *)(ctr + C_REDO); P.win = (uint32_t *)(ctr + C_WIN);
     P.prof = getenv("IMSAME_NW_PROF") ? (unsigned long long *)(ctr + C_PROF) : nullptr;
     HIPCHK(hipMemsetAsync(work, 0, 4, s));
-    HIPCHK(hipEventRecord(c->ev0, s));
+    HIPCHK(hipEventRecord(c->ev0, s));           // the launch's time includes its ordering
+    if (crow && pl.two && n >= 64) {
+        // queue order by predicted row (first-sweep traceback windows)
+        const uint32_t nb = ((uint32_t)pl.xcap + 512) / 8 + 2;
+        if (c->cperm.ensure((uint64_t)n * 4) || c->rhist.ensure((uint64_t)nb * 8)) return IMSAME_E_OOM;
+        uint32_t *hist = c->rhist.as<uint32_t>(), *cur = hist + nb;
+        HIPCHK(hipMemsetAsync(hist, 0, (size_t)nb * 4, s));
+        row_hist_kernel<<<nblk(n, 256), 256, 0, s>>>(crow, n, nb, hist);
+        row_scan_kernel<<<1, 1024, 0, s>>>(hist, nb, cur);
+        row_scatter_kernel<<<nblk(n, 256), 256, 0, s>>>(crow, n, nb, cur, c->cperm.as<uint32_t>());
+        HIPCHK(hipGetLastError());
+        P.perm = c->cperm.as<uint32_t>(); P.cand_row = crow;
+        const char *wu = getenv("IMSAME_NW_WIN_UP"), *wd = getenv("IMSAME_NW_WIN_DOWN");
+        P.win_up = wu ? atoi(wu) : NW16_WIN_UP; P.win_down = wd ? atoi(wd) : NW16_WIN_DOWN;
+    }
     if (pl.two && pl.last4)     nw16_kernel<true, true><<<pl.blocks, 256, pl.lds, s>>>(P);
     else if (pl.two)            nw16_kernel<false, true><<<pl.blocks, 256, pl.lds, s>>>(P);
     else if (pl.pk && pl.last4) nw16_kernel<true, false><<<pl.blocks, 256, pl.lds, s>>>(P);
@@ -750,6 +851,8 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     const uint32_t n = (uint32_t)(read_to - read_from);
+    // this lane's bases (and the 16-byte chunk loads' reach past its last read)
+    if (int rq = query_wait(c, s, hqs(c, read_to) + 64)) return rq;
     imsame_stats st;
     memset(&st, 0, sizeof st);
     st.n_reads = n;
@@ -778,8 +881,12 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         c->act0.ensure((uint64_t)n * 4) || c->act1.ensure((uint64_t)n * 4) || c->cread.ensure((uint64_t)n * 4) ||
         c->csid.ensure((uint64_t)n * 4) || c->cread2.ensure((uint64_t)n * 4) || c->csid2.ensure((uint64_t)n * 4) ||
         c->cout.ensure((uint64_t)n * 64) || c->cout2.ensure((uint64_t)n * 64) || c->cbase.ensure((uint64_t)n * 4) ||
-        c->ccnt.ensure((uint64_t)n * 4) || c->perr.ensure((uint64_t)n * 4))
+        c->ccnt.ensure((uint64_t)n * 4) || c->perr.ensure((uint64_t)n * 4) || c->crow.ensure((uint64_t)n * 4))
         return IMSAME_E_OOM;
+    // predicted rows for the packed kernel's first-sweep traceback windows
+    // (IMSAME_NW_WINDOW=0: off, every traceback from the second sweep)
+    const char *win_env = getenv("IMSAME_NW_WINDOW");
+    int32_t *crow = (win_env && !atoi(win_env)) ? nullptr : c->crow.as<int32_t>();
     // speculation: round 1 emits one candidate per read (most reads accept
     // it); later rounds emit up to SPEC_MAX, bounded by the candidate buffers
     const char *spec_env = getenv("IMSAME_SPEC");
@@ -822,6 +929,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         S.next = nxt; S.nnext = (uint32_t *)(ctr + C_NNEXT);
         S.cbase = c->cbase.as<uint32_t>(); S.ccnt = c->ccnt.as<uint32_t>(); S.perr = c->perr.as<uint32_t>();
         S.cread = c->cread.as<uint32_t>(); S.csid = c->csid.as<uint32_t>(); S.ncand = (uint32_t *)(ctr + C_NCAND);
+        S.crow = crow;
         S.cread2 = c->cread2.as<uint32_t>(); S.csid2 = c->csid2.as<uint32_t>(); S.ncand2 = (uint32_t *)(ctr + C_NCAND2);
         S.err = (unsigned long long *)(ctr + C_ERR); S.nhits = (unsigned long long *)(ctr + C_HITS);
         S.wcap = c->use_wcap ? c->wcap.as<uint64_t>() : nullptr;
@@ -856,11 +964,12 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
             double ms = 0;
             rc = launch_nw(c, pl, cls[k].cr, cls[k].cs, cls[k].n, cls[k].o, p->igap, p->egap, p, ymax, xcap,
                            (uint32_t *)(ctr + cls[k].work), c->db.as<uint8_t>(), c->db_start.as<uint64_t>(), qd, qsd,
-                           pcap, &ms);
+                           pcap, &ms, k == 0 ? crow : nullptr);
             if (rc) return rc;
             if (st.nw_launches < IMSAME_LAUNCH_STATS) {
                 st.launch_cand[st.nw_launches] = cls[k].n;
                 st.launch_ms[st.nw_launches] = ms;
+                if (pl.pk) st.launch_pk |= 1ull << st.nw_launches;
             }
             st.ms_nw += ms; st.nw_launches++; st.n_nw += cls[k].n;
             UpdLaunch U = {cls[k].cr, cls[k].cs, cls[k].n, cls[k].o, read_from, c->res.as<imsame_read_result>(),
@@ -903,6 +1012,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     st.nw_cells = hc[C_CELLS];
     st.n_accepted = hc[C_NACC];
     st.nw_redo = (uint32_t)hc[C_REDO];
+    st.nw_win = (uint32_t)hc[C_WIN];
     if (getenv("IMSAME_NW_PROF")) {           // diagnostics: nw16 phase cycles (summed over waves)
         const double tot = (double)(hc[C_PROF] + hc[C_PROF + 1] + hc[C_PROF + 2] + hc[C_PROF + 3] + hc[C_PROF + 4]);
         fprintf(stderr, "[nwprof] setup %.3f sweep1 %.3f reduce %.3f sweep2 %.3f walk %.3f (fractions of %.4g wave-cycles)\n",
@@ -1022,7 +1132,7 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
     }
     imsame_stats st = S[0];
     std::vector<std::pair<float, float>> iv = c->nw_iv;
-    st.nw_launches = 0;
+    st.nw_launches = 0; st.launch_pk = 0;
     for (int k = 0; k < nl; ++k) {
         const imsame_stats &x = S[k];
         if (k) {
@@ -1030,13 +1140,14 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
             st.n_hits += x.n_hits; st.rounds = std::max(st.rounds, x.rounds);
             if (x.err_read < st.err_read) { st.err_read = x.err_read; st.err_dbseq = x.err_dbseq; }
             st.ms_seed += x.ms_seed; st.ms_nw += x.ms_nw; st.nw_bytes += x.nw_bytes; st.n_rewalk += x.n_rewalk;
-            st.nw_redo += x.nw_redo;
+            st.nw_redo += x.nw_redo; st.nw_win += x.nw_win;
             st.ms_setup = std::max(st.ms_setup, x.ms_setup); st.ms_d2h += x.ms_d2h;
             iv.insert(iv.end(), L[k]->nw_iv.begin(), L[k]->nw_iv.end());
         }
         for (uint64_t j = 0; j < std::min<uint64_t>(x.nw_launches, IMSAME_LAUNCH_STATS); ++j) {
             if (st.nw_launches + j >= IMSAME_LAUNCH_STATS) break;
             st.launch_cand[st.nw_launches + j] = x.launch_cand[j]; st.launch_ms[st.nw_launches + j] = x.launch_ms[j];
+            if ((x.launch_pk >> j) & 1) st.launch_pk |= 1ull << (st.nw_launches + j);
         }
         st.nw_launches += x.nw_launches;
     }

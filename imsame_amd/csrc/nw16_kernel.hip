@@ -54,6 +54,17 @@
 // the first sweep issues ~190 VALU per step instead of 250, and ~90 % of the
 // steps are first-sweep steps at C2 (2000-row records, 150-column reads).
 //
+// Predicted window (P.cand_row): the seed hit that made a candidate puts the
+// read's first base on record row cand_row, so an accepted read's path runs
+// over rows ~[cand_row, cand_row + ylen) and its best cell sits at the bottom
+// of them.  The host orders the queue by that row (P.perm), so a wave's eight
+// candidates predict nearly the same rows, and the FIRST sweep writes the
+// traceback of the union of their windows (~230 of ~2000 steps, at the
+// one-pass cost per step).  A half whose best cell lies inside the window
+// walks it directly (TbAcc16 bounds [t0, t1)); a half whose best cell is
+// elsewhere or whose walk leaves the window falls back to the second sweep
+// above.  Same DP values either way, so the same bits.
+//
 // Range: scores are int16.  The host picks this kernel only when every value
 // of the launch (including the garbage rows/columns a lockstep group computes
 // past a shorter candidate, which are DP values of an extended problem) stays
@@ -64,6 +75,10 @@
 #define NW16_BIG 16384
 #define NW16_CK  24               // checkpoint interval of the first sweep (steps, even: the rotation period)
 #define NW16_NST (5 * NW16_K + 5) // dwords of wave state per lane in a checkpoint
+#define NW16_NOROW INT32_MIN      // cand_row: no prediction
+#define NW16_WIN_UP 32            // window rows above the predicted first row
+#define NW16_WIN_DOWN 24          // ... and below the predicted last row
+#define NW16_WIN_MAX 448          // longest window (steps) a wave writes in its first sweep
 
 // does the launch fit the int16 path?  (all gap terms non-positive)
 __host__ static inline bool nw16_fits(int64_t ig, int64_t eg, uint64_t xcap, uint64_t ymax) {
@@ -93,7 +108,8 @@ WV_DEVICE uint32_t base_code(uint8_t b) { return (b >> 1) & 3u; }          // A0
 // two passes: the half's restart step, cells before it were not written)
 struct TbAcc16 {
     const uint32_t *tb; const uint8_t *X; const uint8_t *Y; int g, G, h, t0;
-    __device__ bool has(int i, int j) const { return i + j / NW16_K >= t0; }
+    int t1 = INT_MAX;                      // steps [t0, t1) were written
+    __device__ bool has(int i, int j) const { const int t = i + j / NW16_K; return t >= t0 && t < t1; }
     __device__ uint32_t nib(int i, int j) const {
         const int l = j / NW16_K, s = j - l * NW16_K;
         const uint32_t *w = tb + ((uint32_t)(i + l - t0) * 64u + (uint32_t)(g * G + l)) * 3u;
@@ -145,13 +161,18 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
         // candidates of the two halves; an absent B repeats A (never written)
         bool valid[2];
         uint32_t cidx[2], sid[2] = {0, 0};
-        int xl[2] = {0, 0}, yl[2] = {0, 0};
+        int xl[2] = {0, 0}, yl[2] = {0, 0}, prow[2] = {NW16_NOROW, NW16_NOROW};
         const uint8_t *Yp[2] = {P.q, P.q}, *Xg[2] = {P.db, P.db};
         for (int h = 0; h < 2; ++h) {
-            cidx[h] = base + 2 * g + h;
+            cidx[h] = base + 2 * g + h;                                   // queue slot
             valid[h] = in_group && cidx[h] < P.n_cand;
-            const uint32_t c = valid[h] ? cidx[h] : cidx[0];
+        }
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t w = valid[h] ? cidx[h] : cidx[0];
             if (valid[0]) {
+                const uint32_t c = P.perm ? P.perm[w] : w;                // candidate
+                cidx[h] = c;
+                if (P.cand_row) prow[h] = P.cand_row[c];
                 const uint32_t rd = P.cand_read[c];
                 sid[h] = P.cand_sid[c];
                 const uint64_t xo = P.db_start[sid[h]];
@@ -201,6 +222,31 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
             xmax = max(xmax, wv_shfl_xor(xmax, o));
             xmin = min(xmin, wv_shfl_xor(xmin, o));
         }
+        // traceback window of the first sweep: steps [tw0, tw1), both odd (the
+        // loops advance t by 2 from 1); rows [lo, hi] of every candidate's
+        // prediction take steps lo .. hi + G - 1
+        int tw0 = INT_MAX - 2, tw1 = INT_MAX - 2;    // none: every step before "the window"
+        if (TWO && P.cand_row) {
+            int lo = INT_MAX, hi = INT_MIN, none = 0;
+            for (int h = 0; h < 2; ++h) {
+                if (!valid[h]) continue;
+                if (prow[h] == NW16_NOROW) { none = 1; continue; }
+                lo = min(lo, prow[h] - P.win_up);
+                hi = max(hi, prow[h] + yl[h] - 1 + P.win_down);
+            }
+            for (int o = 32; o > 0; o >>= 1) {
+                lo = min(lo, wv_shfl_xor(lo, o));
+                hi = max(hi, wv_shfl_xor(hi, o));
+                none = max(none, wv_shfl_xor(none, o));
+            }
+            if (!none && lo <= hi) {
+                int a = max(lo, 1), b = min(hi, xmax) + G;
+                a -= (a & 1) ^ 1; b += (b & 1) ^ 1;
+                if (b > a && b - a <= NW16_WIN_MAX) { tw0 = a; tw1 = b; }
+            }
+            tw0 = (int)wv_first((uint32_t)tw0); tw1 = (int)wv_first((uint32_t)tw1);   // wave-uniform (SGPRs)
+        }
+        const int tb0 = TWO ? tw0 : 0;             // step of traceback record 0
 
         // ------------------------------------------------------------ sweep
         const int j0 = gl * K;
@@ -311,7 +357,7 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
             // rows outside [1, xlen) are never read; 32-bit byte offset from the
             // wave-uniform slot base (global_store saddr form)
             if (TB) {
-                uint32_t *rec = (uint32_t *)(tb3 + ((uint32_t)t * 768u + (uint32_t)lane * 12u));
+                uint32_t *rec = (uint32_t *)(tb3 + ((uint32_t)(t - tb0) * 768u + (uint32_t)lane * 12u));
                 rec[0] = wm; rec[1] = wu; rec[2] = wx;
             }
             // last column (rows 1 .. xlen-2) and last row (:481-484)
@@ -359,23 +405,48 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
         mark(0);
         // (cur, own) and (in0, in1) swap every step; every loop advances t by 2
         // so the phase carries over
+        // (two-pass: steps inside the window write their traceback; t is odd
+        // here, so a pair is inside or outside the window as a whole)
+        auto inwin = [&](const int tt) { return TWO && tt >= tw0 && tt < tw1; };
         int t = 1;
         for (; t + 1 < tend && t <= G + 1; t += 2) {             // skewed start: lanes may be at row <= 1
             ck(t);
-            step(true, true, TB1, t, A, B, I2, I1);
-            step(true, true, TB1, t + 1, B, A, I1, I2);
+            if (inwin(t)) {
+                step(true, true, true, t, A, B, I2, I1);
+                step(true, true, true, t + 1, B, A, I1, I2);
+            } else {
+                step(true, true, TB1, t, A, B, I2, I1);
+                step(true, true, TB1, t + 1, B, A, I1, I2);
+            }
         }
-        for (; t + 1 <= xmin - 2; t += 2) {                      // every lane inside every record, row >= 2
-            ck(t);
-            step(false, false, TB1, t, A, B, I2, I1);
-            step(false, false, TB1, t + 1, B, A, I1, I2);
+        // every lane inside every record, row >= 2: before, inside and after
+        // the window as three loops (one loop with a branch spills)
+        auto fast = [&](const bool TBW, const int tlim) {
+            for (; t + 1 <= tlim; t += 2) {
+                ck(t);
+                step(false, false, TBW, t, A, B, I2, I1);
+                step(false, false, TBW, t + 1, B, A, I1, I2);
+            }
+        };
+        fast(TB1, min(xmin - 2, tw0 - 1));                       // pairs ending before tw0
+        if (TWO) {
+            fast(true, min(xmin - 2, tw1 - 1));                  // t >= tw0 here (both odd) or past the region
+            fast(false, xmin - 2);
         }
         for (; t + 1 < tend; t += 2) {
             ck(t);
-            step(false, true, TB1, t, A, B, I2, I1);
-            step(false, true, TB1, t + 1, B, A, I1, I2);
+            if (inwin(t)) {
+                step(false, true, true, t, A, B, I2, I1);
+                step(false, true, true, t + 1, B, A, I1, I2);
+            } else {
+                step(false, true, TB1, t, A, B, I2, I1);
+                step(false, true, TB1, t + 1, B, A, I1, I2);
+            }
         }
-        if (t < tend) step(true, true, TB1, t, A, B, I2, I1);
+        if (t < tend) {
+            if (inwin(t)) step(true, true, true, t, A, B, I2, I1);
+            else          step(true, true, TB1, t, A, B, I2, I1);
+        }
         wv_mem_sync();                            // traceback / checkpoints written by all lanes
         mark(1);
 
@@ -416,6 +487,23 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
         // above its best cell; 1 = the start) and runs until every lane of its
         // group has passed row bx[h]; per-half rows i_h = t0h[h] + tau - gl.
         bool todo[2] = {valid[0], valid[1]};
+        if (tw1 > tw0) {
+            // halves whose best cell (every lane's step of its row) lies in the window
+            bool cov[2];
+            for (int h = 0; h < 2; ++h) cov[h] = todo[h] && bx[h] + G <= tw1;
+            if (wv_any(cov[0] || cov[1])) {
+                for (int h = 0; h < 2; ++h) {
+                    TbAcc16 acc16 = {tbw, X8, Yp[h], gg, G, h, tw0};
+                    acc16.t1 = tw1;
+                    const bool lost = nw_finish(P, acc16, xl[h], yl[h], cov[h], gg, gl, G, bscore[h], bx[h], by[h],
+                                                cidx[h], sid[h]);
+                    if (cov[h]) todo[h] = lost;
+                    if (cov[h] && !lost && gl == 0 && in_group && P.win) wv_atomic_add(P.win, 1u);
+                }
+                wv_mem_sync();                    // walkers done before the second sweep overwrites the slot
+            }
+            mark(4);
+        }
         int t0h[2] = {1, 1};
         // MASK: some half may be at row <= 1 (it restarted at step 1)
         auto step2 = [&](const bool MASK, const int tau, uint32_t (&cur)[K], const uint32_t (&own)[K],
@@ -465,7 +553,7 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
             in0 = MASK ? wv_bfi(pm, in1, sN) : sN;
             outT = cur[K - 1]; outMS = mfS; outL = l0;
         };
-        for (int att = 0; att < 2; ++att) {
+        for (int att = wv_any(todo[0] || todo[1]) ? 0 : 2; att < 2; ++att) {
             // attempt 0: the band; attempt 1 (a path left it): every half from the start
             int n2 = 0;
             for (int h = 0; h < 2; ++h) {

@@ -40,6 +40,12 @@ struct NwLaunch {
     const uint8_t  *q;   const uint64_t *q_start;     // q_start[n_q]  = q_len
     const uint32_t *cand_read, *cand_sid;
     uint32_t n_cand;
+    // nw16 two-pass: optional work order (slot w of the queue takes candidate
+    // perm[w]) and each candidate's predicted first row (the seed hit's
+    // diagonal, NW16_NOROW = none), see nw16_kernel.hip
+    const uint32_t *perm; const int32_t *cand_row;
+    uint32_t *win;               // count of candidates walked inside their first-sweep window
+    int32_t  win_up, win_down;   // window rows above / below the predicted ones
     int32_t  igap, egap;
     int32_t  G, GPW;             // lanes per group, groups per wave
     int32_t  xcap;               // max xlen of the launch

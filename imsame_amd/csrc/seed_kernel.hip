@@ -39,6 +39,8 @@ struct SeedLaunch {
     const uint32_t *minlen, *minident;     // acceptance tables of the launch (NULL: no a-priori rejection)
     uint32_t n_minlen, n_minident;
     uint32_t *cread, *csid, *ncand;        // class 0: ylen <= short_ylen
+    int32_t *crow;                         // class 0: the record row of the read's first base by the
+                                           // hit that made the candidate (INT32_MIN: none; NULL: off)
     uint32_t *cread2, *csid2, *ncand2;     // class 1: longer reads
     unsigned long long *err;               // min (read << 32 | record)
     unsigned long long *nhits;
@@ -169,6 +171,16 @@ __device__ __forceinline__ bool read_irrelevant(const SeedLaunch &S, uint64_t yl
     return S.max_rec <= S.max_rs && hit_irrelevant(S, S.max_rec, ylen);
 }
 
+// The first candidate of a read predicts its NW path (nw16_kernel.hip's
+// first-sweep traceback window) when its hit is strong: an ungapped raw score
+// of >= 7/3 per read base is a true hit's (C2: accepted first hits score
+// 350-700, the e-value passes of random reads 236-350 by the idents quirk,
+// Appendix A Q6).  A weak hit gets no prediction: its NW takes the second
+// sweep, and it does not widen the window of the true hits' wave.
+__device__ __forceinline__ int32_t predicted_row(uint64_t raw, uint64_t ylen, int64_t rec_pos, int64_t read_pos) {
+    return 3 * raw >= 7 * ylen ? (int32_t)(rec_pos - read_pos) : INT32_MIN;
+}
+
 __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint64_t &hits) {
     const uint64_t r = S.active[idx], k = r - S.read_from;
     const uint64_t rs = S.q_start[r], re = S.q_start[r + 1];
@@ -197,6 +209,7 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint
     // and a later hit of an emitted or rejected record cannot change that.
     uint32_t emit[SPEC_MAX];
     uint32_t ne = 0, perr = 0;
+    int32_t row0 = INT32_MIN;              // first candidate's diagonal (nw16 traceback window)
     uint32_t code = 0;
     bool have = false, stop = false, paused = false;
     // A read that runs out of budget pauses at the hit it has not examined
@@ -244,6 +257,7 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint
                     break;
                 }
                 if (nw_cannot_accept(S, xlen, ylen)) continue;       // NW would reject it
+                if (ne == 0) row0 = predicted_row(raw, ylen, ent.x, (int64_t)(p + 1 - rs));
                 emit[ne++] = sid;
                 if (ne == spec) {
                     S.cur_p[k] = p; S.cur_h[k] = h + 1;              // resume after this hit
@@ -271,6 +285,8 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint
     const uint32_t o = wv_atomic_add(shortc ? S.ncand : S.ncand2, ne);
     uint32_t *cr = shortc ? S.cread : S.cread2, *cs = shortc ? S.csid : S.csid2;
     for (uint32_t m = 0; m < ne; ++m) { cr[o + m] = (uint32_t)r; cs[o + m] = emit[m]; }
+    if (shortc && S.crow)
+        for (uint32_t m = 0; m < ne; ++m) S.crow[o + m] = m ? INT32_MIN : row0;
     S.cbase[k] = o; S.ccnt[k] = ne;
 }
 
@@ -338,6 +354,7 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
 #pragma unroll
     for (int m = 0; m < SPEC_MAX; ++m) emit[m] = 0xFFFFFFFFu;
     uint32_t ne = 0, perr = 0, used = 0;
+    uint32_t e0p = 0, e0r = 0;             // first candidate's window (read-relative) and bucket rank
     bool done = !gvalid || p >= up_to || read_irrelevant(S, ylen), paused = false,
          exhausted = gvalid && p >= up_to;
     while (wv_any(!done)) {
@@ -390,6 +407,7 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
                 const uint2 it = lk[m];
                 if (emit_has(emit, ne, it.x)) continue;            // emitted by an earlier window
                 if (it.y & 0x80000000u) { perr = it.x + 1; stop = true; break; }
+                if (ne == 0) { e0p = (uint32_t)(pk - rs); e0r = it.y & 0x7FFFFFFFu; }
 #pragma unroll
                 for (int q2 = 0; q2 < SPEC_MAX; ++q2) emit[q2] = ((uint32_t)q2 == ne) ? it.x : emit[q2];
                 ++ne;
@@ -434,6 +452,17 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
 #pragma unroll
     for (int m = 0; m < SPEC_MAX; ++m)
         if ((uint32_t)m < ne) { cr[o + m] = (uint32_t)r; cs[o + m] = emit[m]; }
+    if (shortc && S.crow) {
+        // the first candidate's hit again: its entry gives the record position
+        // and its extension the strength
+        const uint2 ent = S.ent[S.off[kmer_code_at(S.q, rs + e0p)] + e0r];
+        const int64_t xs = (int64_t)S.db_start[ent.y];
+        const int64_t xe = (ent.y == S.n_db - 1) ? (int64_t)S.db_len : (int64_t)S.db_start[ent.y + 1] - 1;
+        const uint64_t raw = ungapped_raw(S.db, S.q, xs + ent.x, (int64_t)(rs + e0p) + 1, xs, xe, ys, ye,
+                                          (int64_t)S.db_len, (int64_t)S.q_len);
+        S.crow[o] = predicted_row(raw, ylen, ent.x, (int64_t)e0p + 1);
+        for (uint32_t m = 1; m < ne; ++m) S.crow[o + m] = INT32_MIN;
+    }
     S.cbase[k] = o; S.ccnt[k] = ne;
 }
 

@@ -126,6 +126,10 @@ typedef struct imsame_stats {
     uint64_t lanes;         /* concurrent lanes the call ran (1 or 2)   */
     uint64_t nw_redo;       /* two-pass NW: waves whose traceback band missed a
                                path and redid their second sweep from row 1 */
+    uint64_t launch_pk;     /* bit k: NW launch k ran the packed int16 kernel
+                               (nw16_kernel), else the int32 nw_kernel     */
+    uint64_t nw_win;        /* two-pass NW: candidates whose path was walked in
+                               the first sweep's predicted traceback window  */
 } imsame_stats;
 
 typedef struct imsame_ctx imsame_ctx;
@@ -172,6 +176,19 @@ int imsame_dev_set_query(imsame_ctx *ctx, const uint8_t *q_seq, uint64_t q_len,
 int imsame_dev_set_query_range(imsame_ctx *ctx, const uint8_t *q_seq, uint64_t q_len,
                                const uint64_t *q_start, uint64_t n_q,
                                uint64_t read_from, uint64_t read_to);
+
+/* imsame_dev_set_query_range without waiting for the copies: they are queued
+ * in parts on the context's stream, and each internal lane of the next
+ * imsame_dev_align* starts as soon as the parts holding its reads are in HBM,
+ * so the upload overlaps the first lanes' seed scans.  q_seq must stay valid
+ * and unchanged until that call (or imsame_dev_sync) returns; it should be
+ * page-locked (imsame_host_alloc) for the copies to run asynchronously. */
+int imsame_dev_set_query_range_async(imsame_ctx *ctx, const uint8_t *q_seq, uint64_t q_len,
+                                     const uint64_t *q_start, uint64_t n_q,
+                                     uint64_t read_from, uint64_t read_to);
+
+/* Wait for the context's queued work (an asynchronous query upload). */
+int imsame_dev_sync(imsame_ctx *ctx);
 
 /* Replaces T x computeAlignmentsByThread (alignmentFunctions.c:43-208) over
  * reads [read_from, read_to) of the loaded query (inside the uploaded range).  n_threads_semantic is the

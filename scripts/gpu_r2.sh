@@ -41,6 +41,12 @@ for s in $STEPS; do
     lanes*) LN=${s#lanes}; LN=${LN%%_*}; SH=${s#lanes${LN}}; SH=${SH#_}
            IMSAME_LANES=$LN timeout -k 10 600 python -u bench.py --cpu-sample 0 --e2e off --steps 5 ${SH:+--shard ${SH/_//}} \
            > gpurun_out/bench_${s}_${TAG}.json 2> gpurun_out/bench_${s}_${TAG}.err; ok_or_stop $? $s ;;
+    nowin) IMSAME_NW_WINDOW=0 timeout -k 10 600 python -u bench.py --cpu-sample 0 --e2e off --steps 5 \
+           > gpurun_out/bench_nowin_${TAG}.json 2> gpurun_out/bench_nowin_${TAG}.err; ok_or_stop $? nowin ;;
+    syncup) timeout -k 10 600 python -u bench.py --cpu-sample 0 --e2e off --steps 5 --upload sync \
+           > gpurun_out/bench_syncup_${TAG}.json 2> gpurun_out/bench_syncup_${TAG}.err; ok_or_stop $? syncup ;;
+    bench5) timeout -k 10 600 python -u bench.py --cpu-sample 0 --e2e off --steps 5 \
+           > gpurun_out/bench5_${TAG}.json 2> gpurun_out/bench5_${TAG}.err; ok_or_stop $? bench5 ;;
     onepass) IMSAME_NW_ONEPASS=1 timeout -k 10 600 python -u bench.py --cpu-sample 0 --e2e off --steps 5 \
            > gpurun_out/bench_onepass_${TAG}.json 2> gpurun_out/bench_onepass_${TAG}.err; ok_or_stop $? onepass ;;
     band*) BW=${s#band}; IMSAME_NW_BAND=$BW timeout -k 10 600 python -u bench.py --cpu-sample 0 --e2e off --steps 5 \
@@ -58,7 +64,7 @@ for s in $STEPS; do
     clitests) timeout -k 10 900 python -u -m pytest tests/test_gpu.py tests/test_avav.py -m gpu -v --timeout 300 --timeout-method thread \
              -k "cli or driver or multi_device" > gpurun_out/pytest_cli_${TAG}.log 2>&1; ok_or_stop $? clitests ;;
     nwtests) timeout -k 10 900 python -u -m pytest tests/test_gpu.py -m gpu -v --timeout 300 --timeout-method thread \
-             -k "two_pass or nw_pairs or nw_packed or c2_shape or e2e or lanes or path_arena" \
+             -k "two_pass or nw_pairs or nw_packed or c2_shape or e2e or lanes or path_arena or async_query or shards" \
              > gpurun_out/pytest_nw_${TAG}.log 2>&1; ok_or_stop $? nwtests ;;
     c5) timeout -k 10 600 python -u bench.py --config c5 --steps 1 --warmup 0 > gpurun_out/bench_c5_${TAG}.json \
            2> gpurun_out/bench_c5_${TAG}.err; ok_or_stop $? c5 ;;

@@ -46,11 +46,15 @@ static void run_wave(const std::function<void(int)> &f) {
 // waves whose nw16 traceback band missed a path (NwLaunch::redo), since the last emu_redo_count()
 static uint32_t g_redo;
 extern "C" uint32_t emu_redo_count(void) { const uint32_t r = g_redo; g_redo = 0; return r; }
+// candidates walked inside their first-sweep traceback window (NwLaunch::win), since the last call
+static uint32_t g_win;
+extern "C" uint32_t emu_win_count(void) { const uint32_t r = g_win; g_win = 0; return r; }
 
 static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, const uint64_t *qs,
                   const uint32_t *cread, const uint32_t *csid, uint32_t n, const imsame_params *p, uint32_t ymax,
                   uint32_t xmax, const std::vector<uint32_t> &ml, const std::vector<uint32_t> &mi,
-                  imsame_read_result *out, uint32_t *paths, uint32_t pcap, uint32_t *pused, uint32_t *flags) {
+                  imsame_read_result *out, uint32_t *paths, uint32_t pcap, uint32_t *pused, uint32_t *flags,
+                  const int32_t *crow = nullptr) {
     // same kernel choice as imsame_dev.hip:plan_nw
     const bool pk = !(p->flags & IMSAME_FLAG_NW32) && nw16_fits(p->igap, p->egap, xmax, ymax);
     const char *op = getenv("IMSAME_NW_ONEPASS");
@@ -78,6 +82,25 @@ static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, cons
     P.ck = ck.data(); P.ck_wave_dw = ck.size();
     P.band_w = be ? std::max(0, atoi(be)) : 200;        // imsame_dev.hip:nw16_band_rows
     P.redo = &g_redo;
+    // queue order by predicted row, as imsame_dev.hip:launch_nw (row_bucket:
+    // 8-row buckets, unpredicted last; stable here, any order is correct)
+    std::vector<uint32_t> perm;
+    if (crow && two && n >= 64) {
+        const uint32_t nb = ((uint32_t)sh.xcap + 512) / 8 + 2;
+        auto bucket = [&](int32_t r) -> uint32_t {
+            if (r == INT32_MIN) return nb - 1;
+            const int64_t b = ((int64_t)r + 256) >> 3;
+            return (uint32_t)(b < 0 ? 0 : b > (int64_t)nb - 2 ? (int64_t)nb - 2 : b);
+        };
+        std::vector<uint32_t> cur(nb + 1, 0);
+        for (uint32_t k = 0; k < n; ++k) cur[bucket(crow[k]) + 1]++;
+        for (uint32_t b = 0; b < nb; ++b) cur[b + 1] += cur[b];
+        perm.resize(n);
+        for (uint32_t k = 0; k < n; ++k) perm[cur[bucket(crow[k])]++] = k;
+        P.perm = perm.data(); P.cand_row = crow;
+        P.win_up = NW16_WIN_UP; P.win_down = NW16_WIN_DOWN;
+    }
+    P.win = &g_win;
     bool ymult = true;        // every read length a multiple of NW16_K (imsame_dev.hip: q_len_mult)
     for (uint32_t k = 0; k < n; ++k) ymult = ymult && (qs[cread[k] + 1] - qs[cread[k]]) % NW16_K == 0;
     if (two && ymult)     run_wave([&](int lane) { nw16_wave<true, true>(P, lds.data(), lane, 0); });
@@ -188,6 +211,9 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
     std::vector<uint64_t> cur_p(n);
     std::vector<uint32_t> cur_h(n), memo((size_t)n * MEMO), act(n), nxt(n), cr(n), cs(n), cr2(n), cs2(n);
     std::vector<uint32_t> cbase(n), ccnt(n), perr(n);
+    std::vector<int32_t> crow(n);
+    const char *win_env = getenv("IMSAME_NW_WINDOW");
+    int32_t *crowp = (win_env && !atoi(win_env)) ? nullptr : crow.data();
     const char *spec_env = getenv("IMSAME_SPEC");
     const uint32_t spec_later = spec_env ? (uint32_t)std::max(1, std::min(SPEC_MAX, atoi(spec_env))) : (uint32_t)SPEC_MAX;
     const char *bud_env = getenv("IMSAME_SEED_BUDGET");
@@ -223,7 +249,7 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
         S.budget = seed_budget(budget1, (uint32_t)st.rounds);
         S.next = nxt.data(); S.nnext = &nc[2];
         S.cbase = cbase.data(); S.ccnt = ccnt.data(); S.perr = perr.data();
-        S.cread = cr.data(); S.csid = cs.data(); S.ncand = &nc[0];
+        S.cread = cr.data(); S.csid = cs.data(); S.ncand = &nc[0]; S.crow = crowp;
         S.cread2 = cr2.data(); S.csid2 = cs2.data(); S.ncand2 = &nc[1];
         S.err = &err; S.nhits = &nhits;
         const char *l_env = getenv("IMSAME_SEED_L");
@@ -244,12 +270,12 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
             nhits += wh;
         }
         if (nc[0] + nc[1] + nc[2] == 0) break;
-        struct { uint32_t n; uint32_t *r, *s; imsame_read_result *o; uint32_t y; } cls[2] = {
-            {nc[0], cr.data(), cs.data(), o1.data(), short_y}, {nc[1], cr2.data(), cs2.data(), o2.data(), ycap}};
+        struct { uint32_t n; uint32_t *r, *s; imsame_read_result *o; uint32_t y; const int32_t *row; } cls[2] = {
+            {nc[0], cr.data(), cs.data(), o1.data(), short_y, crowp}, {nc[1], cr2.data(), cs2.data(), o2.data(), ycap, nullptr}};
         for (auto &c : cls) {
             if (!c.n) continue;
             run_nw(db, dbs.data(), q, qsv.data(), c.r, c.s, c.n, p, c.y, xcap, ml, mi, c.o, paths,
-                   (uint32_t)paths_cap, &pused, &flags);
+                   (uint32_t)paths_cap, &pused, &flags, c.row);
             st.n_nw += c.n;
             UpdLaunch U = {c.r, c.s, c.n, c.o, read_from, res, rstat.data(), memo.data(), nmemo.data(),
                            cbase.data(), ccnt.data(), perr.data(), nxt.data(), &nc[2], &cells, &nacc, &err,

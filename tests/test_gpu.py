@@ -205,18 +205,24 @@ def test_nw16_two_pass_equals_one_pass(dev, oracle):
     def path(res, paths, k):
         return paths[res["path_off"][k]:res["path_off"][k] + res["path_len"][k]].tolist()
 
-    for band in (None, "40", "0"):
-        if band is not None:
+    # band sizes, and the first sweep's predicted traceback windows off ("nowin")
+    for band in (None, "40", "0", "nowin"):
+        if band == "nowin":
+            os.environ["IMSAME_NW_WINDOW"] = "0"
+        elif band is not None:
             os.environ["IMSAME_NW_BAND"] = band
         try:
             two, paths2, st2 = dev.align(n_threads=16, params=dev.params(flags=FLAG_NW16), want_paths=True)
         finally:
             os.environ.pop("IMSAME_NW_BAND", None)
+            os.environ.pop("IMSAME_NW_WINDOW", None)
         assert not _cmp(two, one), (band, _cmp(two, one))
         acc = np.flatnonzero(one["status"] == 1)
         assert all(path(two, paths2, k) == path(one, paths1, k) for k in acc[::7]), band
         if band == "0":
             assert st2.nw_redo > 0
+        # most accepted reads are walked inside their predicted window
+        assert (st2.nw_win == 0) if band == "nowin" else (st2.nw_win > 0.8 * len(acc)), (band, st2.nw_win)
     rc, exp, _ = oracle.align(ref, rst, q, qs, None, 16)
     assert rc == 0 and not _cmp(one, exp)
 
@@ -517,6 +523,35 @@ def test_query_shards_equal_whole_run(dev, oracle):
         dev.align(0, 10, n_threads=16)                    # outside the uploaded range
     rc, exp, _ = oracle.align(ref, rst, q, qs, None, 16)
     assert rc == 0 and not _cmp(whole, exp)
+
+
+def test_async_query_upload_equals_sync(dev, monkeypatch):
+    """imsame_dev_set_query_range_async: the copies are queued in parts and
+    each lane of the next align waits only for the parts holding its reads
+    (bench.py's step).  4 lanes over a page-locked query give the rows of
+    the waited upload; a second queued upload (another shard) replaces the
+    first before any align; imsame_dev_sync waits without an align."""
+    import imsame_amd
+    ref, rst = synth.make_reference_arr(2_000_000, 2_000, seed=52)
+    q, qs = synth.make_reads_arr(ref, 140_000, 150, seed=53)
+    dev.index(ref, rst)
+    dev.set_query(q, qs)
+    whole, _, st0 = dev.align(n_threads=16)
+    pin = imsame_amd.PinnedArray(len(q))
+    pin.array[:] = q
+    monkeypatch.setenv("IMSAME_LANES", "4")
+    dev.set_query(pin.array, qs, wait=False)
+    got, _, st = dev.align(n_threads=16)
+    assert st.lanes == 4 and not _cmp(got, whole)
+    dev.set_query(pin.array, qs, 0, 70_000, wait=False)
+    dev.set_query(pin.array, qs, 70_000, 140_000, wait=False)
+    got, _, st = dev.align(n_threads=16)
+    assert st.lanes == 2 and not _cmp(got, whole[70_000:])
+    dev.set_query(pin.array, qs, 1, 139_999, wait=False)
+    dev.sync()
+    got, _, _ = dev.align(n_threads=16)
+    assert not _cmp(got, whole[1:139_999])
+    pin.free()
 
 
 def test_path_arena_overflow_rewalks_only_lost_reads(dev, monkeypatch):

@@ -183,6 +183,39 @@ def test_emulated_two_pass_band(emu, oracle, band, monkeypatch):
         assert n_redo == 0
 
 
+@pytest.mark.parametrize("seed_l", ["1", "4"])
+def test_emulated_predicted_traceback_window(emu, oracle, seed_l, monkeypatch):
+    """nw16_kernel.hip's predicted window (emulated pipeline): the strong seed
+    hit's diagonal (seed_one, or seed_group's re-derivation) orders the queue
+    (8-row buckets) and the first sweep writes the traceback of each wave's
+    predicted rows; halves whose best cell lies there walk it, the others
+    (random reads, reads over a record end, a path that leaves the window)
+    fall back to the second sweep.  Reads with indels and edits, 10 % random;
+    every field equals the oracle and the run without windows
+    (IMSAME_NW_WINDOW=0), and both kinds of half occur."""
+    from tests import synth
+    monkeypatch.setenv("IMSAME_SEED_L", seed_l)
+    win = emu.lib.emu_win_count
+    win.restype = C.c_uint32
+    ref, rst = synth.make_reference_arr(240_000, 700, seed=61)
+    q, qs = synth.make_reads_arr(ref, 110, 150, seed=62, sub=0.02, ins=0.01, dele=0.01)
+    rc0, exp, _ = oracle.align(ref, rst, q, qs, oracle.params(), 4)
+    assert rc0 == 0
+    win()
+    rc, got, _, st = emu.align(ref, rst, q, qs, oracle.params(), 4)
+    n_win = win()
+    assert rc == 0
+    for f in PARITY_FIELDS:
+        assert np.array_equal(got[f], exp[f]), f
+    acc = int((exp["status"] == 1).sum())
+    assert n_win > acc // 2 and n_win < st.n_nw, (n_win, acc, st.n_nw)
+    monkeypatch.setenv("IMSAME_NW_WINDOW", "0")
+    rc, got0, _, _ = emu.align(ref, rst, q, qs, oracle.params(), 4)
+    assert rc == 0 and win() == 0
+    for f in PARITY_FIELDS:
+        assert np.array_equal(got0[f], exp[f]), f
+
+
 def _emu_ungapped(emu, db, dbs, q, qs, pd0, pq0, read, sid):
     f = emu.lib.emu_ungapped
     f.restype = C.c_uint64
