@@ -171,13 +171,14 @@ __global__ void scan_add(T *out, const T *bpre, uint64_t n) {
 
 // ---------------------------------------------------------------------------
 // Launch order of a packed NW queue: candidates by the predicted first row of
-// their read (SeedLaunch::crow) in 8-row buckets, unpredicted ones last, so
+// their read (SeedLaunch::crow) in 8-row buckets, unpredicted ones FIRST (their waves run the second
+// sweep: the costliest go early, the cheap ones fill the launch's tail), so
 // the candidates a wave takes share one traceback window (nw16_kernel.hip).
 // Counting sort: histogram, one-block exclusive scan, scatter.
 __device__ __forceinline__ uint32_t row_bucket(int32_t r, uint32_t nb) {
-    if (r == INT32_MIN) return nb - 1;
-    const int64_t b = ((int64_t)r + 256) >> 3;
-    return (uint32_t)(b < 0 ? 0 : b > (int64_t)nb - 2 ? (int64_t)nb - 2 : b);
+    if (r == INT32_MIN) return 0;
+    const int64_t b = (((int64_t)r + 256) >> 3) + 1;
+    return (uint32_t)(b < 1 ? 1 : b > (int64_t)nb - 1 ? (int64_t)nb - 1 : b);
 }
 __global__ void row_hist_kernel(const int32_t *row, uint32_t n, uint32_t nb, uint32_t *hist) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -739,6 +740,8 @@ static int launch_nw(imsame_ctx *c, NwPlan pl, const uint32_t *cread, const uint
         P.perm = c->cperm.as<uint32_t>(); P.cand_row = crow;
         const char *wu = getenv("IMSAME_NW_WIN_UP"), *wd = getenv("IMSAME_NW_WIN_DOWN");
         P.win_up = wu ? atoi(wu) : NW16_WIN_UP; P.win_down = wd ? atoi(wd) : NW16_WIN_DOWN;
+        const char *wb = getenv("IMSAME_NW_WIN_BOTTOM");
+        P.win_bottom = wb ? atoi(wb) : NW16_WIN_BOTTOM;
     }
     if (pl.two && pl.last4)     nw16_kernel<true, true><<<pl.blocks, 256, pl.lds, s>>>(P);
     else if (pl.two)            nw16_kernel<false, true><<<pl.blocks, 256, pl.lds, s>>>(P);
@@ -883,10 +886,13 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         c->cout.ensure((uint64_t)n * 64) || c->cout2.ensure((uint64_t)n * 64) || c->cbase.ensure((uint64_t)n * 4) ||
         c->ccnt.ensure((uint64_t)n * 4) || c->perr.ensure((uint64_t)n * 4) || c->crow.ensure((uint64_t)n * 4))
         return IMSAME_E_OOM;
-    // predicted rows for the packed kernel's first-sweep traceback windows
-    // (IMSAME_NW_WINDOW=0: off, every traceback from the second sweep)
+    // predicted rows for the packed kernel's first-sweep traceback windows:
+    // OFF by default (IMSAME_NW_WINDOW=1 turns them on).  Measured at C2 they
+    // cut the NW wave-cycles by 2 % but the whole step by -1..-3 %: the window
+    // steps issue +73 VALU per step and spill (profiles/r2s_ab_*.json), and
+    // the second sweep they replace is only 13 % of the cycles.
     const char *win_env = getenv("IMSAME_NW_WINDOW");
-    int32_t *crow = (win_env && !atoi(win_env)) ? nullptr : c->crow.as<int32_t>();
+    int32_t *crow = (win_env && atoi(win_env)) ? c->crow.as<int32_t>() : nullptr;
     // speculation: round 1 emits one candidate per read (most reads accept
     // it); later rounds emit up to SPEC_MAX, bounded by the candidate buffers
     const char *spec_env = getenv("IMSAME_SPEC");

@@ -79,6 +79,7 @@
 #define NW16_WIN_UP 32            // window rows above the predicted first row
 #define NW16_WIN_DOWN 24          // ... and below the predicted last row
 #define NW16_WIN_MAX 448          // longest window (steps) a wave writes in its first sweep
+#define NW16_WIN_BOTTOM 40        // rows above the last one for an unpredicted candidate
 
 // does the launch fit the int16 path?  (all gap terms non-positive)
 __host__ static inline bool nw16_fits(int64_t ig, int64_t eg, uint64_t xcap, uint64_t ymax) {
@@ -230,7 +231,14 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
             int lo = INT_MAX, hi = INT_MIN, none = 0;
             for (int h = 0; h < 2; ++h) {
                 if (!valid[h]) continue;
-                if (prow[h] == NW16_NOROW) { none = 1; continue; }
+                if (prow[h] == NW16_NOROW) {
+                    // no prediction (a weak hit: random reads' e-value passes, whose
+                    // best cells mostly sit on the last row with short paths)
+                    if (P.win_bottom < 0) { none = 1; continue; }
+                    lo = min(lo, xl[h] - 1 - P.win_bottom);
+                    hi = max(hi, xl[h] - 1);
+                    continue;
+                }
                 lo = min(lo, prow[h] - P.win_up);
                 hi = max(hi, prow[h] + yl[h] - 1 + P.win_down);
             }

@@ -46,6 +46,7 @@ struct NwLaunch {
     const uint32_t *perm; const int32_t *cand_row;
     uint32_t *win;               // count of candidates walked inside their first-sweep window
     int32_t  win_up, win_down;   // window rows above / below the predicted ones
+    int32_t  win_bottom;         // unpredicted candidate: its last rows (< 0: no window)
     int32_t  igap, egap;
     int32_t  G, GPW;             // lanes per group, groups per wave
     int32_t  xcap;               // max xlen of the launch

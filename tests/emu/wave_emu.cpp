@@ -83,14 +83,14 @@ static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, cons
     P.band_w = be ? std::max(0, atoi(be)) : 200;        // imsame_dev.hip:nw16_band_rows
     P.redo = &g_redo;
     // queue order by predicted row, as imsame_dev.hip:launch_nw (row_bucket:
-    // 8-row buckets, unpredicted last; stable here, any order is correct)
+    // 8-row buckets, unpredicted first; stable here, any order is correct)
     std::vector<uint32_t> perm;
     if (crow && two && n >= 64) {
         const uint32_t nb = ((uint32_t)sh.xcap + 512) / 8 + 2;
         auto bucket = [&](int32_t r) -> uint32_t {
-            if (r == INT32_MIN) return nb - 1;
-            const int64_t b = ((int64_t)r + 256) >> 3;
-            return (uint32_t)(b < 0 ? 0 : b > (int64_t)nb - 2 ? (int64_t)nb - 2 : b);
+            if (r == INT32_MIN) return 0;
+            const int64_t b = (((int64_t)r + 256) >> 3) + 1;
+            return (uint32_t)(b < 1 ? 1 : b > (int64_t)nb - 1 ? (int64_t)nb - 1 : b);
         };
         std::vector<uint32_t> cur(nb + 1, 0);
         for (uint32_t k = 0; k < n; ++k) cur[bucket(crow[k]) + 1]++;
@@ -99,6 +99,8 @@ static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, cons
         for (uint32_t k = 0; k < n; ++k) perm[cur[bucket(crow[k])]++] = k;
         P.perm = perm.data(); P.cand_row = crow;
         P.win_up = NW16_WIN_UP; P.win_down = NW16_WIN_DOWN;
+        const char *wb = getenv("IMSAME_NW_WIN_BOTTOM");
+        P.win_bottom = wb ? atoi(wb) : NW16_WIN_BOTTOM;
     }
     P.win = &g_win;
     bool ymult = true;        // every read length a multiple of NW16_K (imsame_dev.hip: q_len_mult)
@@ -213,7 +215,7 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
     std::vector<uint32_t> cbase(n), ccnt(n), perr(n);
     std::vector<int32_t> crow(n);
     const char *win_env = getenv("IMSAME_NW_WINDOW");
-    int32_t *crowp = (win_env && !atoi(win_env)) ? nullptr : crow.data();
+    int32_t *crowp = (win_env && atoi(win_env)) ? crow.data() : nullptr;     // imsame_dev.hip: off by default
     const char *spec_env = getenv("IMSAME_SPEC");
     const uint32_t spec_later = spec_env ? (uint32_t)std::max(1, std::min(SPEC_MAX, atoi(spec_env))) : (uint32_t)SPEC_MAX;
     const char *bud_env = getenv("IMSAME_SEED_BUDGET");

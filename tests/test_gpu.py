@@ -207,9 +207,9 @@ def test_nw16_two_pass_equals_one_pass(dev, oracle):
 
     # band sizes, and the first sweep's predicted traceback windows off ("nowin")
     for band in (None, "40", "0", "nowin"):
-        if band == "nowin":
-            os.environ["IMSAME_NW_WINDOW"] = "0"
-        elif band is not None:
+        if band != "nowin":
+            os.environ["IMSAME_NW_WINDOW"] = "1"      # opt-in (imsame_dev.hip: off by default)
+        if band not in (None, "nowin"):
             os.environ["IMSAME_NW_BAND"] = band
         try:
             two, paths2, st2 = dev.align(n_threads=16, params=dev.params(flags=FLAG_NW16), want_paths=True)
