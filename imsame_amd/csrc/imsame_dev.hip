@@ -899,6 +899,12 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     const uint32_t spec_later = spec_env ? (uint32_t)std::max(1, std::min(SPEC_MAX, atoi(spec_env))) : (uint32_t)SPEC_MAX;
     const char *bud_env = getenv("IMSAME_SEED_BUDGET");
     const uint32_t budget1 = bud_env ? (uint32_t)std::max(0, atoi(bud_env)) : SEED_BUDGET1;
+    // budget growth per round: 8x; a lane of < 100k reads (an 8-GPU shard of
+    // C2) 64x, so its third round finishes the random reads' scans instead of
+    // leaving a latency-bound fourth round of tiny launches (C2 shard 1/8:
+    // 23.4 -> 20.1 ms per step; no effect from 1/4 up, profiles/r2u_*, r2v_*)
+    const char *grow_env = getenv("IMSAME_SEED_GROW");
+    const uint32_t grow = grow_env ? (uint32_t)std::max(2, atoi(grow_env)) : (n < 100000 ? 64u : 8u);
     const uint8_t *qd = dev_q(c);
     const uint64_t *qsd = dev_qs(c);
     uint64_t *ctr = c->ctr.as<uint64_t>();
@@ -931,7 +937,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         S.minraw = c->minraw.as<uint64_t>(); S.n_minraw = ymax + 1;
         S.max_rs = p->max_read_size; S.short_ylen = short_y; S.max_rec = c->max_rec;
         S.spec = (st.rounds == 1) ? 1u : std::max<uint32_t>(1u, std::min<uint32_t>(spec_later, n / nact));
-        S.budget = seed_budget(budget1, (uint32_t)st.rounds);
+        S.budget = seed_budget(budget1, (uint32_t)st.rounds, grow);
         S.next = nxt; S.nnext = (uint32_t *)(ctr + C_NNEXT);
         S.cbase = c->cbase.as<uint32_t>(); S.ccnt = c->ccnt.as<uint32_t>(); S.perr = c->perr.as<uint32_t>();
         S.cread = c->cread.as<uint32_t>(); S.csid = c->csid.as<uint32_t>(); S.ncand = (uint32_t *)(ctr + C_NCAND);
@@ -1090,9 +1096,10 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
     // independent given the chunk heads).  Short reads only: a long-read
     // lane's traceback arena takes most of HBM.
     const char *le = getenv("IMSAME_LANES");
-    // default: 2 lanes, 4 from 1M reads on (profiles/r2h_*: 1M reads 6.81 /
-    // 6.86 / 6.91 M reads/s with 2 / 3 / 4 lanes; a 125k-read shard is best at 2)
-    int nl = le ? std::max(1, std::min(8, atoi(le))) : (n >= 1000000 ? 4 : 2);
+    // default: 3 lanes, 4 from 1M reads on (profiles/r2h_*: 1M reads 6.81 /
+    // 6.86 / 6.91 M reads/s with 2 / 3 / 4 lanes; C2 shards of 1/2, 1/4, 1/8
+    // 1-3 % faster with 3 lanes than 2, profiles/r2w_*)
+    int nl = le ? std::max(1, std::min(8, atoi(le))) : (n >= 1000000 ? 4 : 3);
     while (nl > 1 && n < (uint64_t)nl * LANE_MIN) --nl;
     if (c->is_sub || c->use_wcap || ymax > (uint64_t)NW_W / 2) nl = 1;
     if (nl == 1) {

@@ -223,6 +223,8 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
             xmax = max(xmax, wv_shfl_xor(xmax, o));
             xmin = min(xmin, wv_shfl_xor(xmin, o));
         }
+        // wave-uniform in SGPRs: the sweep's step counter and bounds are scalar
+        xmax = (int)wv_first((uint32_t)xmax); xmin = (int)wv_first((uint32_t)xmin);
         // traceback window of the first sweep: steps [tw0, tw1), both odd (the
         // loops advance t by 2 from 1); rows [lo, hi] of every candidate's
         // prediction take steps lo .. hi + G - 1

@@ -50,10 +50,10 @@ struct SeedLaunch {
 // ungapped extensions (true reads accept within a few), each later round 8x
 // more, so reads that scan every window finish in a compacted list.
 #define SEED_BUDGET1 32u
-__host__ __device__ static inline uint32_t seed_budget(uint32_t b1, uint32_t round) {
+__host__ __device__ static inline uint32_t seed_budget(uint32_t b1, uint32_t round, uint32_t grow = 8) {
     if (b1 == 0) return 0;
     uint64_t b = b1;
-    for (uint32_t k = 1; k < round && b < (1ull << 31); ++k) b *= 8;
+    for (uint32_t k = 1; k < round && b < (1ull << 31); ++k) b *= grow;
     return b >= (1ull << 31) ? 0u : (uint32_t)b;
 }
 

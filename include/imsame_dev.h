@@ -123,7 +123,7 @@ typedef struct imsame_stats {
     double   ms_d2h;        /* results (64 B per read) device -> host        */
     double   ms_nw_busy;    /* wall time the device ran NW launches (union of
                                the launch intervals of all lanes)        */
-    uint64_t lanes;         /* concurrent lanes the call ran (1 or 2)   */
+    uint64_t lanes;         /* concurrent lanes the call ran (1-8)     */
     uint64_t nw_redo;       /* two-pass NW: waves whose traceback band missed a
                                path and redid their second sweep from row 1 */
     uint64_t launch_pk;     /* bit k: NW launch k ran the packed int16 kernel
@@ -202,9 +202,10 @@ int imsame_dev_sync(imsame_ctx *ctx);
  * call); if paths_cap is smaller than *paths_used the call returns
  * IMSAME_E_PATHS with res[] complete and the paths still on the device:
  * grow the host arena and call imsame_dev_fetch_paths.
- * A call over >= 65,536 short reads runs its two halves concurrently on two
- * streams of the device (a second internal lane sharing the index and the
- * query); results do not depend on it (IMSAME_LANES=1 turns it off). */
+ * A call over >= 65,536 short reads is cut into 2-4 parts ("lanes") that run
+ * concurrently on their own streams of the device (internal contexts sharing
+ * the index and the query); results do not depend on it (IMSAME_LANES=1
+ * turns it off). */
 int imsame_dev_align(imsame_ctx *ctx, uint64_t read_from, uint64_t read_to,
                      uint64_t n_threads_semantic, const imsame_params *prm,
                      imsame_read_result *res, uint32_t *paths, uint64_t paths_cap,

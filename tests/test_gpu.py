@@ -273,7 +273,7 @@ def test_full_c2_reference_properties(dev, oracle):
     dev.index(ref, rst)
     dev.set_query(q, qs)
     res, paths, st = dev.align(n_threads=16, want_paths=True)
-    assert st.lanes == 2                      # both halves ran concurrently
+    assert st.lanes == 3                      # three parts ran concurrently
     acc = res["status"] == 1
     assert acc.mean() > 0.85
     # every accepted path re-renders to the device's own identity count (both lanes)
@@ -641,18 +641,21 @@ def test_c5_full_50mbp_database(dev, oracle_memo, rec_bp, cap):
 
 
 def test_lanes_equal_one_lane(dev, monkeypatch):
-    """Two concurrent lanes (the halves of a call on two streams) against one
+    """Three concurrent lanes (parts of a call on three streams) against one
     lane: identical per-read rows and identical .align text for every
-    accepted read (lane 1's paths follow lane 0's in the arena)."""
+    accepted read (each lane's paths follow the previous lanes' in the
+    arena).  The same seed budget schedule in both (by default a lane of
+    < 100k reads grows its budget faster, which reshapes the work only)."""
     ref, rst = synth.make_reference_arr(4_000_000, 2_000, seed=61)
     q, qs = synth.make_reads_arr(ref, 140_000, 150, seed=62, ins=0.003, dele=0.003)
     dev.index(ref, rst)
     dev.set_query(q, qs)
+    monkeypatch.setenv("IMSAME_SEED_GROW", "8")
     two, p2, s2 = dev.align(n_threads=7, want_paths=True, paths_cap=64)     # small host arena: fetch path
     monkeypatch.setenv("IMSAME_LANES", "1")
     one, p1, s1 = dev.align(n_threads=7, want_paths=True)
     monkeypatch.delenv("IMSAME_LANES")
-    assert s2.lanes == 2 and s1.lanes == 1
+    assert s2.lanes == 3 and s1.lanes == 1
     assert not _cmp(two, one)
     assert s2.n_nw == s1.n_nw and s2.n_accepted == s1.n_accepted and s2.ms_nw_busy > 0
     for k in np.flatnonzero(two["status"] == 1)[::53]:
