@@ -1096,10 +1096,12 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
     // independent given the chunk heads).  Short reads only: a long-read
     // lane's traceback arena takes most of HBM.
     const char *le = getenv("IMSAME_LANES");
-    // default: 3 lanes, 4 from 1M reads on (profiles/r2h_*: 1M reads 6.81 /
-    // 6.86 / 6.91 M reads/s with 2 / 3 / 4 lanes; C2 shards of 1/2, 1/4, 1/8
-    // 1-3 % faster with 3 lanes than 2, profiles/r2w_*)
-    int nl = le ? std::max(1, std::min(8, atoi(le))) : (n >= 1000000 ? 4 : 3);
+    // default: 3 lanes, 8 from 1M reads on (profiles/r2h_*: 1M reads 6.81 /
+    // 6.86 / 6.91 M reads/s with 2 / 3 / 4 lanes; r2ab_*: 8 lanes +1.4 % over
+    // 4 in three alternating pairs, 5-6 lanes slower; C2 shards of 1/2, 1/4,
+    // 1/8 1-3 % faster with 3 lanes than 2, r2w_*, and no clear gain from 4-6
+    // lanes there, r2ac_*)
+    int nl = le ? std::max(1, std::min(8, atoi(le))) : (n >= 1000000 ? 8 : 3);
     while (nl > 1 && n < (uint64_t)nl * LANE_MIN) --nl;
     if (c->is_sub || c->use_wcap || ymax > (uint64_t)NW_W / 2) nl = 1;
     if (nl == 1) {

@@ -202,7 +202,7 @@ int imsame_dev_sync(imsame_ctx *ctx);
  * call); if paths_cap is smaller than *paths_used the call returns
  * IMSAME_E_PATHS with res[] complete and the paths still on the device:
  * grow the host arena and call imsame_dev_fetch_paths.
- * A call over >= 65,536 short reads is cut into 2-4 parts ("lanes") that run
+ * A call over >= 65,536 short reads is cut into 2-8 parts ("lanes") that run
  * concurrently on their own streams of the device (internal contexts sharing
  * the index and the query); results do not depend on it (IMSAME_LANES=1
  * turns it off). */
