@@ -35,6 +35,9 @@ for s in $STEPS; do
            2> gpurun_out/bench_c3_${TAG}.err; ok_or_stop $? c3 ;;
     shard*) SH=${s#shard}; timeout -k 10 600 python -u bench.py --cpu-sample 0 --e2e off --shard ${SH/_//} --steps 5 \
            > gpurun_out/bench_${s}_${TAG}.json 2> gpurun_out/bench_${s}_${TAG}.err; ok_or_stop $? $s ;;
+    ranks4) timeout -k 10 600 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
+             --master-port 29519 bench.py --gpus 4 --dist-backend gloo --device 0 --cpu-sample 0 --e2e off \
+             > gpurun_out/bench_ranks4_${TAG}.json 2> gpurun_out/bench_ranks4_${TAG}.err; ok_or_stop $? ranks4 ;;
     ranks2) timeout -k 10 600 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
              --master-port 29517 bench.py --gpus 2 --dist-backend gloo --device 0 --cpu-sample 0 --e2e off \
              > gpurun_out/bench_ranks2_${TAG}.json 2> gpurun_out/bench_ranks2_${TAG}.err; ok_or_stop $? ranks2 ;;
