@@ -320,6 +320,8 @@ def main():
                        "nw_window_walks": last.get("nw_win"),
                        "ms_seed": round(last["ms_seed"], 3), "ms_nw": round(last["ms_nw"], 3),
                        "ms_nw_busy": round(last["ms_nw_busy"], 3),
+                       "ms_nw_first_start": round(last["ms_nw_first"], 3),
+                       "ms_nw_last_end": round(last["ms_nw_last"], 3),
                        "ms_align_call": round(last["ms_total"], 3),
                        "ms_host_setup": round(last["ms_setup"], 3), "ms_d2h_results": round(last["ms_d2h"], 3),
                        "nw_launch_cand": last["launch_cand"],

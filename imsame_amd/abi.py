@@ -75,7 +75,8 @@ class Stats(C.Structure):
         ("launch_cand", C.c_uint64 * LAUNCH_STATS), ("launch_ms", C.c_double * LAUNCH_STATS),
         ("n_rewalk", C.c_uint64), ("ms_setup", C.c_double), ("ms_d2h", C.c_double),
         ("ms_nw_busy", C.c_double), ("lanes", C.c_uint64), ("nw_redo", C.c_uint64),
-        ("launch_pk", C.c_uint64), ("nw_win", C.c_uint64),
+        ("launch_pk", C.c_uint64), ("nw_win", C.c_uint64), ("ms_nw_first", C.c_double),
+        ("ms_nw_last", C.c_double),
     ]
 
     def as_dict(self):

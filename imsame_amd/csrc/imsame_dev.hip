@@ -231,6 +231,7 @@ struct DBuf {
 struct imsame_ctx {
     int device = 0, ncu = 0;
     hipStream_t stream = nullptr;
+    hipStream_t ustream = nullptr;    // query uploads (imsame_dev_set_query_range_async)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     // database + index
     DBuf db, db_start, off, ent, brk, codes, fill, big;
@@ -348,6 +349,7 @@ extern "C" int imsame_dev_open(int device, imsame_ctx **out) {
     HIPCHK(hipGetDeviceProperties(&prop, device));
     c->ncu = prop.multiProcessorCount;
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&c->ustream, hipStreamNonBlocking));
     HIPCHK(hipEventCreate(&c->ev0));
     HIPCHK(hipEventCreate(&c->ev1));
     if (c->ctr.ensure(C_NSLOTS * 8)) { delete c; return IMSAME_E_OOM; }
@@ -367,6 +369,7 @@ extern "C" void imsame_dev_close(imsame_ctx *c) {
     c->subs.clear();
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(c->ustream);
     DBuf *bufs[] = {&c->db, &c->db_start, &c->off, &c->ent, &c->brk, &c->codes, &c->fill, &c->big, &c->q,
                     &c->q_start, &c->res, &c->cur_p, &c->cur_h, &c->memo, &c->nmemo, &c->rstat, &c->act0,
                     &c->act1, &c->cread, &c->csid, &c->cread2, &c->csid2, &c->cout, &c->cout2, &c->ctr,
@@ -380,6 +383,7 @@ extern "C" void imsame_dev_close(imsame_ctx *c) {
     if (!c->is_sub)
         for (hipEvent_t e : c->q_part_ev) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
+    (void)hipStreamDestroy(c->ustream);
     delete c;
 }
 
@@ -519,7 +523,7 @@ extern "C" int imsame_dev_set_query_range_async(imsame_ctx *c, const uint8_t *q_
         return IMSAME_E_ARG;
     if (n_q >= 0xFFFFFFF0ull) return IMSAME_E_ARG;
     HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipStreamSynchronize(c->stream));     // a previous upload may still read h_q_start / fill q
+    HIPCHK(hipStreamSynchronize(c->ustream));    // a previous upload may still read h_q_start / fill q
     c->have_query = false;
     auto qs = [&](uint64_t r) { return r < n_q ? q_start[r] : q_len; };
     for (uint64_t r = read_from; r < read_to; ++r)
@@ -544,13 +548,15 @@ extern "C" int imsame_dev_set_query_range_async(imsame_ctx *c, const uint8_t *q_
         c->q_part_ev.push_back(e);
     }
     c->q_part_end.assign(Q_PARTS, 0);
-    HIPCHK(hipMemcpyAsync(c->q_start.p, c->h_q_start.data(), ns * 8, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemsetAsync((uint8_t *)c->q.p + nb, 0, 64, c->stream));
+    // on the upload stream: every lane (this context's stream included) waits
+    // only for the parts that hold its reads
+    HIPCHK(hipMemcpyAsync(c->q_start.p, c->h_q_start.data(), ns * 8, hipMemcpyHostToDevice, c->ustream));
+    HIPCHK(hipMemsetAsync((uint8_t *)c->q.p + nb, 0, 64, c->ustream));
     for (uint64_t k = 0, a = 0; k < Q_PARTS; ++k) {      // bases [q_base + a, q_base + b)
         const uint64_t b = nb * (k + 1) / Q_PARTS;
         if (b > a) HIPCHK(hipMemcpyAsync((uint8_t *)c->q.p + a, q_seq + c->q_base + a, b - a, hipMemcpyHostToDevice,
-                                         c->stream));
-        HIPCHK(hipEventRecord(c->q_part_ev[k], c->stream));
+                                         c->ustream));
+        HIPCHK(hipEventRecord(c->q_part_ev[k], c->ustream));
         c->q_part_end[k] = c->q_base + b;
         a = b;
     }
@@ -571,6 +577,7 @@ static int query_wait(imsame_ctx *c, hipStream_t s, uint64_t end) {
 extern "C" int imsame_dev_sync(imsame_ctx *c) {
     if (!c) return IMSAME_E_ARG;
     HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->ustream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return IMSAME_OK;
 }
@@ -1057,6 +1064,15 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     return ret;
 }
 
+// first start and last end of [a, b) intervals (ms on the call's clock)
+static void span_ms(const std::vector<std::pair<float, float>> &v, double *first, double *last) {
+    *first = *last = 0;
+    for (size_t k = 0; k < v.size(); ++k) {
+        if (k == 0 || v[k].first < *first) *first = v[k].first;
+        if (k == 0 || v[k].second > *last) *last = v[k].second;
+    }
+}
+
 // total length of the union of [a, b) intervals
 static double union_ms(std::vector<std::pair<float, float>> v) {
     std::sort(v.begin(), v.end());
@@ -1107,7 +1123,7 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
     if (nl == 1) {
         const int rc = align_one(c, read_from, read_to, n_threads_semantic, p, res, paths, paths_cap, paths_used,
                                  stats);
-        if (stats) stats->ms_nw_busy = union_ms(c->nw_iv);
+        if (stats) { stats->ms_nw_busy = union_ms(c->nw_iv); span_ms(c->nw_iv, &stats->ms_nw_first, &stats->ms_nw_last); }
         return rc;
     }
     std::vector<imsame_ctx *> L(nl, c);
@@ -1168,6 +1184,7 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
     }
     st.nw_launch_ms = st.nw_launches ? st.ms_nw / st.nw_launches : 0;
     st.ms_nw_busy = union_ms(iv);
+    span_ms(iv, &st.ms_nw_first, &st.ms_nw_last);
     st.lanes = (uint64_t)nl;
     c->paths_split = true; c->paths_n = used[0]; c->paths_on_host = false;
     c->lane_paths.assign(used.begin() + 1, used.end());

@@ -130,6 +130,9 @@ typedef struct imsame_stats {
                                (nw16_kernel), else the int32 nw_kernel     */
     uint64_t nw_win;        /* two-pass NW: candidates whose path was walked in
                                the first sweep's predicted traceback window  */
+    double   ms_nw_first;   /* first NW launch start / last NW launch end, ms
+                               after the call's first device operation     */
+    double   ms_nw_last;
 } imsame_stats;
 
 typedef struct imsame_ctx imsame_ctx;

@@ -12,6 +12,7 @@ for v in "$@"; do
   name=${v%%:*}; envs=${v#*:}
   shard=""
   case $name in *@*) shard="--shard ${name#*@}"; name=${name%@*}_$(echo ${shard#--shard } | tr / _) ;; esac
+  case $name in sync*) shard="$shard --upload sync" ;; esac
   IFS=',' read -ra kv <<< "$envs"
   env "${kv[@]}" timeout -k 10 600 python -u bench.py --cpu-sample 0 --e2e off --steps 5 $shard \
       > gpurun_out/ab_${TAG}_${name}.json 2> gpurun_out/ab_${TAG}_${name}.err
