@@ -28,6 +28,14 @@ import time
 
 import numpy as np
 
+# one hardware queue per alignment lane: HIP maps a process's streams onto
+# GPU_MAX_HW_QUEUES queues (4 on the GPU boxes), and two of the 8 lanes on one
+# queue serialize (imsame_dev.hip:hw_queues_hint, which asks for 8 only when
+# the variable is unset).  The benchmark raises it to 8 before anything starts
+# HIP (torch does in a multi-rank run); results do not depend on it.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 

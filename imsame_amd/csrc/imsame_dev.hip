@@ -247,6 +247,8 @@ struct imsame_ctx {
     uint64_t n_q = 0, q_len = 0, q_lo = 0, q_hi = 0, q_base = 0, q_lo_first = 0;
     std::vector<uint64_t> h_q_start;  // starts of reads q_lo .. q_hi
     const uint64_t *hq = nullptr;     // = h_q_start.data(), or the parent's for a lane
+    std::vector<uint32_t> h_q_bmax;   // longest read of each QB_READS block from q_lo (range_ymax)
+    const uint32_t *hqb = nullptr;    // = h_q_bmax.data(), or the parent's for a lane
     bool have_query = false;
     // the upload in parts (imsame_dev_set_query_range_async): part k holds the
     // bases below q_part_end[k] and is complete when q_part_ev[k] fires (the
@@ -293,6 +295,18 @@ struct imsame_ctx {
 };
 
 static inline uint64_t hqs(const imsame_ctx *c, uint64_t r) { return c->hq[r - c->q_lo]; }
+// longest read of [a, b) within the uploaded range: block maxima (set at
+// upload) for the whole blocks, a scan of the ragged ends
+#define QB_READS 4096
+static uint64_t range_ymax(const imsame_ctx *c, uint64_t a, uint64_t b) {
+    uint64_t m = 0;
+    auto len = [&](uint64_t r) { return hqs(c, r + 1) - hqs(c, r); };
+    uint64_t blk = (a - c->q_lo + QB_READS - 1) / QB_READS, r = c->q_lo + blk * QB_READS;
+    for (uint64_t x = a; x < std::min(b, r); ++x) m = std::max(m, len(x));
+    for (; r + QB_READS <= b; r += QB_READS, ++blk) m = std::max<uint64_t>(m, c->hqb[blk]);
+    for (uint64_t x = std::max(a, r); x < b; ++x) m = std::max(m, len(x));
+    return m;
+}
 // biased views: valid for the uploaded reads (and QPAD bases before them)
 static inline const uint8_t *dev_q(const imsame_ctx *c) { return (const uint8_t *)((uintptr_t)c->q.p - c->q_base); }
 static inline const uint64_t *dev_qs(const imsame_ctx *c) {
@@ -334,12 +348,24 @@ extern "C" const char *imsame_strerror(int code) {
     return "unknown error";
 }
 
+// Hardware queues per process: a call's lanes run on up to 8 streams, and
+// HIP maps streams onto GPU_MAX_HW_QUEUES queues (default 4), so two lanes
+// sharing a queue serialize (rocprofv3 trace, profiles/r2ag_*).  Asking for 8
+// before the process's first HIP call gives every lane its own queue (C2:
+// +2-3 %, profiles/r2ah_*, r2ai_*); a value the user set is kept, and a
+// process whose HIP runtime is already up (e.g. torch first) keeps its own.
+static void hw_queues_hint() {
+    setenv("GPU_MAX_HW_QUEUES", "8", 0);
+}
+
 extern "C" int imsame_dev_count(void) {
+    hw_queues_hint();
     int n = 0;
     return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
 }
 
 extern "C" int imsame_dev_open(int device, imsame_ctx **out) {
+    hw_queues_hint();
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) return IMSAME_E_HIP;
     HIPCHK(hipSetDevice(device));
@@ -401,7 +427,8 @@ static int lane_sub(imsame_ctx *c, int k, imsame_ctx **out) {
     l->n_db = c->n_db; l->db_len = c->db_len; l->n_ent = c->n_ent; l->max_rec = c->max_rec;
     l->have_index = c->have_index;
     l->n_q = c->n_q; l->q_len = c->q_len; l->q_lo = c->q_lo; l->q_hi = c->q_hi; l->q_base = c->q_base;
-    l->q_lo_first = c->q_lo_first; l->hq = c->hq; l->have_query = c->have_query; l->q_len_mult = c->q_len_mult;
+    l->q_lo_first = c->q_lo_first; l->hq = c->hq; l->hqb = c->hqb; l->have_query = c->have_query;
+    l->q_len_mult = c->q_len_mult;
     l->q_part_ev = c->q_part_ev; l->q_part_end = c->q_part_end;
     l->ev_db_len = 0; l->use_wcap = l->use_wstart = false;
     *out = l;
@@ -526,12 +553,30 @@ extern "C" int imsame_dev_set_query_range_async(imsame_ctx *c, const uint8_t *q_
     HIPCHK(hipStreamSynchronize(c->ustream));    // a previous upload may still read h_q_start / fill q
     c->have_query = false;
     auto qs = [&](uint64_t r) { return r < n_q ? q_start[r] : q_len; };
-    for (uint64_t r = read_from; r < read_to; ++r)
-        if (qs(r) > qs(r + 1) || qs(r + 1) > q_len) return IMSAME_E_ARG;       // starts ascend within the query
+    // one pass over the shard's starts: ascending within the query (else
+    // IMSAME_E_ARG), the host copy, every length a multiple of NW16_K?, and
+    // the longest read of each QB_READS block (range_ymax)
+    const uint64_t m = read_to - read_from;
+    c->h_q_start.resize(m + 1);
+    c->h_q_bmax.assign(m / QB_READS + 1, 0);
+    uint64_t *h = c->h_q_start.data();
+    uint32_t *bm = c->h_q_bmax.data();
+    uint64_t prev = qs(read_from);
+    bool ok = prev <= q_len, mult = true;
+    h[0] = prev;
+    for (uint64_t k = 1; k <= m; ++k) {
+        const uint64_t v = read_from + k < n_q ? q_start[read_from + k] : q_len;
+        const uint64_t len = v - prev;
+        ok &= v >= prev;
+        mult &= len % NW16_K == 0;
+        bm[(k - 1) / QB_READS] = std::max<uint32_t>(bm[(k - 1) / QB_READS], (uint32_t)std::min<uint64_t>(len, 0xFFFFFFFFu));
+        h[k] = v;
+        prev = v;
+    }
+    if (!ok || prev > q_len) return IMSAME_E_ARG;                   // starts ascend within the query
     c->n_q = n_q; c->q_len = q_len; c->q_lo = read_from; c->q_hi = read_to;
-    c->h_q_start.resize(read_to - read_from + 1);
-    for (uint64_t r = read_from; r <= read_to; ++r) c->h_q_start[r - read_from] = qs(r);
     c->hq = c->h_q_start.data();
+    c->hqb = c->h_q_bmax.data();
     // reads q_lo_first .. read_from-1 are empty (start where read_from starts)
     uint64_t f = read_from;
     while (f > 0 && qs(f - 1) == qs(read_from)) --f;
@@ -539,8 +584,7 @@ extern "C" int imsame_dev_set_query_range_async(imsame_ctx *c, const uint8_t *q_
     const uint64_t b0 = qs(read_from), b1 = qs(read_to);
     c->q_base = b0 > QPAD ? b0 - QPAD : 0;
     const uint64_t nb = b1 - c->q_base, ns = read_to - read_from + 1;
-    c->q_len_mult = true;
-    for (uint64_t r = read_from; r < read_to; ++r) c->q_len_mult = c->q_len_mult && (qs(r + 1) - qs(r)) % NW16_K == 0;
+    c->q_len_mult = mult;
     if (c->q.ensure(nb + 64) || c->q_start.ensure(ns * 8)) return IMSAME_E_OOM;
     while (c->q_part_ev.size() < Q_PARTS) {
         hipEvent_t e;
@@ -872,7 +916,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     c->paths_n = 0; c->paths_on_host = false;
     // shapes
     uint32_t ymax = 0;
-    for (uint64_t r = read_from; r < read_to; ++r) ymax = (uint32_t)std::max<uint64_t>(ymax, hqs(c, r + 1) - hqs(c, r));
+    ymax = (uint32_t)range_ymax(c, read_from, read_to);
     const uint32_t xcap = (uint32_t)std::min<uint64_t>(c->max_rec, p->max_read_size);
     const uint32_t ycap = (uint32_t)std::min<uint64_t>(ymax, p->max_read_size);
     if (!imsame_gaps_in_range(p->igap, p->egap, xcap, ycap)) return IMSAME_E_RANGE;
@@ -1103,7 +1147,7 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
     c->paths_split = false;
     const uint64_t n = read_to - read_from;
     uint64_t ymax = 0;
-    for (uint64_t r = read_from; r < read_to; ++r) ymax = std::max<uint64_t>(ymax, hqs(c, r + 1) - hqs(c, r));
+    ymax = range_ymax(c, read_from, read_to);
     // LANES: the range is cut into `nl` parts that run concurrently on nl
     // streams (this context and c->subs, which share the index and the
     // query), so one part's latency-bound phases -- seed scans, the last
@@ -1133,6 +1177,8 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
         L[k]->origin = c->origin;
         L[k]->nw_iv.clear();
     }
+
+
     std::vector<uint64_t> cut(nl + 1), used(nl, 0);
     for (int k = 0; k <= nl; ++k) cut[k] = read_from + n * (uint64_t)k / (uint64_t)nl;
     std::vector<imsame_stats> S(nl);
@@ -1264,9 +1310,7 @@ extern "C" int imsame_dev_align_windows(imsame_ctx *c, uint64_t read_from, uint6
     if (win_cap) HIPCHK(hipMemcpyAsync(c->wcap.p, win_cap, (uint64_t)n * 8, hipMemcpyHostToDevice, c->stream));
     else         HIPCHK(hipMemsetAsync(c->wcap.p, 0xFF, (uint64_t)n * 8, c->stream));
     HIPCHK(hipMemsetAsync(c->wout.p, 0xFF, (uint64_t)n * 8, c->stream));
-    uint64_t ymax = 0;
-    for (uint64_t r = read_from; r < read_to; ++r)
-        ymax = std::max<uint64_t>(ymax, hqs(c, r + 1) - hqs(c, r));
+    const uint64_t ymax = range_ymax(c, read_from, read_to);
     c->ev_db_len = ev_db_len;
     c->use_wcap = true;
     c->use_wstart = win_start != nullptr;
@@ -1313,8 +1357,7 @@ extern "C" int imsame_dev_align_sliced(imsame_ctx *c, const uint8_t *db_seq, uin
     auto rec_end = [&](uint64_t k) { return k + 1 < n_db ? db_start[k + 1] : db_len; };
     uint64_t max_rec = 0, ymax = 0;
     for (uint64_t k = 0; k < n_db; ++k) max_rec = std::max<uint64_t>(max_rec, rec_end(k) - db_start[k]);
-    for (uint64_t r = read_from; r < read_to; ++r)
-        ymax = std::max<uint64_t>(ymax, hqs(c, r + 1) - hqs(c, r));
+    ymax = range_ymax(c, read_from, read_to);
     if (max_rec > p->max_read_size || ymax > p->max_read_size) return IMSAME_E_ARG;
     // slices: record ranges [lo, hi), top down, each <= slice_bases (>= 1 record)
     std::vector<std::pair<uint64_t, uint64_t>> sl;
