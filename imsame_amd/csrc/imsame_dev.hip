@@ -292,6 +292,8 @@ struct imsame_ctx {
     // NW launch intervals (ms since the call's origin event) for the busy time
     hipEvent_t origin = nullptr;
     std::vector<std::pair<float, float>> nw_iv;
+    int nlanes = 1;                   // lanes of the running call (the seed scan's group size
+                                      // follows the reads scanned across all of them)
 };
 
 static inline uint64_t hqs(const imsame_ctx *c, uint64_t r) { return c->hq[r - c->q_lo]; }
@@ -1000,7 +1002,11 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         S.minlen = c->minlen.as<uint32_t>(); S.n_minlen = ymax + 1;
         S.minident = c->minident.as<uint32_t>(); S.n_minident = xcap + ymax + 2;
         const char *l_env = getenv(st.rounds == 1 && getenv("IMSAME_SEED_L1") ? "IMSAME_SEED_L1" : "IMSAME_SEED_L");
-        const int L = l_env ? atoi(l_env) : seed_lanes(nact);
+        // group size from the reads the device scans at once: this lane's
+        // times the call's lanes (C2, 8 lanes of 125k: 4 lanes per read in
+        // round 1 instead of 16, whose extra windows a true read never needs;
+        // +1.9 %, profiles/r2am_*)
+        const int L = l_env ? atoi(l_env) : seed_lanes((uint32_t)std::min<uint64_t>((uint64_t)nact * c->nlanes, 0xFFFFFFFFu));
         const size_t slds = 256 * SEED_LDS_PER_LANE;
         HIPCHK(hipEventRecord(c->ev0, s));
         if (L >= 16)     seed_group_kernel<16><<<nblk((uint64_t)nact * 16, 256), 256, slds, s>>>(S);
@@ -1177,6 +1183,7 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
         L[k]->origin = c->origin;
         L[k]->nw_iv.clear();
     }
+    for (int k = 0; k < nl; ++k) L[k]->nlanes = nl;
 
 
     std::vector<uint64_t> cut(nl + 1), used(nl, 0);
@@ -1192,6 +1199,7 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
     R[0] = align_one(c, cut[0], cut[1], n_threads_semantic, p, res, nullptr, 0, &used[0], &S[0]);
     for (auto &t : th) t.join();
     for (int k = 1; k < nl; ++k) L[k]->origin = nullptr;
+    for (int k = 0; k < nl; ++k) L[k]->nlanes = 1;
     for (int r : R)
         if (r && r != IMSAME_E_PATHS && r != IMSAME_E_READ_TOO_LONG) return r;
     int ret = IMSAME_OK;

@@ -305,9 +305,10 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint
 // LDS: SEED_LDS_PER_LANE bytes per lane (the lane's list).
 #define SEED_LDS_PER_LANE (SPEC_MAX * 8)
 // lanes per read: enough lanes in flight to hide the probe latency
-// (~2M lanes) without scanning many windows a read will not reach
+// (~1-4M lanes) without scanning many windows a read will not reach; nact =
+// the reads the device scans at once (all lanes of a call)
 __host__ __device__ static inline int seed_lanes(uint32_t nact) {
-    return nact >= 1000000u ? 1 : nact >= 250000u ? 4 : 16;
+    return nact >= 2000000u ? 1 : nact >= 750000u ? 4 : 16;
 }
 
 __device__ __forceinline__ uint32_t kmer_code_at(const uint8_t *__restrict__ q, uint64_t p) {
