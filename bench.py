@@ -391,7 +391,8 @@ def run_e2e(ref, rst, q, qs, a):
         need = 4 * 1024 ** 3                         # ~3.3 KB of text per accepted read at C2
         out = outf if free > need else "/dev/null"
         t0 = time.monotonic()
-        p = subprocess.run([cli, "-query", qf, "-db", dbf, "-out", out, "-n_threads", str(a.n_threads)],
+        extra = os.environ.get("IMSAME_E2E_ARGS", "").split()          # experiments, e.g. -batch_reads N
+        p = subprocess.run([cli, "-query", qf, "-db", dbf, "-out", out, "-n_threads", str(a.n_threads)] + extra,
                            stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=900)
         wall = time.monotonic() - t0
         m = re.search(rb"\[imsame\] phases (\{.*\})", p.stderr)

@@ -25,6 +25,8 @@ for s in $STEPS; do
            ok_or_stop $? bench ;;
     e2e) timeout -k 10 900 python -u bench.py --cpu-sample 0 --steps 1 > gpurun_out/bench_e2e_${TAG}.json \
            2> gpurun_out/bench_e2e_${TAG}.err; ok_or_stop $? e2e ;;
+    e2eb*) BR=${s#e2eb}; IMSAME_E2E_ARGS="${BR:+-batch_reads $BR}" timeout -k 10 900 python -u bench.py --cpu-sample 0 --steps 1 \
+           --warmup 0 --e2e on > gpurun_out/bench_${s}_${TAG}.json 2> gpurun_out/bench_${s}_${TAG}.err; ok_or_stop $? $s ;;
     benchq) timeout -k 10 600 python -u bench.py --cpu-sample 0 --e2e off > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err
            ok_or_stop $? benchq ;;
     seedl*) L=${s#seedl}; IMSAME_SEED_L1=$L timeout -k 10 600 python -u bench.py --cpu-sample 0 --e2e off \
