@@ -640,6 +640,26 @@ def test_c5_full_50mbp_database(dev, oracle_memo, rec_bp, cap):
         assert st.n_nw == 0 and st.n_hits == 0 and (res["status"] == 1).sum() == 0
 
 
+def test_eight_skewed_lanes_equal_one_lane(dev, monkeypatch):
+    """8 lanes (the default from 1M reads) cut with skewed shares (weights
+    0.6 .. 1.4, imsame_dev_align) on their own hardware queues: the same rows
+    as one lane, and the same rows at skew 0.9 (the smallest lane 1/8 of the
+    average)."""
+    ref, rst = synth.make_reference_arr(3_000_000, 2_000, seed=71)
+    q, qs = synth.make_reads_arr(ref, 320_000, 150, seed=72)
+    dev.index(ref, rst)
+    dev.set_query(q, qs)
+    monkeypatch.setenv("IMSAME_LANES", "1")
+    one, _, s1 = dev.align(n_threads=16)
+    monkeypatch.setenv("IMSAME_LANES", "8")
+    eight, _, s8 = dev.align(n_threads=16)
+    assert s1.lanes == 1 and s8.lanes == 8
+    assert not _cmp(eight, one), _cmp(eight, one)
+    monkeypatch.setenv("IMSAME_LANE_SKEW", "0.9")
+    sk, _, _ = dev.align(n_threads=16)
+    assert not _cmp(sk, one), _cmp(sk, one)
+
+
 def test_lanes_equal_one_lane(dev, monkeypatch):
     """Three concurrent lanes (parts of a call on three streams) against one
     lane: identical per-read rows and identical .align text for every
