@@ -245,8 +245,9 @@ struct imsame_ctx {
     // and base numbers through the biased views dev_q / dev_qs.
     DBuf q, q_start;
     uint64_t n_q = 0, q_len = 0, q_lo = 0, q_hi = 0, q_base = 0, q_lo_first = 0;
-    std::vector<uint64_t> h_q_start;  // starts of reads q_lo .. q_hi
-    const uint64_t *hq = nullptr;     // = h_q_start.data(), or the parent's for a lane
+    uint64_t *h_q_start = nullptr;    // starts of reads q_lo .. q_hi, page-locked (the
+    uint64_t h_q_cap = 0;             // H2D copy of them runs asynchronously)
+    const uint64_t *hq = nullptr;     // = h_q_start, or the parent's for a lane
     std::vector<uint32_t> h_q_bmax;   // longest read of each QB_READS block from q_lo (range_ymax)
     const uint32_t *hqb = nullptr;    // = h_q_bmax.data(), or the parent's for a lane
     bool have_query = false;
@@ -410,6 +411,7 @@ extern "C" void imsame_dev_close(imsame_ctx *c) {
     if (c->origin && !c->is_sub) (void)hipEventDestroy(c->origin);     // a lane borrows its parent's
     if (!c->is_sub)
         for (hipEvent_t e : c->q_part_ev) (void)hipEventDestroy(e);
+    if (!c->is_sub && c->h_q_start) (void)hipHostFree(c->h_q_start);
     (void)hipStreamDestroy(c->stream);
     (void)hipStreamDestroy(c->ustream);
     delete c;
@@ -559,25 +561,56 @@ extern "C" int imsame_dev_set_query_range_async(imsame_ctx *c, const uint8_t *q_
     // IMSAME_E_ARG), the host copy, every length a multiple of NW16_K?, and
     // the longest read of each QB_READS block (range_ymax)
     const uint64_t m = read_to - read_from;
-    c->h_q_start.resize(m + 1);
-    c->h_q_bmax.assign(m / QB_READS + 1, 0);
-    uint64_t *h = c->h_q_start.data();
-    uint32_t *bm = c->h_q_bmax.data();
-    uint64_t prev = qs(read_from);
-    bool ok = prev <= q_len, mult = true;
-    h[0] = prev;
-    for (uint64_t k = 1; k <= m; ++k) {
-        const uint64_t v = read_from + k < n_q ? q_start[read_from + k] : q_len;
-        const uint64_t len = v - prev;
-        ok &= v >= prev;
-        mult &= len % NW16_K == 0;
-        bm[(k - 1) / QB_READS] = std::max<uint32_t>(bm[(k - 1) / QB_READS], (uint32_t)std::min<uint64_t>(len, 0xFFFFFFFFu));
-        h[k] = v;
-        prev = v;
+    if (c->h_q_cap < m + 1) {
+        if (c->h_q_start) HIPCHK(hipHostFree(c->h_q_start));
+        c->h_q_start = nullptr; c->h_q_cap = 0;
+        const uint64_t cap = (m + 1) + (m + 1) / 8 + 1024;
+        if (hipHostMalloc((void **)&c->h_q_start, cap * 8, hipHostMallocDefault) != hipSuccess) {
+            c->h_q_start = nullptr;
+            return IMSAME_E_OOM;
+        }
+        c->h_q_cap = cap;
     }
+    c->h_q_bmax.assign(m / QB_READS + 1, 0);
+    uint64_t *h = c->h_q_start;
+    uint32_t *bm = c->h_q_bmax.data();
+    h[0] = qs(read_from);
+    // reads k-1 (k = 1 .. m) in chunks of whole blocks, one host thread each
+    // (1M reads: ~1 ms on one core, on the critical path of every upload)
+    auto pass = [&](uint64_t k0, uint64_t k1, bool *okp, bool *multp) {
+        uint64_t prev = k0 == 1 ? h[0] : qs(read_from + k0 - 1);
+        bool ok = true, mult = true;
+        for (uint64_t k = k0; k < k1; ++k) {
+            const uint64_t v = read_from + k < n_q ? q_start[read_from + k] : q_len;
+            const uint64_t len = v - prev;
+            ok &= v >= prev;
+            mult &= len % NW16_K == 0;
+            uint32_t &b = bm[(k - 1) / QB_READS];
+            b = std::max<uint32_t>(b, (uint32_t)std::min<uint64_t>(len, 0xFFFFFFFFu));
+            h[k] = v;
+            prev = v;
+        }
+        *okp = ok; *multp = mult;
+    };
+    const uint64_t nblk_r = (m + QB_READS - 1) / QB_READS;
+    const int nt = (int)std::min<uint64_t>(8, (nblk_r + 15) / 16);      // >= 16 blocks per thread
+    bool okv[8] = {true, true, true, true, true, true, true, true}, mv[8] = {true, true, true, true, true, true, true, true};
+    if (nt <= 1) {
+        pass(1, m + 1, &okv[0], &mv[0]);
+    } else {
+        std::vector<std::thread> th;
+        for (int t = 0; t < nt; ++t) {
+            const uint64_t k0 = 1 + (nblk_r * t / nt) * QB_READS, k1 = std::min<uint64_t>(1 + (nblk_r * (t + 1) / nt) * QB_READS, m + 1);
+            th.emplace_back(pass, k0, k1, &okv[t], &mv[t]);
+        }
+        for (auto &x : th) x.join();
+    }
+    bool ok = h[0] <= q_len, mult = true;
+    for (int t = 0; t < 8; ++t) { ok = ok && okv[t]; mult = mult && mv[t]; }
+    const uint64_t prev = h[m];
     if (!ok || prev > q_len) return IMSAME_E_ARG;                   // starts ascend within the query
     c->n_q = n_q; c->q_len = q_len; c->q_lo = read_from; c->q_hi = read_to;
-    c->hq = c->h_q_start.data();
+    c->hq = c->h_q_start;
     c->hqb = c->h_q_bmax.data();
     // reads q_lo_first .. read_from-1 are empty (start where read_from starts)
     uint64_t f = read_from;
@@ -596,7 +629,7 @@ extern "C" int imsame_dev_set_query_range_async(imsame_ctx *c, const uint8_t *q_
     c->q_part_end.assign(Q_PARTS, 0);
     // on the upload stream: every lane (this context's stream included) waits
     // only for the parts that hold its reads
-    HIPCHK(hipMemcpyAsync(c->q_start.p, c->h_q_start.data(), ns * 8, hipMemcpyHostToDevice, c->ustream));
+    HIPCHK(hipMemcpyAsync(c->q_start.p, c->h_q_start, ns * 8, hipMemcpyHostToDevice, c->ustream));
     HIPCHK(hipMemsetAsync((uint8_t *)c->q.p + nb, 0, 64, c->ustream));
     for (uint64_t k = 0, a = 0; k < Q_PARTS; ++k) {      // bases [q_base + a, q_base + b)
         const uint64_t b = nb * (k + 1) / Q_PARTS;
