@@ -710,8 +710,8 @@ struct NwPlan { int G, GPW, xcap, xstride, steps, nstr; bool pk, last4, two; siz
 
 // Rows above its best cell the second nw16 sweep keeps (nw16_kernel.hip).  A
 // path longer than that (rare: C2 paths span <= 209 rows) makes its wave redo
-// the sweep from row 1.  IMSAME_NW_BAND overrides (tests use tiny bands to
-// drive the redo path).
+// the sweep over 4 bands, then from row 1.  IMSAME_NW_BAND overrides (tests
+// use tiny bands to drive the redo path).
 static int nw16_band_rows() {
     const char *e = getenv("IMSAME_NW_BAND");
     return e ? std::max(0, atoi(e)) : 200;
@@ -1201,7 +1201,9 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
     // 1/8 1-3 % faster with 3 lanes than 2, r2w_*, and no clear gain from 4-6
     // lanes there, r2ac_*)
     int nl = le ? std::max(1, std::min(8, atoi(le))) : (n >= 1000000 ? 8 : 3);
-    while (nl > 1 && n < (uint64_t)nl * LANE_MIN) --nl;
+    const char *lme = getenv("IMSAME_LANE_MIN");
+    const uint64_t lane_min = lme ? strtoull(lme, nullptr, 10) : LANE_MIN;
+    while (nl > 1 && n < (uint64_t)nl * lane_min) --nl;
     if (c->is_sub || c->use_wcap || ymax > (uint64_t)NW_W / 2) nl = 1;
     if (nl == 1) {
         const int rc = align_one(c, read_from, read_to, n_threads_semantic, p, res, paths, paths_cap, paths_used,

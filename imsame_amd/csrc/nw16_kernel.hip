@@ -48,8 +48,9 @@
 // best cell, per half (its own rows: two LDS row reads and per-half row masks),
 // and writes the traceback of those ~band_w + NW16_CK + G steps only.  The
 // walk reads only rows the second sweep wrote (TbAcc16::has); a path that
-// leaves them is LOST and the wave redoes the second sweep from row 1 for it
-// (same values: the state restored is the state the first sweep had).  The
+// leaves them is LOST and the wave redoes the second sweep over 4 bands, then
+// from row 1 (same values: the state restored is the state the first sweep
+// had).  The
 // move bits and their packing are 6 of the 23 instructions per cell pair, so
 // the first sweep issues ~190 VALU per step instead of 250, and ~90 % of the
 // steps are first-sweep steps at C2 (2000-row records, 150-column reads).
@@ -80,6 +81,7 @@
 #define NW16_WIN_DOWN 24          // ... and below the predicted last row
 #define NW16_WIN_MAX 448          // longest window (steps) a wave writes in its first sweep
 #define NW16_WIN_BOTTOM 40        // rows above the last one for an unpredicted candidate
+#define NW16_BAND2 4              // the second sweep's retry band, in bands
 
 // does the launch fit the int16 path?  (all gap terms non-positive)
 __host__ static inline bool nw16_fits(int64_t ig, int64_t eg, uint64_t xcap, uint64_t ymax) {
@@ -563,12 +565,13 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
             in0 = MASK ? wv_bfi(pm, in1, sN) : sN;
             outT = cur[K - 1]; outMS = mfS; outL = l0;
         };
-        for (int att = wv_any(todo[0] || todo[1]) ? 0 : 2; att < 2; ++att) {
-            // attempt 0: the band; attempt 1 (a path left it): every half from the start
+        for (int att = wv_any(todo[0] || todo[1]) ? 0 : 3; att < 3; ++att) {
+            // attempt 0: the band; 1 (a path left it): NW16_BAND2 x the band;
+            // 2: every half from the start
             int n2 = 0;
             for (int h = 0; h < 2; ++h) {
-                const int lo = bx[h] - P.band_w - 1;
-                t0h[h] = (att == 0 && lo >= 0) ? 1 + NW16_CK * (lo / NW16_CK) : 1;
+                const int lo = bx[h] - (att == 0 ? P.band_w : NW16_BAND2 * P.band_w) - 1;
+                t0h[h] = (att < 2 && lo >= 0) ? 1 + NW16_CK * (lo / NW16_CK) : 1;
                 if (todo[h]) n2 = max(n2, bx[h] + G - t0h[h]);
             }
             for (int o = 32; o > 0; o >>= 1) n2 = max(n2, wv_shfl_xor(n2, o));

@@ -124,8 +124,9 @@ typedef struct imsame_stats {
     double   ms_nw_busy;    /* wall time the device ran NW launches (union of
                                the launch intervals of all lanes)        */
     uint64_t lanes;         /* concurrent lanes the call ran (1-8)     */
-    uint64_t nw_redo;       /* two-pass NW: waves whose traceback band missed a
-                               path and redid their second sweep from row 1 */
+    uint64_t nw_redo;       /* two-pass NW: second-sweep retries of waves whose
+                               traceback band missed a path (4 bands, then
+                               from row 1)                                  */
     uint64_t launch_pk;     /* bit k: NW launch k ran the packed int16 kernel
                                (nw16_kernel), else the int32 nw_kernel     */
     uint64_t nw_win;        /* two-pass NW: candidates whose path was walked in
