@@ -22,7 +22,7 @@ MAX_READ_SIZE = 3000
 ALIGN_LEN = 60
 
 MOVE_DIAG, MOVE_UP, MOVE_LEFT = 0, 1, 2
-LAUNCH_STATS = 16        # IMSAME_LAUNCH_STATS
+LAUNCH_STATS = 64        # IMSAME_LAUNCH_STATS
 
 
 class Params(C.Structure):

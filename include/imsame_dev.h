@@ -97,7 +97,7 @@ typedef struct imsame_read_result {
 #define IMSAME_MOVE_UP   1u   /* one jump of n rows: X[px..px-n+1] vs '-'      */
 #define IMSAME_MOVE_LEFT 2u   /* one jump of n cols: '-' vs Y[py..py-n+1]      */
 
-#define IMSAME_LAUNCH_STATS 16
+#define IMSAME_LAUNCH_STATS 64
 typedef struct imsame_stats {
     uint64_t n_reads;       /* reads processed                       */
     uint64_t n_accepted;    /* reads accepted                        */
