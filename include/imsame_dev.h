@@ -144,7 +144,11 @@ int  imsame_dev_count(void);
 
 /* Open device `device` (HIP ordinal).  Fails with IMSAME_E_HIP if no GPU.
  * Several contexts may be opened on one device (each owns its own stream
- * and buffers). */
+ * and buffers).  imsame_dev_count / imsame_dev_open set GPU_MAX_HW_QUEUES=8
+ * when the variable is unset, before their first HIP call: a large call's 8
+ * lanes then get a hardware queue each (with HIP's default 4, two lanes share
+ * a queue and serialize).  A host program that starts HIP itself first should
+ * set it (<= 32) before doing so; results never depend on it. */
 int  imsame_dev_open(int device, imsame_ctx **out);
 void imsame_dev_close(imsame_ctx *ctx);
 const char *imsame_strerror(int code);
