@@ -439,13 +439,18 @@ __device__ void nw_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const u
             nw_sweep<false, false>(P, cd, tbw, bnd, 0, lane, gl, G, xmax, cvalid, bestR, bestRj, bestC, bestCi);
         } else {
             for (int st = 0; st < nstr; ++st) {
+                // a read of one strip in a multi-strip launch has no seam at all
+                // (its lead lane is column 0: reading the seam buffer there took
+                // whatever an earlier candidate or allocation left in it)
                 const bool in = st > 0, outs = st + 1 < nstr;
                 if (!in && outs)
                     nw_sweep<false, true>(P, cd, tbw, bnd, st, lane, gl, G, xmax, cvalid, bestR, bestRj, bestC, bestCi);
                 else if (in && outs)
                     nw_sweep<true, true>(P, cd, tbw, bnd, st, lane, gl, G, xmax, cvalid, bestR, bestRj, bestC, bestCi);
-                else
+                else if (in)
                     nw_sweep<true, false>(P, cd, tbw, bnd, st, lane, gl, G, xmax, cvalid, bestR, bestRj, bestC, bestCi);
+                else
+                    nw_sweep<false, false>(P, cd, tbw, bnd, st, lane, gl, G, xmax, cvalid, bestR, bestRj, bestC, bestCi);
                 wv_mem_sync();                    // seam written by the last lane, read by the lead
             }
         }

@@ -238,6 +238,20 @@ def test_c1_shape_vs_oracle(dev, oracle):
     assert not _cmp(res, exp), _cmp(res, exp)
 
 
+def test_single_strip_reads_in_multi_strip_launch(dev, oracle):
+    """163- and 400-column reads in one launch (multi-strip kernel): the
+    one-strip reads read no seam (round 1 did, and failed when the seam
+    buffer held large stale values)."""
+    from tests.test_host import _strip_mix_pairs
+    X, Y = _strip_mix_pairs()
+    for _ in range(3):
+        res, _, _ = dev.nw_pairs(X, Y, dev.params())
+        for k in range(len(X)):
+            o = oracle.nw(X[k], Y[k], text=False)
+            for f in ("score", "bx", "by", "length", "identities", "igaps", "egaps", "head_x", "head_y"):
+                assert int(res[k][f]) == int(o[f]), (f, k, len(Y[k]))
+
+
 def test_long_reads_multi_strip(dev, oracle):
     """Reads longer than one strip (320 columns): 600-2500 bp vs 3 kbp records."""
     ref, rst = synth.make_reference_arr(300_000, 3_000, seed=9)

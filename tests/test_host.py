@@ -217,6 +217,37 @@ def test_emulated_predicted_traceback_window(emu, oracle, seed_l, monkeypatch):
         assert np.array_equal(got0[f], exp[f]), f
 
 
+def _strip_mix_pairs():
+    """163- and 400-column reads in ONE launch: the launch takes the
+    multi-strip kernel (ymax > 320) and the 163-column reads have one strip."""
+    rng = np.random.default_rng(3)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    X, Y = [], []
+    for k in range(6):
+        xl = 359 if k == 0 else int(rng.integers(300, 600))
+        yl = 163 if k % 2 == 0 else 400
+        x = acgt[rng.integers(0, 4, xl)]
+        o0 = int(rng.integers(0, max(1, xl - yl)))
+        y = np.concatenate([x[o0:o0 + yl], acgt[rng.integers(0, 4, max(0, yl - (xl - o0)))]])[:yl].copy()
+        m = rng.random(yl) < 0.05
+        y[m] = acgt[rng.integers(0, 4, int(m.sum()))]
+        X.append(x.tobytes()); Y.append(y.tobytes())
+    return X, Y
+
+
+def test_emulated_single_strip_reads_in_multi_strip_launch(emu, oracle):
+    """nw_kernel.hip MULTI: a read of one strip has no seam (its lead lane is
+    column 0).  The emulator's seam buffer is poisoned like fresh device
+    memory, so a read of it shows (round 1 read it: wrong scores there)."""
+    X, Y = _strip_mix_pairs()
+    rc, res, _, fl = emu.nw_pairs(X, Y, oracle.params())
+    assert rc == 0 and fl == 0
+    for k in range(len(X)):
+        o = oracle.nw(X[k], Y[k], text=False)
+        for f in ("score", "bx", "by", "length", "identities", "igaps", "egaps", "head_x", "head_y"):
+            assert int(res[k][f]) == int(o[f]), (f, k, len(Y[k]))
+
+
 def _emu_ungapped(emu, db, dbs, q, qs, pd0, pq0, read, sid):
     f = emu.lib.emu_ungapped
     f.restype = C.c_uint64
