@@ -223,6 +223,10 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
     const uint32_t budget1 = bud_env ? (uint32_t)std::max(0, atoi(bud_env)) : SEED_BUDGET1;
     std::vector<uint8_t> nmemo(n), rstat(n);
     std::vector<imsame_read_result> o1(n), o2(n);
+    // per-candidate results poisoned like reused device buffers: a candidate the
+    // NW kernels leave unwritten shows
+    memset(o1.data(), 0xEE, o1.size() * sizeof(imsame_read_result));
+    memset(o2.data(), 0xEE, o2.size() * sizeof(imsame_read_result));
     InitLaunch I = {qsv.data(), read_from, n, res, cur_p.data(), cur_h.data(), nmemo.data(), rstat.data(), act.data()};
     for (uint32_t k = 0; k < n; ++k) init_one(I, k);
     uint32_t nc[3] = {0, 0, 0}, pused = 0, flags = 0;
