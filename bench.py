@@ -250,11 +250,11 @@ def main():
     n_nw = sum(s["n_nw"] for s in stats)
     seq_bytes = n_nw * (a.record_bp + a.read_len)
     alg_bytes = 2 * cells + seq_bytes
-    # achieved: algorithmic bytes / the time the device ran NW launches.  With
-    # two lanes, launches of the two halves overlap: the per-launch average
-    # (avg_launch_ms, what rocprofv3 --stats reports) times the launches
-    # exceeds that time by launch_overlap (scripts/nw_busy.py recomputes the
-    # union from the kernel trace)
+    # achieved: algorithmic bytes / the time the device ran NW launches.  The
+    # lanes' launches overlap: the per-launch average (avg_launch_ms; what
+    # rocprofv3 --stats reports per kernel: kernel_avg_launch_ms) times the
+    # launches exceeds that time by launch_overlap (scripts/nw_busy.py
+    # recomputes the union from the kernel trace)
     achieved = alg_bytes / (nw_busy / 1e3) / 1e9 if nw_busy else 0.0
     kernel = nw_kernel_name(a.read_len, a.record_bp) if not stats[-1]["nw_launches"] or a.read_len <= 160 \
         else "nw_kernel"

@@ -284,9 +284,9 @@ struct imsame_ctx {
     uint64_t ev_db_len = 0;          // 0: db_len
     bool use_wcap = false, use_wstart = false;
     DBuf wcap, wout, wstart;
-    // second LANE: a context sharing this one's index and query (aliased
-    // buffers), with its own stream and per-read state, so one call's two
-    // halves run concurrently (see imsame_dev_align)
+    // LANES 1, 2, ...: contexts sharing this one's index and query (aliased
+    // buffers), each with its own stream and per-read state, so the parts of
+    // one call run concurrently (see imsame_dev_align)
     std::vector<imsame_ctx *> subs;   // lanes 1, 2, ...
     bool is_sub = false, paths_split = false;
     std::vector<uint64_t> lane_paths; // path entries of lanes 1, 2, ... after a split call
@@ -1181,7 +1181,7 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
     if (p->want_paths && !paths && paths_cap) return IMSAME_E_ARG;
     HIPCHK(hipSetDevice(c->device));
     if (!c->origin) HIPCHK(hipEventCreate(&c->origin));
-    HIPCHK(hipEventRecord(c->origin, c->stream));          // common clock of both lanes' NW launches
+    HIPCHK(hipEventRecord(c->origin, c->stream));          // common clock of every lane's NW launches
     c->nw_iv.clear();
     c->paths_split = false;
     const uint64_t n = read_to - read_from;

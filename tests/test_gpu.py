@@ -290,7 +290,7 @@ def test_full_c2_reference_properties(dev, oracle):
     assert st.lanes == 3                      # three parts ran concurrently
     acc = res["status"] == 1
     assert acc.mean() > 0.85
-    # every accepted path re-renders to the device's own identity count (both lanes)
+    # every accepted path re-renders to the device's own identity count (all lanes)
     ka = np.flatnonzero(acc)
     for k in np.concatenate([ka[:1000], ka[ka >= len(qs) // 2][:1000]]):
         r = res[k]
