@@ -29,10 +29,11 @@ import time
 import numpy as np
 
 # one hardware queue per alignment lane: HIP maps a process's streams onto
-# GPU_MAX_HW_QUEUES queues (4 on the GPU boxes), and two of the 8 lanes on one
-# queue serialize (imsame_dev.hip:hw_queues_hint, which asks for 8 only when
-# the variable is unset).  The benchmark raises it to 8 before anything starts
-# HIP (torch does in a multi-rank run); results do not depend on it.
+# GPU_MAX_HW_QUEUES queues (4 on the GPU boxes when unset), two lanes on one
+# queue serialize, and the library runs at most one lane per queue
+# (imsame_dev.hip:lanes_for_queues; it never sets the variable itself).  The
+# benchmark, as a host program, asks for 8 before anything starts HIP (torch
+# does in a multi-rank run); results do not depend on it.
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
     os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
@@ -117,13 +118,16 @@ def parse():
     ap.add_argument("--upload", choices=("async", "sync"), default="async",
                     help="query H2D per step: queued in parts that each lane waits for (async) or waited for "
                          "before the alignment (sync); inside the timed step either way")
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "nw_traffic.json"))
-    ap.add_argument("--valu-json", default=os.path.join(REPO, "profiles", "nw_valu.json"))
+    ap.add_argument("--traffic-json", default=None, help="PMC bytes per cell (default profiles/nw_traffic[_CONFIG].json)")
+    ap.add_argument("--valu-json", default=None, help="PMC VALU per cell (default profiles/nw_valu[_CONFIG].json)")
     a = ap.parse_args()
     cfg = CONFIGS[a.config]
     for k in ("reads", "read_len", "ref_bp", "record_bp", "cpu_sample"):
         if getattr(a, k) is None:
             setattr(a, k, cfg[k])
+    sfx = "" if a.config == "c2" else "_" + a.config       # scripts/pmc_r2.py writes them per config
+    a.traffic_json = a.traffic_json or os.path.join(REPO, "profiles", f"nw_traffic{sfx}.json")
+    a.valu_json = a.valu_json or os.path.join(REPO, "profiles", f"nw_valu{sfx}.json")
     return a
 
 
@@ -259,7 +263,7 @@ def main():
     kernel = nw_kernel_name(a.read_len, a.record_bp) if not stats[-1]["nw_launches"] or a.read_len <= 160 \
         else "nw_kernel"
     per_launch = alg_bytes / max(nw_launches, 1)
-    traffic = None
+    traffic = bpc = None
     if os.path.exists(a.traffic_json):
         try:
             tj = json.load(open(a.traffic_json))
@@ -269,28 +273,46 @@ def main():
                 bpc = tj.get("hbm_bytes_per_cell")
                 traffic = int(bpc * cells / max(nw_launches, 1)) if bpc else None
         except Exception:
-            traffic = None
+            traffic = bpc = None
     cells_per_s = cells / (nw_busy / 1e3) if nw_busy else 0.0
     # launches of the dominant kernel alone (imsame_stats.launch_pk: packed
     # nw16_kernel vs the int32 nw_kernel that takes the small last launches),
     # the average rocprofv3 --stats reports for that kernel name
     pk_ms = [m for s_ in stats for j, m in enumerate(s_["launch_ms"])
              if ((s_["launch_pk"] >> j) & 1) == (1 if kernel == "nw16_kernel" else 0)]
-    roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "traffic_over_alg": round(traffic / per_launch, 4) if traffic and per_launch else None,
-                "kernel": kernel, "launches": nw_launches,
-                "avg_launch_ms": round(nw_ms / max(nw_launches, 1), 4),
-                "kernel_launches": len(pk_ms),
-                "kernel_avg_launch_ms": round(sum(pk_ms) / max(len(pk_ms), 1), 4),
-                "nw_busy_ms_per_step": round(nw_busy / a.steps, 3),
-                "launch_overlap": round(nw_ms / nw_busy, 3) if nw_busy else None,
-                "alg_bytes_per_launch": int(per_launch),
-                "cells_per_s": round(cells_per_s, 1),
-                "valu": valu_roofline(a.valu_json, kernel, a.config, cells_per_s)}
+    # HBM: the contract's algorithmic figure and the bytes the PMC counters saw
+    measured = bpc * cells_per_s / 1e9 if bpc and cells_per_s else None
+    hbm = {"basis": "algorithmic bytes (SURVEY 8(d): xlen + ylen + 2 B/cell traceback floor per NW) / NW busy time",
+           "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved / HBM_PEAK_GBS, 4),
+           "measured_gbs": round(measured, 2) if measured else None,
+           "measured_frac": round(measured / HBM_PEAK_GBS, 4) if measured else None,
+           "measured_basis": "PMC bytes per DP cell (2 x FETCH_SIZE + WRITE_SIZE, %s) x this run's cells/s of NW "
+                             "busy time" % os.path.relpath(a.traffic_json, REPO)}
+    valu = valu_roofline(a.valu_json, kernel, a.config, cells_per_s)
+    common = {"traffic": traffic,
+              "traffic_over_alg": round(traffic / per_launch, 4) if traffic and per_launch else None,
+              "kernel": kernel, "launches": nw_launches,
+              "avg_launch_ms": round(nw_ms / max(nw_launches, 1), 4),
+              "kernel_launches": len(pk_ms),
+              "kernel_avg_launch_ms": round(sum(pk_ms) / max(len(pk_ms), 1), 4),
+              "nw_busy_ms_per_step": round(nw_busy / a.steps, 3),
+              "launch_overlap": round(nw_ms / nw_busy, 3) if nw_busy else None,
+              "alg_bytes_per_launch": int(per_launch),
+              "cells_per_s": round(cells_per_s, 1)}
+    if valu:
+        # the NW kernel's binding resource is VALU issue: the
+        # headline bound; the contract's HBM figure stays under "hbm"
+        roofline = dict({"bound": "valu", "achieved": valu["achieved"], "peak": valu["issue_peak"],
+                         "unit": valu["unit"], "frac": valu["frac"]}, **common, valu=valu, hbm=hbm)
+    else:
+        roofline = dict({"bound": "hbm", "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": hbm["frac"]}, **common, valu=None, hbm=hbm)
 
-    cpu = None
+    cpu = parity = None
     if rank == 0 and world == 1 and a.cpu_sample > 0:
+        # the oracle as the checker: the timed run's own rows on three windows
+        parity = timed_parity(ref, rst, q, qs, res, lo, hi, a, params)
         if a.slice_bases:
             dev.index(ref, rst)                     # the sample is checked against the whole index
         cpu = cpu_baseline(dev, ref, rst, q, qs, a, params)
@@ -317,6 +339,7 @@ def main():
                        + ("" if world == 1 or a.dist_backend == "nccl" else
                           f"; REHEARSAL: {a.dist_backend} collectives, device {gpu} shared by all ranks")},
             "roofline": roofline,
+            "parity": parity,
             "cpu_baseline": cpu,
             "e2e": e2e,
             "detail": {"accepted_reads": accepted_all, "index_build_s": round(t_index, 3),
@@ -408,6 +431,22 @@ def run_e2e(ref, rst, q, qs, a):
         return ph
     finally:
         shutil.rmtree(td, ignore_errors=True)
+
+
+def timed_parity(ref, rst, q, qs, res, lo, hi, a, params):
+    """Part of the CPU-baseline leg (the oracle as the checker, outside the
+    timed region): the LAST TIMED STEP's own rows -- produced in exactly the
+    mode that gives `value` (lanes, queues, async upload) -- against the oracle
+    on three windows of the query (start, a -n_threads chunk head, end)."""
+    from tests import parity as P
+    from tests.oracle_bind import Oracle
+    o = Oracle.load()
+    po = o.params(max_read_size=params.max_read_size)
+    t0 = time.time()
+    out = P.check_windows(o, ref, rst, q, qs, res, lo, P.windows(lo, hi, len(qs), a.n_threads), a.n_threads, po)
+    out["oracle_s"] = round(time.time() - t0, 2)
+    out["rows_of"] = "the last timed step"
+    return out
 
 
 def cpu_baseline(dev, ref, rst, q, qs, a, params):

@@ -243,11 +243,11 @@ class Device:
         paths = np.zeros(max(cap, 1), dtype=np.uint32)
         rc = lib().imsame_dev_align(self._h, read_from, read_to, n_threads, C.byref(p), res.ctypes.data,
                                     paths.ctypes.data if want_paths else None, cap, C.byref(used), C.byref(st))
-        if rc == abi.IMSAME_E_PATHS:              # results complete; the paths wait on the device
-            paths = self.fetch_paths(used.value)
-            rc = 0
-        if rc and not (rc == abi.IMSAME_E_READ_TOO_LONG and allow_too_long):
+        if rc and not (rc in (abi.IMSAME_E_PATHS, abi.IMSAME_E_READ_TOO_LONG)
+                       and (rc == abi.IMSAME_E_PATHS or allow_too_long)):
             raise ImsameError(rc, "imsame_dev_align")
+        if want_paths and used.value > cap:       # not copied (E_PATHS or E_READ_TOO_LONG): on the device
+            paths = self.fetch_paths(used.value)
         return res, paths[:used.value], st
 
     def align_windows(self, ev_db_len, win_cap=None, read_from=None, read_to=None, n_threads=4, params=None,
@@ -295,11 +295,10 @@ class Device:
                                            slice_bases, read_from, read_to, n_threads, C.byref(p),
                                            res.ctypes.data, paths.ctypes.data if want_paths else None, cap,
                                            C.byref(used), C.byref(ns), C.byref(st))
-        if rc == abi.IMSAME_E_PATHS:
-            paths = self.fetch_paths(used.value)
-            rc = 0
-        if rc:
+        if rc and rc != abi.IMSAME_E_PATHS:
             raise ImsameError(rc, "imsame_dev_align_sliced")
+        if want_paths and used.value > cap:
+            paths = self.fetch_paths(used.value)
         return res, paths[:used.value], st, ns.value
 
     def nw_pairs(self, X, Y, params=None, want_paths=False):

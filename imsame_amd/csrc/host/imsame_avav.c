@@ -178,6 +178,7 @@ static void load_rc(mgen *m, imsame_ctx *ctx) {
 }
 
 int main(int argc, char **argv) {
+    setenv("GPU_MAX_HW_QUEUES", "8", 0);     /* one hardware queue per lane (see imsame_cli.c) */
     /* positional arguments exactly as the script; options after them */
     int npos = 0, dry = 0;
     const char *pos[6] = {0}, *devspec = NULL;

@@ -66,6 +66,10 @@ static void usage(void) {
 }
 
 int main(int argc, char **argv) {
+    /* one hardware queue per alignment lane (include/imsame_dev.h: the library
+     * runs at most one lane per queue and never sets this itself); a value in
+     * the environment is kept.  Before the first HIP call. */
+    setenv("GPU_MAX_HW_QUEUES", "8", 0);
     const char *qpath = NULL, *dpath = NULL, *opath = NULL, *devspec = NULL;
     imsame_params prm;
     imsame_params_default(&prm);

@@ -319,10 +319,13 @@ static void *align_worker(void *a) {
             if (!rc)
                 rc = imsame_dev_align(w->d->ctx, b->from, b->to, w->o->T, w->prm, w->res + b->from, b->paths, cap,
                                       &used, &b->st);
-            if (rc == IMSAME_E_PATHS) {                /* results complete; fetch the paths */
+            /* paths not copied (IMSAME_E_PATHS, or a size abort whose paths did
+             * not fit either, include/imsame_dev.h): fetch them */
+            if ((rc == IMSAME_E_PATHS || rc == IMSAME_E_READ_TOO_LONG) && cap && used > cap) {
                 uint32_t *p = realloc(b->paths, (used + 1) * sizeof(uint32_t));
-                rc = p ? imsame_dev_fetch_paths(w->d->ctx, p, used, &used) : IMSAME_E_OOM;
+                const int rf = p ? imsame_dev_fetch_paths(w->d->ctx, p, used, &used) : IMSAME_E_OOM;
                 if (p) b->paths = p;
+                if (rc == IMSAME_E_PATHS || rf) rc = rf;
             }
         }
         b->npaths = used;
@@ -369,6 +372,12 @@ int pipe_align_render(pipe_dev *d, int G, const host_seqs *db, const host_seqs *
         total += nb[g];
     }
     batch *B = calloc((size_t)total + 1, sizeof *B);
+    const int nt = render_threads(o->render_threads);
+    rtask *rt = prm.want_paths ? calloc(2 * (size_t)nt, sizeof *rt) : NULL;       /* two buffer sets */
+    if (!B || (prm.want_paths && !rt)) {
+        free(B); free(rt); free(res);
+        return r->rc = IMSAME_E_OOM;
+    }
     worker W[PIPE_MAX_DEV];
     pthread_mutex_t mu = PTHREAD_MUTEX_INITIALIZER;
     pthread_cond_t cv = PTHREAD_COND_INITIALIZER;
@@ -390,8 +399,6 @@ int pipe_align_render(pipe_dev *d, int G, const host_seqs *db, const host_seqs *
     for (int g = 0; g < G; ++g)
         if (!started[g]) align_worker(&W[g]);
     /* walk the batches in read order: render each as it completes */
-    const int nt = render_threads(o->render_threads);
-    rtask *rt = prm.want_paths ? calloc(2 * (size_t)nt, sizeof *rt) : NULL;       /* two buffer sets */
     const int seekable = prm.want_paths && lseek(o->out_fd, 0, SEEK_CUR) >= 0;
     uint64_t off = seekable ? (uint64_t)lseek(o->out_fd, 0, SEEK_CUR) : 0;
     int rc = 0, werr = 0, nrend = 0;

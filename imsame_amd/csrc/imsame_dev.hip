@@ -21,6 +21,7 @@
 #include <vector>
 #include <algorithm>
 #include <thread>
+#include <mutex>
 #include "../../include/imsame_dev.h"
 
 #include "tables.h"
@@ -213,6 +214,19 @@ __global__ void row_scatter_kernel(const int32_t *row, uint32_t n, uint32_t nb, 
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
+// IMSAME_DEBUG_POISON=1: every device arena is filled with POISON_BYTE when it
+// is allocated and every per-call scratch arena again at the start of each
+// alignment call, so a kernel that reads memory it did not write this call
+// (the class of round 1's stale seam buffer) reads garbage
+// instead of a plausible leftover.  Debug only: results never depend on it.
+#define POISON_BYTE 0xA5
+static bool poison_on() {
+    static std::once_flag f;
+    static bool on = false;
+    std::call_once(f, [] { const char *e = getenv("IMSAME_DEBUG_POISON"); on = e && atoi(e); });
+    return on;
+}
+
 struct DBuf {
     void *p = nullptr; size_t cap = 0;
     int ensure(size_t n) {
@@ -222,7 +236,11 @@ struct DBuf {
         size_t want = n + std::min<size_t>(n / 8, (size_t)1 << 30) + 4096;   // slack for regrowth, <= 1 GB
         if (hipMalloc(&p, want) != hipSuccess) { p = nullptr; return IMSAME_E_OOM; }
         cap = want;
+        if (poison_on() && hipMemset(p, POISON_BYTE, want) != hipSuccess) return IMSAME_E_HIP;
         return 0;
+    }
+    int poison(hipStream_t s) const {
+        return p && poison_on() && hipMemsetAsync(p, POISON_BYTE, cap, s) != hipSuccess ? IMSAME_E_HIP : 0;
     }
     void release() { if (p) (void)hipFree(p); p = nullptr; cap = 0; }
     template <class T> T *as() const { return (T *)p; }
@@ -351,26 +369,34 @@ extern "C" const char *imsame_strerror(int code) {
     return "unknown error";
 }
 
-// Hardware queues per process: a call's lanes run on up to 8 streams, and
-// HIP maps streams onto GPU_MAX_HW_QUEUES queues (default 4), so two lanes
-// sharing a queue serialize (rocprofv3 trace, profiles/r2ag_*).  Asking for 8
-// before the process's first HIP call gives every lane its own queue (C2:
-// +2-3 %, profiles/r2ah_*, r2ai_*); a value the user set is kept, and a
-// process whose HIP runtime is already up (e.g. torch first) keeps its own.
-static void hw_queues_hint() {
-    setenv("GPU_MAX_HW_QUEUES", "8", 0);
+// Hardware queues: HIP maps a process's streams onto GPU_MAX_HW_QUEUES
+// hardware queues (4 when unset), and two lanes whose streams share a queue
+// serialize completely (rocprofv3 trace, profiles/r2ag_lane_timeline.txt).
+// The library never changes the variable (it is the host program's to set,
+// before its first HIP call: the imsame CLI and bench.py ask for 8); it reads
+// the value the runtime started with, once, and sizes its lanes to it.
+static int hw_queues() {
+    static std::once_flag f;
+    static int q = 4;
+    std::call_once(f, [] {
+        const char *e = getenv("GPU_MAX_HW_QUEUES");
+        const int v = e ? atoi(e) : 0;
+        q = v > 0 ? v : 4;
+    });
+    return q;
 }
 
+// Most lanes a call runs (imsame_dev_align): one per hardware queue, <= 8.
+#define LANES_MAX 8
+static int lanes_for_queues() { return std::max(1, std::min(LANES_MAX, hw_queues())); }
+
 extern "C" int imsame_dev_count(void) {
-    hw_queues_hint();
     int n = 0;
     return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
 }
 
-extern "C" int imsame_dev_open(int device, imsame_ctx **out) {
-    hw_queues_hint();
-    int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) return IMSAME_E_HIP;
+// A context with its compute stream (imsame_dev_open adds the upload stream).
+static int ctx_create(int device, imsame_ctx **out) {
     HIPCHK(hipSetDevice(device));
     imsame_ctx *c = new imsame_ctx();
     c->device = device;
@@ -378,10 +404,36 @@ extern "C" int imsame_dev_open(int device, imsame_ctx **out) {
     HIPCHK(hipGetDeviceProperties(&prop, device));
     c->ncu = prop.multiProcessorCount;
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    HIPCHK(hipStreamCreateWithFlags(&c->ustream, hipStreamNonBlocking));
     HIPCHK(hipEventCreate(&c->ev0));
     HIPCHK(hipEventCreate(&c->ev1));
     if (c->ctr.ensure(C_NSLOTS * 8)) { delete c; return IMSAME_E_OOM; }
+    *out = c;
+    return IMSAME_OK;
+}
+
+static int lane_add(imsame_ctx *c) {
+    imsame_ctx *l = nullptr;
+    const int rc = ctx_create(c->device, &l);
+    if (rc) return rc;
+    l->is_sub = true;
+    c->subs.push_back(l);
+    return 0;
+}
+
+extern "C" int imsame_dev_open(int device, imsame_ctx **out) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) return IMSAME_E_HIP;
+    imsame_ctx *c = nullptr;
+    int rc = ctx_create(device, &c);
+    if (rc) return rc;
+    // Stream creation order fixes the hardware queues: the runtime gives each
+    // new stream a queue of its own until GPU_MAX_HW_QUEUES are in use, then
+    // shares the least used one.  So the compute streams of this context and
+    // its lanes come first, one queue each, and the upload stream last, on the
+    // last lane's queue (that lane starts after the whole upload anyway).
+    for (int k = 1; k < lanes_for_queues() && !rc; ++k) rc = lane_add(c);
+    if (!rc && hipStreamCreateWithFlags(&c->ustream, hipStreamNonBlocking) != hipSuccess) rc = IMSAME_E_HIP;
+    if (rc) { imsame_dev_close(c); return rc; }
     *out = c;
     return IMSAME_OK;
 }
@@ -398,7 +450,7 @@ extern "C" void imsame_dev_close(imsame_ctx *c) {
     c->subs.clear();
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    (void)hipStreamSynchronize(c->ustream);
+    if (c->ustream) (void)hipStreamSynchronize(c->ustream);
     DBuf *bufs[] = {&c->db, &c->db_start, &c->off, &c->ent, &c->brk, &c->codes, &c->fill, &c->big, &c->q,
                     &c->q_start, &c->res, &c->cur_p, &c->cur_h, &c->memo, &c->nmemo, &c->rstat, &c->act0,
                     &c->act1, &c->cread, &c->csid, &c->cread2, &c->csid2, &c->cout, &c->cout2, &c->ctr,
@@ -412,19 +464,17 @@ extern "C" void imsame_dev_close(imsame_ctx *c) {
     if (!c->is_sub)
         for (hipEvent_t e : c->q_part_ev) (void)hipEventDestroy(e);
     if (!c->is_sub && c->h_q_start) (void)hipHostFree(c->h_q_start);
-    (void)hipStreamDestroy(c->stream);
-    (void)hipStreamDestroy(c->ustream);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->ustream) (void)hipStreamDestroy(c->ustream);
     delete c;
 }
 
-// Lane k >= 1 of c, aliasing c's index and query (not owned).
+// Lane k >= 1 of c, aliasing c's index and query (not owned).  Lanes beyond
+// the hardware queues (IMSAME_LANES) are added on demand and share queues.
 static int lane_sub(imsame_ctx *c, int k, imsame_ctx **out) {
     while ((int)c->subs.size() < k) {
-        imsame_ctx *l = nullptr;
-        int rc = imsame_dev_open(c->device, &l);
+        const int rc = lane_add(c);
         if (rc) return rc;
-        l->is_sub = true;
-        c->subs.push_back(l);
     }
     imsame_ctx *l = c->subs[k - 1];
     l->db = c->db; l->db_start = c->db_start; l->off = c->off; l->ent = c->ent; l->q = c->q; l->q_start = c->q_start;
@@ -481,6 +531,11 @@ extern "C" int imsame_dev_index(imsame_ctx *c, const uint8_t *db_seq, uint64_t d
         c->codes.ensure((db_len + 1) * 4) || c->off.ensure(((uint64_t)NBUCKETS + 1) * 8) ||
         c->fill.ensure((uint64_t)NBUCKETS * 4) || c->big.ensure((uint64_t)NBUCKETS * 4))
         return IMSAME_E_OOM;
+    {
+        const DBuf *scr[] = {&c->db, &c->codes, &c->off, &c->fill, &c->big, &c->ent};
+        for (const DBuf *b : scr)
+            if (int rc = b->poison(s)) return rc;
+    }
     if (db_len) HIPCHK(hipMemcpyAsync(c->db.p, db_seq, db_len, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(c->db_start.p, c->h_db_start.data(), (n_db + 1) * 8, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemsetAsync(c->brk.p, 0, nw * 4, s));
@@ -792,6 +847,11 @@ static int launch_nw(imsame_ctx *c, NwPlan pl, const uint32_t *cread, const uint
         if (pl.blocks == 1) return IMSAME_E_OOM;
         pl.blocks = (pl.blocks + 1) / 2;
     }
+    if (poison_on()) {                           // slots hold nothing from earlier launches
+        const DBuf *scr[] = {&c->tb, &c->ck, &c->bnd};
+        for (const DBuf *b : scr)
+            if (int rc = b->poison(s)) return rc;
+    }
     NwLaunch P;
     memset(&P, 0, sizeof P);
     P.db = dbp; P.db_start = dbs; P.q = qp; P.q_start = qs;
@@ -972,6 +1032,13 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         c->cout.ensure((uint64_t)n * 64) || c->cout2.ensure((uint64_t)n * 64) || c->cbase.ensure((uint64_t)n * 4) ||
         c->ccnt.ensure((uint64_t)n * 4) || c->perr.ensure((uint64_t)n * 4) || c->crow.ensure((uint64_t)n * 4))
         return IMSAME_E_OOM;
+    if (poison_on()) {                        // this call's scratch holds nothing it may read
+        const DBuf *scr[] = {&c->res, &c->cur_p, &c->cur_h, &c->memo, &c->nmemo, &c->rstat, &c->act0, &c->act1,
+                             &c->cread, &c->csid, &c->cread2, &c->csid2, &c->cout, &c->cout2, &c->cbase, &c->ccnt,
+                             &c->perr, &c->crow, &c->cperm, &c->rhist, &c->paths, &c->tb, &c->ck, &c->bnd};
+        for (const DBuf *b : scr)
+            if ((rc = b->poison(s))) return rc;
+    }
     // predicted rows for the packed kernel's first-sweep traceback windows:
     // OFF by default (IMSAME_NW_WINDOW=1 turns them on).  Measured at C2 they
     // cut the NW wave-cycles by 2 % but the whole step by -1..-3 %: the window
@@ -1170,6 +1237,7 @@ static double union_ms(std::vector<std::pair<float, float>> v) {
 
 // Reads per lane below which a call is not split (a lane must fill the chip)
 #define LANE_MIN 32768
+#define LANE_READS 40000
 
 extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64_t n_threads_semantic,
                                 const imsame_params *p, imsame_read_result *res, uint32_t *paths, uint64_t paths_cap,
@@ -1194,13 +1262,18 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
     // NW sweeps.  Per-read results do not depend on the cut (reads are
     // independent given the chunk heads).  Short reads only: a long-read
     // lane's traceback arena takes most of HBM.
+    // How many: from the work and the hardware queues.  A lane needs
+    // LANE_READS reads for its first NW launch to fill the chip's wave slots
+    // on its own (~0.9 candidates per read, 8 per wave: 40k reads -> 4.5k
+    // waves against 4 per SIMD x 1024 SIMDs), and a hardware queue of its own
+    // (lanes_for_queues).  C2 with 8 queues: 1M reads -> 8 lanes (+1.4 % over
+    // 4, profiles/r2ab_*), its 1/8 shard (125k) -> 3 (1-3 % faster than 2,
+    // r2w_*).  IMSAME_LANES overrides (tests, A/B runs).
     const char *le = getenv("IMSAME_LANES");
-    // default: 3 lanes, 8 from 1M reads on (profiles/r2h_*: 1M reads 6.81 /
-    // 6.86 / 6.91 M reads/s with 2 / 3 / 4 lanes; r2ab_*: 8 lanes +1.4 % over
-    // 4 in three alternating pairs, 5-6 lanes slower; C2 shards of 1/2, 1/4,
-    // 1/8 1-3 % faster with 3 lanes than 2, r2w_*, and no clear gain from 4-6
-    // lanes there, r2ac_*)
-    int nl = le ? std::max(1, std::min(8, atoi(le))) : (n >= 1000000 ? 8 : 3);
+    const char *lre = getenv("IMSAME_LANE_READS");
+    const uint64_t lane_reads = std::max<uint64_t>(1, lre ? strtoull(lre, nullptr, 10) : LANE_READS);
+    int nl = le ? std::max(1, std::min(LANES_MAX, atoi(le)))
+                : (int)std::max<uint64_t>(1, std::min<uint64_t>(lanes_for_queues(), n / lane_reads));
     const char *lme = getenv("IMSAME_LANE_MIN");
     const uint64_t lane_min = lme ? strtoull(lme, nullptr, 10) : LANE_MIN;
     while (nl > 1 && n < (uint64_t)nl * lane_min) --nl;
@@ -1601,6 +1674,7 @@ extern "C" int imsame_dev_revcomp(imsame_ctx *c, const uint8_t *in, uint64_t n, 
     HIPCHK(hipStreamSynchronize(s));
     if (nr == 0) return IMSAME_OK;
     if (c->rc_c.ensure((uint64_t)nr * 4 * 5 + 64)) return IMSAME_E_OOM;
+    if ((rc = c->rc_c.poison(s)) || (rc = c->rc_out.poison(s))) return rc;
     uint32_t *off = c->rc_c.as<uint32_t>(), *hend = off + nr, *bend = hend + nr, *szr = bend + nr, *oo = szr + nr;
     rc_offsets<<<nblk(n, 256), 256, 0, s>>>(c->rc_in.as<uint8_t>(), n, gpos, off);
     rc_records<<<nblk(nr, 256), 256, 0, s>>>(c->rc_in.as<uint8_t>(), n, off, nr, let, hend, bend, szr);

@@ -143,12 +143,13 @@ typedef struct imsame_ctx imsame_ctx;
 int  imsame_dev_count(void);
 
 /* Open device `device` (HIP ordinal).  Fails with IMSAME_E_HIP if no GPU.
- * Several contexts may be opened on one device (each owns its own stream
- * and buffers).  imsame_dev_count / imsame_dev_open set GPU_MAX_HW_QUEUES=8
- * when the variable is unset, before their first HIP call: a large call's 8
- * lanes then get a hardware queue each (with HIP's default 4, two lanes share
- * a queue and serialize).  A host program that starts HIP itself first should
- * set it (<= 32) before doing so; results never depend on it. */
+ * Several contexts may be opened on one device (each owns its own streams
+ * and buffers).  A context runs a large imsame_dev_align call as up to 8
+ * concurrent lanes, one per hardware queue: the library reads
+ * GPU_MAX_HW_QUEUES (HIP's default 4 when unset) once and never changes it.
+ * A host program that wants 8 lanes sets GPU_MAX_HW_QUEUES=8 (<= 32) in its
+ * environment before its first HIP call (the imsame CLI and bench.py do);
+ * results never depend on it. */
 int  imsame_dev_open(int device, imsame_ctx **out);
 void imsame_dev_close(imsame_ctx *ctx);
 const char *imsame_strerror(int code);
@@ -207,13 +208,17 @@ int imsame_dev_sync(imsame_ctx *ctx);
  * u32 arena for want_paths (may be NULL when want_paths == 0).  The device
  * keeps its own arena, sized to what the alignments need (paths that
  * overflow it are re-walked for exactly the reads concerned, never the whole
- * call); if paths_cap is smaller than *paths_used the call returns
- * IMSAME_E_PATHS with res[] complete and the paths still on the device:
- * grow the host arena and call imsame_dev_fetch_paths.
- * A call over >= 65,536 short reads is cut into 2-8 parts ("lanes") that run
- * concurrently on their own streams of the device (internal contexts sharing
- * the index and the query); results do not depend on it (IMSAME_LANES=1
- * turns it off). */
+ * call).  On ANY return, *paths_used > paths_cap means the paths were NOT
+ * copied and wait on the device: the call returns IMSAME_E_PATHS with res[]
+ * complete -- or IMSAME_E_READ_TOO_LONG, which takes precedence, with res[]
+ * complete below the offending read -- so callers compare *paths_used with
+ * paths_cap whatever the code, grow the host arena and call
+ * imsame_dev_fetch_paths.
+ * A call over short reads is cut into up to 8 parts ("lanes") that run
+ * concurrently on their own streams (internal contexts sharing the index
+ * and the query): one lane per 40,000 reads, at most one per hardware queue
+ * (GPU_MAX_HW_QUEUES, see imsame_dev_open).  Results do not depend on it
+ * (IMSAME_LANES=n forces n lanes, 1 turns it off). */
 int imsame_dev_align(imsame_ctx *ctx, uint64_t read_from, uint64_t read_to,
                      uint64_t n_threads_semantic, const imsame_params *prm,
                      imsame_read_result *res, uint32_t *paths, uint64_t paths_cap,

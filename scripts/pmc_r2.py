@@ -67,11 +67,14 @@ def main():
     n = max(int(v.get("launches", 1)), 1)
     kname = nwk.split("<")[0].split("(")[0]
     cfg = (bench or {}).get("config", {})
-    config = "c2" if cfg.get("ref_bp") == 50_000_000 and cfg.get("read_len") == 150 else "other"
+    wl = cfg.get("workload", "")
+    config = next((c for c, p in (("c5w", "C5w:"), ("c5", "C5:"), ("c3", "C3 "), ("c2", "C2:")) if wl.startswith(p)),
+                  "other")
+    sfx = "" if config == "c2" else "_" + config      # bench.py: profiles/nw_{traffic,valu}[_CONFIG].json
     if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
         fetch2, write = 2 * v["FETCH_SIZE"] * 1024, v["WRITE_SIZE"] * 1024
         cells = (bench or {}).get("detail", {}).get("nw_cells")
-        with open(os.path.join(prof, "nw_traffic.json"), "w") as f:
+        with open(os.path.join(prof, f"nw_traffic{sfx}.json"), "w") as f:
             json.dump({"tag": tag, "kernel": kname, "config": config, "launches": n,
                        "hbm_bytes_per_launch": round((fetch2 + write) / n),
                        # per DP cell: bench.py scales it by the cells of ITS launches
@@ -84,7 +87,7 @@ def main():
     if "SQ_INSTS_VALU" in v and bench:
         cells = bench["detail"]["nw_cells"]
         ipc = v["SQ_INSTS_VALU"] * 64.0 / cells
-        with open(os.path.join(prof, "nw_valu.json"), "w") as f:
+        with open(os.path.join(prof, f"nw_valu{sfx}.json"), "w") as f:
             json.dump({"tag": tag, "kernel": kname, "config": config, "launches": n,
                        "sq_insts_valu": v["SQ_INSTS_VALU"], "nw_cells": cells,
                        "lane_instr_per_cell": round(ipc, 4),

@@ -1,0 +1,45 @@
+"""Window parity of a large device run against the oracle -- TEST
+INFRASTRUCTURE (tests/, and bench.py's cpu_baseline leg as the checker).
+
+The oracle (oracle/imsame_oracle.c) aligns only the reads of a few windows of
+the WHOLE query (its -n_threads chunk heads), so a 1M-read device result can
+be checked read for read at start, middle (across a chunk head) and end in
+seconds.  Reference: computeAlignmentsByThread, alignmentFunctions.c:43-208.
+"""
+import numpy as np
+
+from imsame_amd import PARITY_FIELDS
+
+
+def windows(lo, hi, n_total, n_threads=16, w=1500):
+    """[start, middle, end) windows of reads [lo, hi) of an n_total-read
+    query: the middle one straddles a chunk head {k * floor(n/T)} inside the
+    range when there is one (a head reads no borrowed base)."""
+    w = min(w, max((hi - lo) // 3, 1))
+    rpt = n_total // max(n_threads, 1)
+    heads = [k * rpt for k in range(1, n_threads) if rpt and lo + w // 2 <= k * rpt <= hi - w // 2]
+    mid = heads[len(heads) // 2] if heads else (lo + hi) // 2
+    out = [(lo, lo + w), (mid - w // 2, mid - w // 2 + w), (hi - w, hi)]
+    return sorted(set((max(lo, a), min(hi, b)) for a, b in out))
+
+
+def check_windows(oracle, ref, rst, q, qs, res, res_lo, wins, n_threads, params=None):
+    """Compare res (rows of reads res_lo, res_lo + 1, ...) with the oracle on
+    the windows; the oracle's memo of rejected pairs (identical results, NW is
+    pure: Appendix A Q18) keeps it fast."""
+    oracle.lib.or_set_memo_rejected(1)
+    try:
+        rc, exp, er = oracle.align_windows(ref, rst, q, qs, wins, params, n_threads)
+    finally:
+        oracle.lib.or_set_memo_rejected(0)
+    compared = identical = 0
+    bad = []
+    for (a, b), e in zip(wins, exp):
+        got = res[a - res_lo:b - res_lo]
+        same = np.all([got[f] == e[f] for f in PARITY_FIELDS], axis=0)
+        compared += b - a
+        identical += int(same.sum())
+        bad += [a + int(i) for i in np.flatnonzero(~same)[:3]]
+    return {"reads_compared": compared, "identical": identical, "windows": [list(x) for x in wins],
+            "n_threads": n_threads, "oracle_rc": int(rc), "first_mismatches": bad,
+            "accepted_in_windows": int(sum(int((res[a - res_lo:b - res_lo]["status"] == 1).sum()) for a, b in wins))}

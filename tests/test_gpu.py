@@ -287,7 +287,9 @@ def test_full_c2_reference_properties(dev, oracle):
     dev.index(ref, rst)
     dev.set_query(q, qs)
     res, paths, st = dev.align(n_threads=16, want_paths=True)
-    assert st.lanes == 3                      # three parts ran concurrently
+    # 40k reads per lane, at most one lane per hardware queue (4 on the box)
+    queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) or 4
+    assert st.lanes == min(2, queues)         # parts ran concurrently
     acc = res["status"] == 1
     assert acc.mean() > 0.85
     # every accepted path re-renders to the device's own identity count (all lanes)
@@ -305,6 +307,27 @@ def test_full_c2_reference_properties(dev, oracle):
     for (a, b), e in zip(wins, exp):
         assert not _cmp(res[a:b], e), ((a, b), _cmp(res[a:b], e))
     assert sum(b - a for a, b in wins) >= 4_500
+
+
+@pytest.mark.timeout(900)
+def test_headline_mode_parity():
+    """The benchmark's own execution mode: 1M x 150 bp vs the 50 Mbp C2
+    reference in ONE call, async page-locked upload, -n_threads 16, with
+    GPU_MAX_HW_QUEUES=8 set before HIP starts (a subprocess: this process's
+    runtime keeps the box's value) -- 8 lanes on 8 hardware queues -- and
+    read-for-read oracle parity on the start, a chunk head and the end."""
+    import json
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="8")
+    p = subprocess.run([sys.executable, "-u", "-m", "tests.headline_run"], cwd=repo, env=env,
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=840)
+    assert p.returncode == 0, p.stderr[-3000:].decode(errors="replace")
+    d = json.loads(p.stdout.decode().strip().splitlines()[-1])
+    print(d)
+    assert d["lanes"] == 8, d
+    assert d["reads_compared"] >= 4500 and d["identical"] == d["reads_compared"], d
+    assert d["accepted"] > 850_000
 
 
 @pytest.fixture
