@@ -1025,12 +1025,18 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     if (const char *pc = getenv("IMSAME_DEV_PATHS_CAP")) want_cap = strtoull(pc, nullptr, 10);   // test hook
     if ((rc = paths_setup(c, p, want_cap, &pcap))) return rc;
     if (n == 0) { if (stats) *stats = st; return IMSAME_OK; }
+    // speculation from a read's first weak candidate on (seed_kernel.hip:
+    // spec_after_first); a round then emits up to n * spec_weak + n candidates
+    // (reads with a rejection emit <= n in all, S.spec below)
+    const char *sw_env = getenv("IMSAME_SPEC_WEAK");
+    const uint32_t spec_weak = (uint32_t)std::max(1, std::min(SPEC_MAX, sw_env ? atoi(sw_env) : SPEC_WEAK));
+    const uint64_t ccap = (uint64_t)n * (spec_weak > 1 ? spec_weak + 1 : 1);
     if (c->res.ensure((uint64_t)n * 64) || c->cur_p.ensure((uint64_t)n * 8) || c->cur_h.ensure((uint64_t)n * 4) ||
         c->memo.ensure((uint64_t)n * 4 * MEMO) || c->nmemo.ensure(n) || c->rstat.ensure(n) ||
-        c->act0.ensure((uint64_t)n * 4) || c->act1.ensure((uint64_t)n * 4) || c->cread.ensure((uint64_t)n * 4) ||
-        c->csid.ensure((uint64_t)n * 4) || c->cread2.ensure((uint64_t)n * 4) || c->csid2.ensure((uint64_t)n * 4) ||
-        c->cout.ensure((uint64_t)n * 64) || c->cout2.ensure((uint64_t)n * 64) || c->cbase.ensure((uint64_t)n * 4) ||
-        c->ccnt.ensure((uint64_t)n * 4) || c->perr.ensure((uint64_t)n * 4) || c->crow.ensure((uint64_t)n * 4))
+        c->act0.ensure((uint64_t)n * 4) || c->act1.ensure((uint64_t)n * 4) || c->cread.ensure(ccap * 4) ||
+        c->csid.ensure(ccap * 4) || c->cread2.ensure(ccap * 4) || c->csid2.ensure(ccap * 4) ||
+        c->cout.ensure(ccap * 64) || c->cout2.ensure(ccap * 64) || c->cbase.ensure((uint64_t)n * 4) ||
+        c->ccnt.ensure((uint64_t)n * 4) || c->perr.ensure((uint64_t)n * 4) || c->crow.ensure(ccap * 4))
         return IMSAME_E_OOM;
     if (poison_on()) {                        // this call's scratch holds nothing it may read
         const DBuf *scr[] = {&c->res, &c->cur_p, &c->cur_h, &c->memo, &c->nmemo, &c->rstat, &c->act0, &c->act1,
@@ -1090,6 +1096,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         S.minraw = c->minraw.as<uint64_t>(); S.n_minraw = ymax + 1;
         S.max_rs = p->max_read_size; S.short_ylen = short_y; S.max_rec = c->max_rec;
         S.spec = (st.rounds == 1) ? 1u : std::max<uint32_t>(1u, std::min<uint32_t>(spec_later, n / nact));
+        S.spec_weak = spec_weak;
         S.budget = seed_budget(budget1, (uint32_t)st.rounds, grow);
         S.next = nxt; S.nnext = (uint32_t *)(ctr + C_NNEXT);
         S.cbase = c->cbase.as<uint32_t>(); S.ccnt = c->ccnt.as<uint32_t>(); S.perr = c->perr.as<uint32_t>();

@@ -29,6 +29,8 @@ struct SeedLaunch {
     uint64_t max_rs; uint32_t short_ylen;
     uint64_t max_rec;                      // longest database record (a-priori rejection of whole reads)
     uint32_t spec;                         // candidates a read may emit this round (1..SPEC_MAX)
+    uint32_t spec_weak;                    // ... a read with no rejection yet whose first candidate's hit
+                                           // is weak (weak_hit): up to this many (<= 1: off)
     uint32_t budget;                       // ungapped extensions a read may run this round (0: no limit)
     uint32_t *next, *nnext;                // reads that paused on the budget (next round's active list)
     uint32_t *cbase, *ccnt;                // per read: first slot and count of this round's candidates
@@ -46,6 +48,10 @@ struct SeedLaunch {
     unsigned long long *nhits;
 };
 #define SPEC_MAX 8
+// speculation width from a weak first candidate on (spec_after_first); 1 = off
+#ifndef SPEC_WEAK
+#define SPEC_WEAK 1
+#endif
 // Hit budget per read and round: round 1 lets a read run SEED_BUDGET1
 // ungapped extensions (true reads accept within a few), each later round 8x
 // more, so reads that scan every window finish in a compacted list.
@@ -177,8 +183,18 @@ __device__ __forceinline__ bool read_irrelevant(const SeedLaunch &S, uint64_t yl
 // 350-700, the e-value passes of random reads 236-350 by the idents quirk,
 // Appendix A Q6).  A weak hit gets no prediction: its NW takes the second
 // sweep, and it does not widen the window of the true hits' wave.
+__device__ __forceinline__ bool weak_hit(uint64_t raw, uint64_t ylen) { return 3 * raw < 7 * ylen; }
 __device__ __forceinline__ int32_t predicted_row(uint64_t raw, uint64_t ylen, int64_t rec_pos, int64_t read_pos) {
-    return 3 * raw >= 7 * ylen ? (int32_t)(rec_pos - read_pos) : INT32_MIN;
+    return weak_hit(raw, ylen) ? INT32_MIN : (int32_t)(rec_pos - read_pos);
+}
+// Speculation from the first candidate on: a read whose first e-value pass is
+// weak (a random read's, by the idents quirk) will most likely see it
+// rejected, and its next passes too, so it emits up to spec_weak of them in
+// this round instead of one per round (exact for the same reason as any
+// speculation: NW is pure, the first accepted in visiting order wins).
+__device__ __forceinline__ uint32_t spec_after_first(const SeedLaunch &S, uint32_t spec, uint32_t nm, uint64_t raw,
+                                                     uint64_t ylen) {
+    return (nm == 0 && S.spec_weak > spec && weak_hit(raw, ylen)) ? S.spec_weak : spec;
 }
 
 __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint64_t &hits) {
@@ -219,7 +235,7 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint
     uint32_t budget = S.budget ? S.budget : 0xFFFFFFFFu;
     // speculate only for reads that already had a candidate rejected: a
     // read's first candidate is usually accepted (paused reads included)
-    const uint32_t spec = nm ? S.spec : 1u;
+    uint32_t spec = nm ? S.spec : 1u;
     for (; p < up_to && !stop; ++p, h = 0) {
         if (!have) {
             code = 0;
@@ -257,7 +273,10 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint
                     break;
                 }
                 if (nw_cannot_accept(S, xlen, ylen)) continue;       // NW would reject it
-                if (ne == 0) row0 = predicted_row(raw, ylen, ent.x, (int64_t)(p + 1 - rs));
+                if (ne == 0) {
+                    row0 = predicted_row(raw, ylen, ent.x, (int64_t)(p + 1 - rs));
+                    spec = spec_after_first(S, spec, nm, raw, ylen);
+                }
                 emit[ne++] = sid;
                 if (ne == spec) {
                     S.cur_p[k] = p; S.cur_h[k] = h + 1;              // resume after this hit
@@ -304,6 +323,8 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint
 // `budget` extensions; like seed_one's pauses they only reshape the work.
 // LDS: SEED_LDS_PER_LANE bytes per lane (the lane's list).
 #define SEED_LDS_PER_LANE (SPEC_MAX * 8)
+// list entry: {record, rank in the bucket | bit 31 size error | bit 30 weak hit}
+#define LST_RANK 0x3FFFFFFFu
 // lanes per read: enough lanes in flight to hide the probe latency
 // (~1-4M lanes) without scanning many windows a read will not reach; nact =
 // the reads the device scans at once (all lanes of a call)
@@ -364,7 +385,8 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
         uint32_t nl = 0, last_rel = 0, ev = 0;
         bool full = false;
         if (!done && pw < up_to) {
-            const uint32_t need = spec - ne;
+            // (a read that may still start speculating lists for it already)
+            const uint32_t need = (ne == 0 && nm == 0 && S.spec_weak > spec ? S.spec_weak : spec) - ne;
             const uint32_t code = kmer_code_at(S.q, pw);
             const uint64_t wbase = S.off[code], hi = S.off[code + 1];
             for (uint64_t e = wbase + (wl == 0 ? h : 0u); e < hi; ++e) {
@@ -384,7 +406,8 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
                     const uint64_t xlen = S.db_start[sid + 1] - S.db_start[sid];
                     const bool bad = xlen > S.max_rs || ylen > S.max_rs;   // terror (:155) if reached
                     if (!bad && nw_cannot_accept(S, xlen, ylen)) continue; // NW would reject it
-                    lst[nl++] = make_uint2(sid, (uint32_t)(e - wbase) | (bad ? 0x80000000u : 0u));
+                    lst[nl++] = make_uint2(sid, (uint32_t)(e - wbase) | (bad ? 0x80000000u : 0u) |
+                                                    (weak_hit(raw, ylen) ? 0x40000000u : 0u));
                     last_rel = (uint32_t)(e - wbase);
                     if (bad || nl == need) { full = true; break; }
                 }
@@ -408,12 +431,15 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
                 const uint2 it = lk[m];
                 if (emit_has(emit, ne, it.x)) continue;            // emitted by an earlier window
                 if (it.y & 0x80000000u) { perr = it.x + 1; stop = true; break; }
-                if (ne == 0) { e0p = (uint32_t)(pk - rs); e0r = it.y & 0x7FFFFFFFu; }
+                if (ne == 0) {
+                    e0p = (uint32_t)(pk - rs); e0r = it.y & LST_RANK;
+                    if (nm == 0 && S.spec_weak > spec && (it.y & 0x40000000u)) spec = S.spec_weak;   // spec_after_first
+                }
 #pragma unroll
                 for (int q2 = 0; q2 < SPEC_MAX; ++q2) emit[q2] = ((uint32_t)q2 == ne) ? it.x : emit[q2];
                 ++ne;
                 if (ne == spec) {                                  // resume after this hit
-                    if (wl == 0) { S.cur_p[k] = pk; S.cur_h[k] = (it.y & 0x7FFFFFFFu) + 1; }
+                    if (wl == 0) { S.cur_p[k] = pk; S.cur_h[k] = (it.y & LST_RANK) + 1; }
                     stop = true;
                 }
             }

@@ -212,9 +212,13 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
     imsame_build_tables(p, db_len, ymax, xcap, mr, ml, mi);
     const uint32_t n = (uint32_t)(read_to - read_from);
     std::vector<uint64_t> cur_p(n);
-    std::vector<uint32_t> cur_h(n), memo((size_t)n * MEMO), act(n), nxt(n), cr(n), cs(n), cr2(n), cs2(n);
+    // imsame_dev.hip:align_one -- speculation from a weak first candidate, candidate capacity
+    const char *sw_env = getenv("IMSAME_SPEC_WEAK");
+    const uint32_t spec_weak = (uint32_t)std::max(1, std::min(SPEC_MAX, sw_env ? atoi(sw_env) : SPEC_WEAK));
+    const size_t ccap = (size_t)n * (spec_weak > 1 ? spec_weak + 1 : 1);
+    std::vector<uint32_t> cur_h(n), memo((size_t)n * MEMO), act(n), nxt(n), cr(ccap), cs(ccap), cr2(ccap), cs2(ccap);
     std::vector<uint32_t> cbase(n), ccnt(n), perr(n);
-    std::vector<int32_t> crow(n);
+    std::vector<int32_t> crow(ccap);
     const char *win_env = getenv("IMSAME_NW_WINDOW");
     int32_t *crowp = (win_env && atoi(win_env)) ? crow.data() : nullptr;     // imsame_dev.hip: off by default
     const char *spec_env = getenv("IMSAME_SPEC");
@@ -222,7 +226,7 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
     const char *bud_env = getenv("IMSAME_SEED_BUDGET");
     const uint32_t budget1 = bud_env ? (uint32_t)std::max(0, atoi(bud_env)) : SEED_BUDGET1;
     std::vector<uint8_t> nmemo(n), rstat(n);
-    std::vector<imsame_read_result> o1(n), o2(n);
+    std::vector<imsame_read_result> o1(ccap), o2(ccap);
     // per-candidate results poisoned like reused device buffers: a candidate the
     // NW kernels leave unwritten shows
     memset(o1.data(), 0xEE, o1.size() * sizeof(imsame_read_result));
@@ -253,6 +257,7 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
         S.minident = mi.data(); S.n_minident = xcap + ymax + 2;
         S.max_rs = p->max_read_size; S.short_ylen = short_y; S.max_rec = max_rec;
         S.spec = (st.rounds == 1) ? 1u : std::max<uint32_t>(1u, std::min<uint32_t>(spec_later, n / nact));
+        S.spec_weak = spec_weak;
         S.budget = seed_budget(budget1, (uint32_t)st.rounds);
         S.next = nxt.data(); S.nnext = &nc[2];
         S.cbase = cbase.data(); S.ccnt = ccnt.data(); S.perr = perr.data();
