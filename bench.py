@@ -415,6 +415,8 @@ def run_e2e(ref, rst, q, qs, a):
         out = outf if free > need else "/dev/null"
         t0 = time.monotonic()
         extra = os.environ.get("IMSAME_E2E_ARGS", "").split()          # experiments, e.g. -batch_reads N
+        if os.environ.get("IMSAME_E2E_MMAP"):
+            extra += ["-out_mmap", os.environ["IMSAME_E2E_MMAP"]]
         p = subprocess.run([cli, "-query", qf, "-db", dbf, "-out", out, "-n_threads", str(a.n_threads)] + extra,
                            stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=900)
         wall = time.monotonic() - t0
@@ -424,6 +426,7 @@ def run_e2e(ref, rst, q, qs, a):
         ph = json.loads(m.group(1))
         ph = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in ph.items()}
         ph.update({"process_wall_s": round(wall, 3), "output": "file" if out == outf else "/dev/null (disk full)",
+                   "output_fs": mount_fs(td), "cli_args": extra,
                    "reads_per_s_e2e": round(len(qs) / wall, 1),
                    "note": "imsame -query q.fa -db db.fa -out out.align -n_threads %d on one GPU; render+write of "
                            "finished batches overlaps the device's later batches; render_tail_s = exposed output "
@@ -447,6 +450,19 @@ def timed_parity(ref, rst, q, qs, res, lo, hi, a, params):
     out["oracle_s"] = round(time.time() - t0, 2)
     out["rows_of"] = "the last timed step"
     return out
+
+
+def mount_fs(path):
+    """Filesystem type of the mount holding path (/proc/mounts, longest prefix)."""
+    best, fs = "", None
+    try:
+        for line in open("/proc/mounts"):
+            f = line.split()
+            if len(f) > 2 and (path == f[1] or path.startswith(f[1].rstrip("/") + "/")) and len(f[1]) > len(best):
+                best, fs = f[1], f[2]
+    except OSError:
+        pass
+    return fs
 
 
 def cpu_baseline(dev, ref, rst, q, qs, a, params):

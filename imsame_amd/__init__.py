@@ -32,6 +32,9 @@ FLAG_NW16_ONEPASS = 4  # ... the packed kernel in one pass (default: score sweep
 
 _lib = None
 _host = None
+# imsame_part_fn (include/imsame_dev.h)
+PART_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_uint64, C.c_uint64, C.c_int, C.c_uint64, C.POINTER(C.c_uint32),
+                      C.c_uint64)
 
 
 class ImsameError(RuntimeError):
@@ -69,6 +72,8 @@ def lib():
         L.imsame_host_free.argtypes = [vp]
         L.imsame_dev_align.argtypes = [vp, u64, u64, u64, C.POINTER(Params), vp, vp, u64, C.POINTER(u64),
                                        C.POINTER(Stats)]
+        L.imsame_dev_align_parts.argtypes = [vp, u64, u64, u64, C.POINTER(Params), vp, PART_FN, vp,
+                                             C.POINTER(Stats)]
         L.imsame_dev_align_windows.argtypes = [vp, u64, u64, u64, C.POINTER(Params), u64, vp, vp, vp, vp, vp, u64,
                                                C.POINTER(u64), C.POINTER(Stats)]
         L.imsame_dev_align_sliced.argtypes = [vp, vp, u64, vp, u64, vp, u64, u64, u64, u64, C.POINTER(Params),
@@ -249,6 +254,30 @@ class Device:
         if want_paths and used.value > cap:       # not copied (E_PATHS or E_READ_TOO_LONG): on the device
             paths = self.fetch_paths(used.value)
         return res, paths[:used.value], st
+
+    def align_parts(self, read_from=None, read_to=None, n_threads=4, params=None, want_paths=False):
+        """imsame_dev_align_parts: per-read results plus the parts as the
+        library handed them over, in arrival order: [(from, to, status,
+        err_read, paths of the part), ...] (each part's path_off index its
+        own paths)."""
+        read_from = self.q_range[0] if read_from is None else read_from
+        read_to = self.q_range[1] if read_to is None else read_to
+        p = params if params is not None else self.params()
+        p.want_paths = 1 if want_paths else 0
+        res = np.zeros(read_to - read_from, dtype=RESULT_DTYPE)
+        parts = []
+
+        def got(_user, a, b, status, err, paths, n):      # runs on the library's lane threads
+            arr = np.ctypeslib.as_array(paths, shape=(n,)).copy() if n else np.zeros(0, np.uint32)
+            parts.append((int(a), int(b), int(status), int(err), arr))
+
+        cb = PART_FN(got)
+        st = Stats()
+        rc = lib().imsame_dev_align_parts(self._h, read_from, read_to, n_threads, C.byref(p), res.ctypes.data, cb,
+                                          None, C.byref(st))
+        if rc:
+            raise ImsameError(rc, "imsame_dev_align_parts")
+        return res, parts, st
 
     def align_windows(self, ev_db_len, win_cap=None, read_from=None, read_to=None, n_threads=4, params=None,
                       allow_too_long=False, win_start=None):

@@ -12,9 +12,9 @@
  * reads are sharded over several device contexts, the multi-GPU form of the
  * reference's -n_threads fan-out, IMSAME.c:414-467), -max_read_size N (raise
  * the 3000-base NW cap of structs.h:19; the reference has it compile-time
- * only), -slice_bases N, -render_threads N, -batch_reads N.  The .align
- * records are rendered by a thread pool while the GPUs align later batches
- * (imsame_pipe.c).  Timing lines report wall-clock seconds (the reference
+ * only), -slice_bases N, -render_threads N, -batch_reads N, -out_mmap 0|1.
+ * The .align records are rendered by a thread pool as the device hands over
+ * finished parts of the reads, while it aligns the rest (imsame_pipe.c).  Timing lines report wall-clock seconds (the reference
  * prints clock(), i.e. CPU time summed over threads); a JSON phase line goes
  * to stderr.
  */
@@ -27,6 +27,7 @@
 #include <inttypes.h>
 #include "../../../include/imsame_dev.h"
 #include <fcntl.h>
+#include <pthread.h>
 #include <unistd.h>
 #include "imsame_host.h"
 #include "imsame_pipe.h"
@@ -41,6 +42,17 @@ static double now_s(void) {
 static void terror(const char *s) {
     printf("ERR**** %s ****\n", s);
     exit(-1);
+}
+
+/* device contexts, opened on a thread of their own (overlapping the parse) */
+static pipe_dev dv_all[PIPE_MAX_DEV];
+typedef struct { pipe_dev *d; const int *devs; int G, rc; double secs; } open_job;
+static void *open_run(void *a) {
+    open_job *j = a;
+    const double t = now_s();
+    j->rc = pipe_open(j->d, j->devs, j->G);
+    j->secs = now_s() - t;
+    return NULL;
 }
 
 static void usage(void) {
@@ -62,6 +74,7 @@ static void usage(void) {
     printf("           -slice_bases [Integer: index the database in slices of at most this many bases]\n");
     printf("           -render_threads [Integer: host threads writing the .align records]\n");
     printf("           -batch_reads [Integer: reads per device call]\n");
+    printf("           -out_mmap   [0|1: write the .align through a shared mapping]\n");
     exit(1);
 }
 
@@ -74,7 +87,7 @@ int main(int argc, char **argv) {
     imsame_params prm;
     imsame_params_default(&prm);
     uint64_t T = 4;                                   /* IMSAME.c:49 */
-    int device = 0, render_threads = 0;
+    int device = 0, render_threads = 0, out_mmap = 0;
     uint64_t slice_bases = 0, batch_reads = 0;       /* 0: one index (the reference's) */
     /* init_args, IMSAME.c:520-578 (same strcmp scan over every argv slot) */
     for (int a = 0; a < argc; a++) {
@@ -104,10 +117,11 @@ int main(int argc, char **argv) {
         if (!strcmp(argv[a], "-slice_bases")) slice_bases = strtoull(argv[a + 1], NULL, 10);
         if (!strcmp(argv[a], "-render_threads")) render_threads = atoi(argv[a + 1]);
         if (!strcmp(argv[a], "-batch_reads")) batch_reads = strtoull(argv[a + 1], NULL, 10);
+        if (!strcmp(argv[a], "-out_mmap")) out_mmap = atoi(argv[a + 1]);
     }
     if (!qpath || !dpath) terror("A query and database is required");
     /* the reference fopen()s "wt" and never checks it (IMSAME.c:541-551) */
-    int out_fd = opath ? open(opath, O_WRONLY | O_CREAT | O_TRUNC, 0666) : -1;
+    int out_fd = opath ? open(opath, (out_mmap ? O_RDWR : O_WRONLY) | O_CREAT | O_TRUNC, 0666) : -1;
     int devs[PIPE_MAX_DEV], G = 1;
     devs[0] = device;
     if (devspec) G = pipe_parse_devices(devspec, devs, PIPE_MAX_DEV);
@@ -115,32 +129,43 @@ int main(int argc, char **argv) {
     if (slice_bases && G > 1) terror("-slice_bases runs on one device");
 
     const double t_wall = now_s();
+    /* The device runtime starts (a few hundred ms) on its own thread while
+     * the FASTA files are parsed; the [INFO] lines keep the reference's order
+     * and each reports its own phase. */
+    open_job oj = {.d = dv_all, .devs = devs, .G = G};
+    pthread_t oth;
+    const int othr = pthread_create(&oth, NULL, open_run, &oj) == 0;
+    if (!othr) open_run(&oj);
     double t0 = now_s();
+    host_seqs db, q;
+    const int db_bad = host_load_fasta(dpath, 1, &db);
+    const double t_parse_db = now_s() - t0;
+    t0 = now_s();
+    const int q_bad = db_bad ? 1 : host_load_fasta(qpath, 0, &q);
+    const double t_parse_q = now_s() - t0;
+    if (othr) pthread_join(oth, NULL);
+    pipe_dev *dv = dv_all;
     printf("[INFO] Init. quick table\n");
-    pipe_dev dv[PIPE_MAX_DEV];
-    if (pipe_open(dv, devs, G)) terror("Could not open the GPU device");
-    printf("[INFO] Initialization took %e seconds \n", now_s() - t0);
+    if (oj.rc) terror("Could not open the GPU device");
+    printf("[INFO] Initialization took %e seconds \n", oj.secs);
 
     printf("[INFO] Loading database\n");
+    if (db_bad) terror("Could not open database file");
     t0 = now_s();
-    host_seqs db, q;
-    if (host_load_fasta(dpath, 1, &db)) terror("Could not open database file");
-    const double t_parse_db = now_s() - t0;
     if (db.n == 0) slice_bases = 0;                  /* nothing to slice */
     int rc = slice_bases ? IMSAME_OK : pipe_index(dv, G, &db);
     if (rc) terror(imsame_strerror(rc));
-    const double t_index = now_s() - t0 - t_parse_db;
+    const double t_index = now_s() - t0;
     printf("[INFO] Database loaded and of length %" PRIu64 ". Hash table building took %e seconds\n", db.len,
-           now_s() - t0);
+           t_parse_db + t_index);
 
     t0 = now_s();
     printf("[INFO] Loading query.\n");
-    if (host_load_fasta(qpath, 0, &q)) terror("Could not open query file");
-    const double t_parse_q = now_s() - t0;
+    if (q_bad) terror("Could not open query file");
     rc = pipe_set_query(dv, G, &q);
     if (rc) terror(imsame_strerror(rc));
-    const double t_upload = now_s() - t0 - t_parse_q;
-    printf("[INFO] Query loaded and of length %" PRIu64 ". Took %e seconds\n", q.len, now_s() - t0);
+    const double t_upload = now_s() - t0;
+    printf("[INFO] Query loaded and of length %" PRIu64 ". Took %e seconds\n", q.len, t_parse_q + t_upload);
 
     t0 = now_s();
     printf("[INFO] Computing alignments.\n");
@@ -183,7 +208,7 @@ int main(int argc, char **argv) {
         free(paths);
     } else {
         pipe_opts po = {.T = T, .prm = prm, .out_fd = out_fd, .render_threads = render_threads,
-                        .batch_reads = batch_reads};
+                        .batch_reads = batch_reads, .out_mmap = out_mmap};
         rc = pipe_align_render(dv, G, &db, &q, &po, &pr);
         if (rc && rc != IMSAME_E_READ_TOO_LONG) terror(imsame_strerror(rc));
     }
@@ -199,11 +224,11 @@ int main(int argc, char **argv) {
     fflush(stdout);
     fprintf(stderr, "[imsame] rounds=%" PRIu64 " nw=%" PRIu64 " cells=%" PRIu64 " seed_ms=%.3f nw_ms=%.3f total_ms=%.3f\n",
             pr.st.rounds, pr.st.n_nw, pr.st.nw_cells, pr.st.ms_seed, pr.st.ms_nw, pr.st.ms_total);
-    fprintf(stderr, "[imsame] phases {\"devices\": %d, \"batches\": %" PRIu64 ", \"parse_db_s\": %.4f, \"index_s\": %.4f, "
+    fprintf(stderr, "[imsame] phases {\"devices\": %d, \"parts\": %" PRIu64 ", \"open_s\": %.4f, \"parse_db_s\": %.4f, \"index_s\": %.4f, "
             "\"parse_query_s\": %.4f, \"upload_s\": %.4f, \"align_s\": %.4f, \"render_busy_s\": %.4f, "
             "\"write_busy_s\": %.4f, \"render_tail_s\": %.4f, \"bytes_out\": %" PRIu64 ", \"accepted\": %" PRIu64
             ", \"wall_s\": %.4f}\n",
-            G, pr.batches, t_parse_db, t_index, t_parse_q, t_upload, pr.t_align, pr.t_render, pr.t_write, pr.t_tail,
+            G, pr.batches, oj.secs, t_parse_db, t_index, t_parse_q, t_upload, pr.t_align, pr.t_render, pr.t_write, pr.t_tail,
             pr.bytes_out, acc, now_s() - t_wall);
     host_free_seqs(&db);
     host_free_seqs(&q);

@@ -1,11 +1,13 @@
 /* imsame_pipe.c -- see imsame_pipe.h.
  *
- * Threads: one per device context (index build, query upload, the batches of
- * its shard), plus a pool of render threads per finished batch.  The main
- * thread walks the batches in read order; when batch b is done it renders b
- * (records into per-thread buffers, then each buffer written at its file
- * offset) while the devices align b+1, b+2, ...  The record of a read is the
- * reference's (alignmentFunctions.c:165-168):
+ * Threads: one per device context (index build, query upload, the
+ * alignment calls of its shard), the library's lane threads (each hands its
+ * reads over as soon as they are final, imsame_dev_align_parts), plus a pool
+ * of render threads.  The main thread takes the parts in read order; while
+ * the devices finish later parts it renders part p (records into per-thread
+ * buffers) and a writer thread writes part p-1's buffers at their file
+ * offsets.  The record of a read is the reference's
+ * (alignmentFunctions.c:165-168):
  *     "(%lu, %lu) : %d%% %d%% %lu\n $$$$$$$ \n" + build_alignment's text. */
 #define _GNU_SOURCE
 #include <stdio.h>
@@ -15,6 +17,7 @@
 #include <fcntl.h>
 #include <inttypes.h>
 #include <pthread.h>
+#include <sys/mman.h>
 #include <time.h>
 #include <unistd.h>
 #include "imsame_pipe.h"
@@ -131,6 +134,8 @@ typedef struct {
     host_text text, scratch;           /* reused across batches */
     uint64_t off;
     int fd, err;
+    char *map;                         /* mmap output: the part's mapping, file offset map_base */
+    uint64_t map_base;
 } rtask;
 
 static void *render_task(void *a) {
@@ -175,6 +180,12 @@ static void *write_task(void *a) {
     return NULL;
 }
 
+static void *copy_task(void *a) {
+    rtask *t = a;
+    memcpy(t->map + (t->off - t->map_base), t->text.buf, t->text.len);
+    return NULL;
+}
+
 static void run_pool(rtask *t, int n, void *(*fn)(void *)) {
     pthread_t th[HOST_MAX_THREADS];
     int started[HOST_MAX_THREADS] = {0};
@@ -210,12 +221,31 @@ static int render_part(rtask *t, int *nt, const host_seqs *db, const host_seqs *
     return 0;
 }
 
-/* write what render_part left in t[0..nt): parallel pwrite at the offsets, or
- * ordered write() for pipes; returns an errno and the wall time in *secs */
+/* mmap output: the file grows to the part's end and the tasks copy their
+ * buffers into a shared mapping of it in parallel (a write() of one file
+ * copies into the page cache under the file's lock, one writer at a time;
+ * page faults on a shared mapping run in parallel) */
+static int map_part(rtask *t, int nt, int fd) {
+    const uint64_t lo = t[0].off, hi = t[nt - 1].off + t[nt - 1].text.len;
+    if (hi <= lo) return 0;
+    if (ftruncate(fd, (off_t)hi) != 0) return errno;
+    const uint64_t pg = (uint64_t)sysconf(_SC_PAGESIZE), base = lo / pg * pg;
+    char *m = mmap(NULL, hi - base, PROT_READ | PROT_WRITE, MAP_SHARED, fd, (off_t)base);
+    if (m == MAP_FAILED) return errno;
+    for (int k = 0; k < nt; ++k) { t[k].map = m; t[k].map_base = base; }
+    run_pool(t, nt, copy_task);
+    return munmap(m, hi - base) ? errno : 0;
+}
+
+/* write what render_part left in t[0..nt): parallel pwrite at the offsets
+ * (seekable 1), copies into a mapping of the file (seekable 2), or ordered
+ * write() for pipes; returns an errno and the wall time in *secs */
 static int write_part(rtask *t, int nt, int fd, int seekable, double *secs) {
     const double t0 = pipe_now();
     int err = 0;
-    if (seekable) {
+    if (seekable == 2) {
+        err = map_part(t, nt, fd);
+    } else if (seekable) {
         run_pool(t, nt, write_task);
         for (int k = 0; k < nt && !err; ++k) err = t[k].err;
     } else {
@@ -281,63 +311,65 @@ int pipe_render_range(const host_seqs *db, const host_seqs *q, const imsame_read
     return err;
 }
 
-/* ---- alignment: device workers over batches ------------------------------- */
+/* ---- alignment: device workers, results handed over in parts ---------------
+ * Each device aligns its shard in one imsame_dev_align_parts call (or
+ * batches of -batch_reads); the library hands over each lane's reads as soon
+ * as they are final (imsame_dev.h), in any order.  The main thread renders
+ * the parts in read order -- the part starting at the next unwritten read --
+ * while the devices finish the others. */
+typedef struct part {
+    uint64_t from, to, err;
+    int status;
+    uint32_t *paths;                   /* copy of the part's paths (path_off index it) */
+    struct part *next;
+} part;
+
 typedef struct {
-    uint64_t from, to;
-    uint32_t *paths;
-    uint64_t npaths;
-    imsame_stats st;
-    int rc, done;
-    double t_done;
-} batch;
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+    part *ready;                       /* delivered, not rendered yet          */
+    uint64_t stop_read;                /* min erroring read so far             */
+    int fatal;                         /* a hard error (not the size abort)    */
+    int workers_left;
+    double t_last;                     /* last part delivered                  */
+} exchange;
 
 typedef struct {
     pipe_dev *d;
-    batch *b;
-    int nb;
+    uint64_t from, to, bsz;
     const pipe_opts *o;
     const imsame_params *prm;
     imsame_read_result *res;
-    pthread_mutex_t *mu;
-    pthread_cond_t *cv;
-    uint64_t *stop_read;               /* min erroring read so far (shared)  */
+    exchange *x;
+    imsame_stats st;                   /* summed over the worker's calls       */
+    double ms_calls;
+    int batches;
 } worker;
 
-static void *align_worker(void *a) {
-    worker *w = a;
-    for (int k = 0; k < w->nb; ++k) {
-        batch *b = &w->b[k];
-        pthread_mutex_lock(w->mu);
-        const int skip = b->from >= *w->stop_read;     /* past a fatal read: never written */
-        pthread_mutex_unlock(w->mu);
-        uint64_t used = 0;
-        int rc = 0;
-        if (!skip) {
-            const uint64_t cap = w->prm->want_paths ? 2 * (b->to - b->from) + 1024 : 0;
-            b->paths = cap ? malloc(cap * sizeof(uint32_t)) : NULL;
-            if (cap && !b->paths) rc = IMSAME_E_OOM;
-            if (!rc)
-                rc = imsame_dev_align(w->d->ctx, b->from, b->to, w->o->T, w->prm, w->res + b->from, b->paths, cap,
-                                      &used, &b->st);
-            /* paths not copied (IMSAME_E_PATHS, or a size abort whose paths did
-             * not fit either, include/imsame_dev.h): fetch them */
-            if ((rc == IMSAME_E_PATHS || rc == IMSAME_E_READ_TOO_LONG) && cap && used > cap) {
-                uint32_t *p = realloc(b->paths, (used + 1) * sizeof(uint32_t));
-                const int rf = p ? imsame_dev_fetch_paths(w->d->ctx, p, used, &used) : IMSAME_E_OOM;
-                if (p) b->paths = p;
-                if (rc == IMSAME_E_PATHS || rf) rc = rf;
-            }
-        }
-        b->npaths = used;
-        pthread_mutex_lock(w->mu);
-        b->rc = skip ? IMSAME_E_STATE : rc;
-        if (rc == IMSAME_E_READ_TOO_LONG && b->st.err_read < *w->stop_read) *w->stop_read = b->st.err_read;
-        b->done = 1;
-        b->t_done = pipe_now();
-        pthread_cond_broadcast(w->cv);
-        pthread_mutex_unlock(w->mu);
+static void on_part(void *user, uint64_t a, uint64_t b, int status, uint64_t err, const uint32_t *paths,
+                    uint64_t np) {
+    worker *w = user;
+    exchange *x = w->x;
+    part *pt = calloc(1, sizeof *pt);
+    uint32_t *pp = np ? malloc(np * sizeof(uint32_t)) : NULL;
+    if (pt && (pp || !np)) {
+        if (np) memcpy(pp, paths, np * sizeof(uint32_t));
+        *pt = (part){.from = a, .to = b, .err = err, .status = status, .paths = pp};
+    } else {
+        free(pt); free(pp);
+        pt = NULL;
     }
-    return NULL;
+    pthread_mutex_lock(&x->mu);
+    if (!pt) x->fatal = x->fatal ? x->fatal : IMSAME_E_OOM;
+    else {
+        pt->next = x->ready;
+        x->ready = pt;
+        if (status == IMSAME_E_READ_TOO_LONG && err < x->stop_read) x->stop_read = err;
+        else if (status && status != IMSAME_E_READ_TOO_LONG && !x->fatal) x->fatal = status;
+    }
+    x->t_last = pipe_now();
+    pthread_cond_broadcast(&x->cv);
+    pthread_mutex_unlock(&x->mu);
 }
 
 static void add_stats(imsame_stats *t, const imsame_stats *s) {
@@ -345,6 +377,48 @@ static void add_stats(imsame_stats *t, const imsame_stats *s) {
     t->n_hits += s->n_hits; t->rounds = s->rounds > t->rounds ? s->rounds : t->rounds;
     t->ms_seed += s->ms_seed; t->ms_nw += s->ms_nw; t->nw_launches += s->nw_launches; t->nw_bytes += s->nw_bytes;
     t->n_rewalk += s->n_rewalk;
+    t->lanes = s->lanes > t->lanes ? s->lanes : t->lanes;
+}
+
+static void *align_worker(void *a) {
+    worker *w = a;
+    exchange *x = w->x;
+    for (uint64_t f = w->from; f < w->to; f += w->bsz) {
+        const uint64_t t = f + w->bsz < w->to ? f + w->bsz : w->to;
+        pthread_mutex_lock(&x->mu);
+        const int skip = f >= x->stop_read || x->fatal;    /* past a fatal read: never written */
+        pthread_mutex_unlock(&x->mu);
+        if (skip) break;
+        imsame_stats st;
+        memset(&st, 0, sizeof st);
+        const int rc = imsame_dev_align_parts(w->d->ctx, f, t, w->o->T, w->prm, w->res + f, on_part, w, &st);
+        add_stats(&w->st, &st);
+        w->ms_calls += st.ms_total;
+        w->batches++;
+        if (rc && rc != IMSAME_E_READ_TOO_LONG) {          /* parts may be missing: stop the run */
+            pthread_mutex_lock(&x->mu);
+            if (!x->fatal) x->fatal = rc;
+            pthread_cond_broadcast(&x->cv);
+            pthread_mutex_unlock(&x->mu);
+            break;
+        }
+    }
+    pthread_mutex_lock(&x->mu);
+    x->workers_left--;
+    pthread_cond_broadcast(&x->cv);
+    pthread_mutex_unlock(&x->mu);
+    return NULL;
+}
+
+/* the delivered part starting at read `at` (unlinked), or NULL */
+static part *take_part(exchange *x, uint64_t at) {
+    for (part **pp = &x->ready; *pp; pp = &(*pp)->next)
+        if ((*pp)->from == at) {
+            part *p = *pp;
+            *pp = p->next;
+            return p;
+        }
+    return NULL;
 }
 
 int pipe_align_render(pipe_dev *d, int G, const host_seqs *db, const host_seqs *q, const pipe_opts *o,
@@ -355,78 +429,59 @@ int pipe_align_render(pipe_dev *d, int G, const host_seqs *db, const host_seqs *
     imsame_params prm = o->prm;
     prm.want_paths = o->out_fd >= 0;
     imsame_read_result *res = calloc(n + 1, sizeof *res);
-    if (!res) return IMSAME_E_OOM;
-    /* batches: each device's shard in pieces (several when rendering, so
-     * the host renders batch b while the device aligns b+1) */
-    int nb[PIPE_MAX_DEV], total = 0;
-    uint64_t from[PIPE_MAX_DEV], to[PIPE_MAX_DEV], bsz[PIPE_MAX_DEV];
-    for (int g = 0; g < G; ++g) {
-        shard(n, g, G, &from[g], &to[g]);
-        const uint64_t m = to[g] - from[g];
-        uint64_t b = o->batch_reads;
-        if (!b) b = prm.want_paths ? (m + 3) / 4 : m;          /* 4 batches when rendering */
-        if (prm.want_paths && !o->batch_reads && b < 131072) b = 131072;
-        if (b == 0) b = 1;
-        bsz[g] = b;
-        nb[g] = m ? (int)((m + b - 1) / b) : 0;
-        total += nb[g];
-    }
-    batch *B = calloc((size_t)total + 1, sizeof *B);
     const int nt = render_threads(o->render_threads);
     rtask *rt = prm.want_paths ? calloc(2 * (size_t)nt, sizeof *rt) : NULL;       /* two buffer sets */
-    if (!B || (prm.want_paths && !rt)) {
-        free(B); free(rt); free(res);
+    if (!res || (prm.want_paths && !rt)) {
+        free(res); free(rt);
         return r->rc = IMSAME_E_OOM;
     }
+    exchange x = {.mu = PTHREAD_MUTEX_INITIALIZER, .cv = PTHREAD_COND_INITIALIZER, .stop_read = n, .workers_left = G};
     worker W[PIPE_MAX_DEV];
-    pthread_mutex_t mu = PTHREAD_MUTEX_INITIALIZER;
-    pthread_cond_t cv = PTHREAD_COND_INITIALIZER;
-    uint64_t stop_read = n;
-    int k = 0;
     for (int g = 0; g < G; ++g) {
-        W[g] = (worker){.d = &d[g], .b = B + k, .nb = nb[g], .o = o, .prm = &prm, .res = res, .mu = &mu, .cv = &cv,
-                        .stop_read = &stop_read};
-        for (int j = 0; j < nb[g]; ++j, ++k) {
-            B[k].from = from[g] + (uint64_t)j * bsz[g];
-            B[k].to = B[k].from + bsz[g] < to[g] ? B[k].from + bsz[g] : to[g];
-        }
+        uint64_t f, t;
+        shard(n, g, G, &f, &t);
+        W[g] = (worker){.d = &d[g], .from = f, .to = t, .bsz = o->batch_reads ? o->batch_reads : (t - f ? t - f : 1),
+                        .o = o, .prm = &prm, .res = res, .x = &x};
     }
-    r->batches = (uint64_t)total;
     const double t0 = pipe_now();
+    x.t_last = t0;
     pthread_t th[PIPE_MAX_DEV];
     int started[PIPE_MAX_DEV] = {0};
     for (int g = 0; g < G; ++g) started[g] = pthread_create(&th[g], NULL, align_worker, &W[g]) == 0;
     for (int g = 0; g < G; ++g)
         if (!started[g]) align_worker(&W[g]);
-    /* walk the batches in read order: render each as it completes */
-    const int seekable = prm.want_paths && lseek(o->out_fd, 0, SEEK_CUR) >= 0;
+    /* render the parts in read order as they arrive */
+    int seekable = prm.want_paths && lseek(o->out_fd, 0, SEEK_CUR) >= 0;
     uint64_t off = seekable ? (uint64_t)lseek(o->out_fd, 0, SEEK_CUR) : 0;
+    if (seekable && o->out_mmap) seekable = 2;
     int rc = 0, werr = 0, nrend = 0;
     writer wr = {0};
-    double t_last = t0;
-    for (k = 0; k < total; ++k) {
-        pthread_mutex_lock(&mu);
-        while (!B[k].done) pthread_cond_wait(&cv, &mu);
-        const uint64_t sr = stop_read;
-        pthread_mutex_unlock(&mu);
-        if (B[k].t_done > t_last) t_last = B[k].t_done;
-        if (B[k].from >= sr) continue;                        /* past the fatal read */
-        if (B[k].rc && B[k].rc != IMSAME_E_READ_TOO_LONG) { if (!rc) rc = B[k].rc; continue; }
-        if (B[k].rc == IMSAME_E_READ_TOO_LONG && !rc) rc = IMSAME_E_READ_TOO_LONG;
-        const uint64_t hi = B[k].to < sr ? B[k].to : sr;
-        if (rt && !werr && (rc == 0 || rc == IMSAME_E_READ_TOO_LONG)) {
-            /* set nrend & 1 was last written two batches ago: that writer is joined */
+    uint64_t nxt = 0;
+    for (;;) {
+        pthread_mutex_lock(&x.mu);
+        part *pt = NULL;
+        while (nxt < x.stop_read && !x.fatal && !(pt = take_part(&x, nxt)) && x.workers_left > 0)
+            pthread_cond_wait(&x.cv, &x.mu);
+        if (!pt && nxt < x.stop_read && !x.fatal) pt = take_part(&x, nxt);   /* workers done meanwhile */
+        const uint64_t sr = x.stop_read;
+        if (x.fatal && !rc) rc = x.fatal;
+        pthread_mutex_unlock(&x.mu);
+        if (!pt) break;                                     /* done, past the fatal read, or failed */
+        nxt = pt->to;
+        const uint64_t hi = pt->to < sr ? pt->to : sr;
+        if (rt && !werr && !rc && hi > pt->from) {
+            /* set nrend & 1 was last written two parts ago: that writer is joined */
             rtask *set = rt + (size_t)(nrend & 1) * nt;
             int used = nt;
-            werr = render_part(set, &used, db, q, res, B[k].paths, B[k].from, hi, o->out_fd, &off, r);
-            const int e = writer_join(&wr, r);              /* batch k-1's output is out */
+            werr = render_part(set, &used, db, q, res, pt->paths, pt->from, hi, o->out_fd, &off, r);
+            const int e = writer_join(&wr, r);              /* the previous part's output is out */
             if (!werr) werr = e;
             if (!werr) werr = writer_start(&wr, set, used, o->out_fd, seekable);
             nrend++;
         }
-        /* its paths are no longer needed once rendered (the text is in the set) */
-        free(B[k].paths);
-        B[k].paths = NULL;
+        free(pt->paths);                                    /* rendered: the text is in the set */
+        free(pt);
+        r->batches++;
     }
     {
         const int e = writer_join(&wr, r);
@@ -434,27 +489,27 @@ int pipe_align_render(pipe_dev *d, int G, const host_seqs *db, const host_seqs *
     }
     for (int g = 0; g < G; ++g)
         if (started[g]) pthread_join(th[g], NULL);
-    if (stop_read < n && !rc) rc = IMSAME_E_READ_TOO_LONG;       /* its batch may start at the read */
-    for (k = 0; k < total; ++k) {
-        if (B[k].t_done > t_last) t_last = B[k].t_done;
-        add_stats(&r->st, &B[k].st);
-        free(B[k].paths);
+    for (part *p = x.ready; p;) {                           /* parts past the stop */
+        part *nx = p->next;
+        free(p->paths);
+        free(p);
+        p = nx;
     }
-    double dev_ms[PIPE_MAX_DEV] = {0};
-    for (int g = 0; g < G; ++g)
-        for (int j = 0; j < nb[g]; ++j) dev_ms[g] += W[g].b[j].st.ms_total;
-    for (int g = 0; g < G; ++g)
-        if (dev_ms[g] > r->st.ms_total) r->st.ms_total = dev_ms[g];
-    r->t_align = t_last - t0;
-    r->t_tail = pipe_now() - t_last;
-    r->stop = stop_read;
-    r->st.err_read = stop_read < n ? stop_read : ~0ull;
-    for (uint64_t x = 0; x < stop_read; ++x) r->accepted += res[x].status == 1;
+    if (x.fatal && !rc) rc = x.fatal;
+    if (!rc && x.stop_read < n) rc = IMSAME_E_READ_TOO_LONG;
+    for (int g = 0; g < G; ++g) {
+        add_stats(&r->st, &W[g].st);
+        if (W[g].ms_calls > r->st.ms_total) r->st.ms_total = W[g].ms_calls;
+    }
+    r->st.err_read = x.stop_read < n ? x.stop_read : ~0ull;
+    r->t_align = x.t_last - t0;
+    r->t_tail = pipe_now() - x.t_last;
+    r->stop = x.stop_read;
+    for (uint64_t k = 0; k < x.stop_read; ++k) r->accepted += res[k].status == 1;
     if (rt) {
         for (int j = 0; j < 2 * nt; ++j) { free(rt[j].text.buf); free(rt[j].scratch.buf); }
         free(rt);
     }
-    free(B);
     free(res);
     if (werr) { fprintf(stderr, "[imsame] write error: %s\n", strerror(werr)); if (!rc) rc = IMSAME_E_ARG; }
     r->rc = rc;

@@ -5,8 +5,9 @@
  * accepted records to one FILE* as they go (IMSAME.c:414-467,
  * alignmentFunctions.c:165-168).  Here reads are cut into G contiguous
  * shards, one per device context (chunk heads stay those of -n_threads over
- * the whole query); each device aligns its shard in
- * batches, and the host renders finished batches in read order with a pool
+ * the whole query); each device aligns its shard in one
+ * call (or batches of batch_reads) that hands over its lanes' reads as they
+ * become final, and the host renders those parts in read order with a pool
  * of threads while the devices continue.  Records land in
  * ascending read order (= the reference's -n_threads 1 file). */
 #ifndef IMSAME_PIPE_H
@@ -28,19 +29,21 @@ typedef struct {
     imsame_params prm;           /* want_paths is set from out_fd            */
     int out_fd;                  /* -1: no .align output                     */
     int render_threads;          /* host threads rendering (0: host_threads) */
-    uint64_t batch_reads;        /* reads per device call (0: automatic)     */
+    uint64_t batch_reads;        /* reads per device call (0: the whole shard) */
+    int out_mmap;                /* 1: write a regular output file through a shared
+                                    mapping (parallel copies), 0: pwrite      */
 } pipe_opts;
 
 typedef struct {
     int rc;                      /* 0, IMSAME_E_READ_TOO_LONG, or an error   */
     uint64_t stop;               /* reads [0, stop) were decided and written  */
     uint64_t accepted;           /* accepted reads among them                */
-    uint64_t bytes_out, batches;
+    uint64_t bytes_out, batches; /* batches: parts rendered                  */
     imsame_stats st;             /* summed over devices (ms_total: max)      */
-    double t_align;              /* first align call -> last batch finished  */
-    double t_render;             /* render threads' busy wall, summed per batch */
-    double t_write;              /* pwrite wall, summed per batch            */
-    double t_tail;               /* last batch finished -> output complete   */
+    double t_align;              /* first align call -> last part delivered  */
+    double t_render;             /* render threads' busy wall, summed per part */
+    double t_write;              /* pwrite wall, summed per part             */
+    double t_tail;               /* last part delivered -> output complete   */
 } pipe_result;
 
 /* parse "-devices" values: "N" (devices 0..N-1) or "d0,d1,..." */

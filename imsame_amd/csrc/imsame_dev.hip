@@ -214,11 +214,15 @@ __global__ void row_scatter_kernel(const int32_t *row, uint32_t n, uint32_t nb, 
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-// IMSAME_DEBUG_POISON=1: every device arena is filled with POISON_BYTE when it
-// is allocated and every per-call scratch arena again at the start of each
-// alignment call, so a kernel that reads memory it did not write this call
-// (the class of round 1's stale seam buffer) reads garbage
-// instead of a plausible leftover.  Debug only: results never depend on it.
+// IMSAME_DEBUG_POISON=1: every reused device arena is filled with POISON_BYTE
+// on the stream of the call that uses it -- the index build's buffers before
+// the build, every per-call scratch arena at the start of each alignment call,
+// the traceback / checkpoint / seam slots before each NW launch -- so a kernel
+// that reads memory it did not write this call (the class of round 1's stale
+// seam buffer) reads garbage instead of a plausible leftover.
+// (Never at allocation: a null-stream memset is not ordered with the
+// non-blocking streams that fill the buffer next.)  Debug only: results never
+// depend on it.
 #define POISON_BYTE 0xA5
 static bool poison_on() {
     static std::once_flag f;
@@ -226,6 +230,21 @@ static bool poison_on() {
     std::call_once(f, [] { const char *e = getenv("IMSAME_DEBUG_POISON"); on = e && atoi(e); });
     return on;
 }
+
+// With the flag, the host also waits for every kernel and names it on stderr
+// first, so a kernel that faults on poison is the last one named.
+static int poison_sync(hipStream_t s, const char *what, const void *who) {
+    if (!poison_on()) return 0;
+    fprintf(stderr, "[poison] %s ctx=%p\n", what, who);
+    fflush(stderr);
+    const hipError_t e = hipStreamSynchronize(s);
+    if (e != hipSuccess) {
+        fprintf(stderr, "[poison] %s failed: %s\n", what, hipGetErrorString(e));
+        return IMSAME_E_HIP;
+    }
+    return 0;
+}
+#define POISON_SYNC(s, what, who) do { if (int prc_ = poison_sync((s), (what), (who))) return prc_; } while (0)
 
 struct DBuf {
     void *p = nullptr; size_t cap = 0;
@@ -236,7 +255,6 @@ struct DBuf {
         size_t want = n + std::min<size_t>(n / 8, (size_t)1 << 30) + 4096;   // slack for regrowth, <= 1 GB
         if (hipMalloc(&p, want) != hipSuccess) { p = nullptr; return IMSAME_E_OOM; }
         cap = want;
-        if (poison_on() && hipMemset(p, POISON_BYTE, want) != hipSuccess) return IMSAME_E_HIP;
         return 0;
     }
     int poison(hipStream_t s) const {
@@ -313,6 +331,7 @@ struct imsame_ctx {
     std::vector<std::pair<float, float>> nw_iv;
     int nlanes = 1;                   // lanes of the running call (the seed scan's group size
                                       // follows the reads scanned across all of them)
+    std::vector<uint32_t> part_paths; // host copy of this lane's paths for an imsame_dev_align_parts callback
 };
 
 static inline uint64_t hqs(const imsame_ctx *c, uint64_t r) { return c->hq[r - c->q_lo]; }
@@ -545,6 +564,7 @@ extern "C" int imsame_dev_index(imsame_ctx *c, const uint8_t *db_seq, uint64_t d
     HIPCHK(hipMemsetAsync(c->fill.p, 0, (uint64_t)NBUCKETS * 4, s));
     if (db_len) kmer_code_kernel<<<gsblk(db_len, 256), 256, 0, s>>>(c->db.as<uint8_t>(), db_len, c->brk.as<uint32_t>(),
                                                                   c->codes.as<uint32_t>(), c->fill.as<uint32_t>());
+    POISON_SYNC(s, "kmer_code_kernel", c);
     // exclusive scan of the counts -> off[0..NB], off[NB] = total
     uint64_t total = 0;
     {
@@ -564,10 +584,12 @@ extern "C" int imsame_dev_index(imsame_ctx *c, const uint8_t *db_seq, uint64_t d
     if (db_len) kmer_scatter<<<gsblk(db_len, 256), 256, 0, s>>>(c->codes.as<uint32_t>(), db_len, c->off.as<uint64_t>(),
                                                               c->fill.as<uint32_t>(), c->db_start.as<uint64_t>(), n_db,
                                                               c->ent.as<uint2>());
+    POISON_SYNC(s, "kmer_scatter", c);
     uint32_t *nbig = c->fill.as<uint32_t>();       // fill is free again: reuse as a counter
     HIPCHK(hipMemsetAsync(nbig, 0, 4, s));
     segsort_small<<<nblk(NBUCKETS, 256), 256, 0, s>>>(c->off.as<uint64_t>(), c->ent.as<uint2>(),
                                                       c->big.as<uint32_t>(), nbig);
+    POISON_SYNC(s, "segsort_small", c);
     uint32_t hbig = 0;
     HIPCHK(hipMemcpyAsync(&hbig, nbig, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -695,6 +717,7 @@ extern "C" int imsame_dev_set_query_range_async(imsame_ctx *c, const uint8_t *q_
         a = b;
     }
     c->have_query = true;
+    POISON_SYNC(c->ustream, "query upload", c);
     return IMSAME_OK;
 }
 
@@ -897,6 +920,7 @@ static int launch_nw(imsame_ctx *c, NwPlan pl, const uint32_t *cread, const uint
     else                  nw_kernel<false><<<pl.blocks, 256, pl.lds, s>>>(P);
     HIPCHK(hipEventRecord(c->ev1, s));
     HIPCHK(hipGetLastError());
+    POISON_SYNC(s, pl.pk ? "nw16_kernel" : "nw_kernel", c);
     HIPCHK(hipEventSynchronize(c->ev1));
     float f = 0;
     HIPCHK(hipEventElapsedTime(&f, c->ev0, c->ev1));
@@ -1073,6 +1097,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     InitLaunch I = {qsd, read_from, n, c->res.as<imsame_read_result>(), c->cur_p.as<uint64_t>(),
                     c->cur_h.as<uint32_t>(), c->nmemo.as<uint8_t>(), c->rstat.as<uint8_t>(), c->act0.as<uint32_t>()};
     init_kernel<<<nblk(n, 256), 256, 0, s>>>(I);
+    POISON_SYNC(s, "init_kernel", c);
     HIPCHK(hipGetLastError());
     st.ms_setup = now_ms() - t_start;
 
@@ -1120,6 +1145,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         else if (L >= 4) seed_group_kernel<4><<<nblk((uint64_t)nact * 4, 256), 256, slds, s>>>(S);
         else if (L >= 2) seed_group_kernel<2><<<nblk((uint64_t)nact * 2, 256), 256, slds, s>>>(S);
         else             seed_kernel<<<nblk(nact, 256), 256, 0, s>>>(S);
+        POISON_SYNC(s, "seed kernel", c);
         HIPCHK(hipEventRecord(c->ev1, s));
         HIPCHK(hipGetLastError());
         uint64_t hc[3];
@@ -1155,6 +1181,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
                            (unsigned long long *)(ctr + C_NACC), (unsigned long long *)(ctr + C_ERR),
                            c->db_start.as<uint64_t>()};
             update_kernel<<<nblk(cls[k].n, 256), 256, 0, s>>>(U);
+            POISON_SYNC(s, "update_kernel", c);
             HIPCHK(hipGetLastError());
         }
         uint64_t nn = 0;
@@ -1246,9 +1273,44 @@ static double union_ms(std::vector<std::pair<float, float>> v) {
 #define LANE_MIN 32768
 #define LANE_READS 40000
 
+// Hand lane l's finished reads [a, b) to an imsame_dev_align_parts callback,
+// with its paths copied to the host (path_off of those rows index them).
+static int deliver_part(imsame_ctx *l, const imsame_params *p, uint64_t a, uint64_t b, int rc, uint64_t used,
+                        uint64_t err_read, imsame_part_fn fn, void *user) {
+    const int status = (rc == IMSAME_E_PATHS) ? IMSAME_OK : rc;
+    uint64_t np = 0;
+    if (p->want_paths && used && (status == IMSAME_OK || status == IMSAME_E_READ_TOO_LONG)) {
+        l->part_paths.resize(used);
+        HIPCHK(hipMemcpyAsync(l->part_paths.data(), l->paths.p, used * 4, hipMemcpyDeviceToHost, l->stream));
+        HIPCHK(hipStreamSynchronize(l->stream));
+        np = used;
+    }
+    fn(user, a, b, status, status == IMSAME_E_READ_TOO_LONG ? err_read : ~0ull, np ? l->part_paths.data() : nullptr, np);
+    return 0;
+}
+
+static int align_impl(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64_t n_threads_semantic,
+                      const imsame_params *p, imsame_read_result *res, uint32_t *paths, uint64_t paths_cap,
+                      uint64_t *paths_used, imsame_stats *stats, imsame_part_fn fn, void *user);
+
 extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64_t n_threads_semantic,
                                 const imsame_params *p, imsame_read_result *res, uint32_t *paths, uint64_t paths_cap,
                                 uint64_t *paths_used, imsame_stats *stats) {
+    return align_impl(c, read_from, read_to, n_threads_semantic, p, res, paths, paths_cap, paths_used, stats, nullptr,
+                      nullptr);
+}
+
+extern "C" int imsame_dev_align_parts(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64_t n_threads_semantic,
+                                      const imsame_params *p, imsame_read_result *res, imsame_part_fn fn, void *user,
+                                      imsame_stats *stats) {
+    if (!fn) return IMSAME_E_ARG;
+    uint64_t used = 0;
+    return align_impl(c, read_from, read_to, n_threads_semantic, p, res, nullptr, 0, &used, stats, fn, user);
+}
+
+static int align_impl(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64_t n_threads_semantic,
+                      const imsame_params *p, imsame_read_result *res, uint32_t *paths, uint64_t paths_cap,
+                      uint64_t *paths_used, imsame_stats *stats, imsame_part_fn fn, void *user) {
     const double t_start = now_ms();
     if (!c || !p || (!res && read_to > read_from)) return IMSAME_E_ARG;
     if (!c->have_index || !c->have_query) return IMSAME_E_STATE;
@@ -1286,9 +1348,16 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
     while (nl > 1 && n < (uint64_t)nl * lane_min) --nl;
     if (c->is_sub || c->use_wcap || ymax > (uint64_t)NW_W / 2) nl = 1;
     if (nl == 1) {
-        const int rc = align_one(c, read_from, read_to, n_threads_semantic, p, res, paths, paths_cap, paths_used,
-                                 stats);
-        if (stats) { stats->ms_nw_busy = union_ms(c->nw_iv); span_ms(c->nw_iv, &stats->ms_nw_first, &stats->ms_nw_last); }
+        imsame_stats s1;
+        int rc = align_one(c, read_from, read_to, n_threads_semantic, p, res, paths, paths_cap, paths_used, &s1);
+        s1.ms_nw_busy = union_ms(c->nw_iv);
+        span_ms(c->nw_iv, &s1.ms_nw_first, &s1.ms_nw_last);
+        if (stats) *stats = s1;
+        if (fn) {
+            const int rd = deliver_part(c, p, read_from, read_to, rc, paths_used ? *paths_used : 0, s1.err_read, fn, user);
+            if (rd) return rd;
+            if (rc == IMSAME_E_PATHS) rc = IMSAME_OK;
+        }
         return rc;
     }
     std::vector<imsame_ctx *> L(nl, c);
@@ -1318,12 +1387,18 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
     std::vector<imsame_stats> S(nl);
     std::vector<int> R(nl, 0);
     std::vector<std::thread> th;
-    for (int k = 1; k < nl; ++k)
-        th.emplace_back([&, k] {
-            R[k] = align_one(L[k], cut[k], cut[k + 1], n_threads_semantic, p, res + (cut[k] - read_from), nullptr, 0,
-                             &used[k], &S[k]);
-        });
-    R[0] = align_one(c, cut[0], cut[1], n_threads_semantic, p, res, nullptr, 0, &used[0], &S[0]);
+    // each lane runs on its own host thread (lane 0 on the caller's) and,
+    // with a callback, hands over its reads as soon as they are final
+    auto lane_run = [&](int k) {
+        R[k] = align_one(L[k], cut[k], cut[k + 1], n_threads_semantic, p, res + (cut[k] - read_from), nullptr, 0,
+                         &used[k], &S[k]);
+        if (fn) {
+            const int rd = deliver_part(L[k], p, cut[k], cut[k + 1], R[k], used[k], S[k].err_read, fn, user);
+            if (rd) R[k] = rd;
+        }
+    };
+    for (int k = 1; k < nl; ++k) th.emplace_back(lane_run, k);
+    lane_run(0);
     for (auto &t : th) t.join();
     for (int k = 1; k < nl; ++k) L[k]->origin = nullptr;
     for (int k = 0; k < nl; ++k) L[k]->nlanes = 1;
@@ -1332,10 +1407,11 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
     int ret = IMSAME_OK;
     for (int r : R)
         if (r == IMSAME_E_READ_TOO_LONG) ret = IMSAME_E_READ_TOO_LONG;
-    // one result set: each lane's paths follow the previous lanes'
+    // one result set: each lane's paths follow the previous lanes' (parts:
+    // each part's rows index its own paths, handed over in the callback)
     uint64_t base = 0;
     for (int k = 0; k < nl; ++k) {
-        if (p->want_paths && k)
+        if (p->want_paths && k && !fn)
             for (uint64_t r = cut[k]; r < cut[k + 1]; ++r) {
                 imsame_read_result &x = res[r - read_from];
                 if (x.status == 1 && x.path_len) x.path_off += (uint32_t)base;
@@ -1370,7 +1446,7 @@ extern "C" int imsame_dev_align(imsame_ctx *c, uint64_t read_from, uint64_t read
     c->paths_split = true; c->paths_n = used[0]; c->paths_on_host = false;
     c->lane_paths.assign(used.begin() + 1, used.end());
     if (paths_used) *paths_used = base;
-    if (p->want_paths && base) {
+    if (p->want_paths && base && !fn) {
         if (base > paths_cap || !paths) { if (ret == IMSAME_OK) ret = IMSAME_E_PATHS; }
         else {
             uint64_t got = 0;

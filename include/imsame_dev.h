@@ -224,6 +224,26 @@ int imsame_dev_align(imsame_ctx *ctx, uint64_t read_from, uint64_t read_to,
                      imsame_read_result *res, uint32_t *paths, uint64_t paths_cap,
                      uint64_t *paths_used, imsame_stats *stats);
 
+/* imsame_dev_align that hands the results over as they become final -- the
+ * reference's workers write each accepted record as soon as it is found
+ * (alignmentFunctions.c:165-168), so its output starts long before the last
+ * thread joins (IMSAME.c:460-462).  The call runs its lanes as
+ * imsame_dev_align does and, as soon as lane k's reads [a, b) are final,
+ * calls part(user, a, b, status, err_read, paths, n_paths) from that lane's
+ * host thread: res[a - read_from .. b - read_from) are complete, and when
+ * prm->want_paths their path_off index `paths` (n_paths entries, valid
+ * during the callback only).  status: IMSAME_OK, IMSAME_E_READ_TOO_LONG (rows
+ * below err_read are complete) or another IMSAME_E_* code.  The parts cover
+ * [read_from, read_to) exactly, arrive in any order and may run
+ * concurrently; the call returns when every part's callback has returned,
+ * with the first failure it saw (IMSAME_E_PATHS never: the paths go through
+ * the callbacks; imsame_dev_fetch_paths does not apply). */
+typedef void (*imsame_part_fn)(void *user, uint64_t read_from, uint64_t read_to, int status, uint64_t err_read,
+                               const uint32_t *paths, uint64_t n_paths);
+int imsame_dev_align_parts(imsame_ctx *ctx, uint64_t read_from, uint64_t read_to, uint64_t n_threads_semantic,
+                           const imsame_params *prm, imsame_read_result *res, imsame_part_fn part, void *user,
+                           imsame_stats *stats);
+
 /* imsame_dev_align on the loaded index when it holds ONE SLICE (whole
  * records) of a larger database: ev_db_len is the whole database's length
  * for the e-value (0 = the loaded index's), win_cap[k] (host, may be NULL)

@@ -620,14 +620,15 @@ def test_path_arena_overflow_rewalks_only_lost_reads(dev, monkeypatch):
 @pytest.mark.parametrize("name", G.e2e_cases())
 def test_cli_devices_matches_reference_golden(name):
     """imsame -devices 0,0 (two contexts, each holding one shard of the
-    query) with tiny batches and 3 render threads: the reference's .align
-    bytes and [INFO] lines for every -n_threads."""
+    query) with tiny batches, 3 render threads and the output written through
+    a shared mapping (-out_mmap 1): the reference's .align bytes and [INFO]
+    lines for every -n_threads."""
     case = G.e2e_case(name)
     for T in case["meta"]["runs"]:
         with tempfile.TemporaryDirectory() as td:
             outp = os.path.join(td, "o.align")
             p = subprocess.run([CLI, "-query", case["query"], "-db", case["db"], "-out", outp, "-n_threads", T,
-                                "-devices", "0,0", "-batch_reads", "7", "-render_threads", "3",
+                                "-devices", "0,0", "-batch_reads", "7", "-render_threads", "3", "-out_mmap", "1",
                                 *case["meta"]["extra"]], stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=300)
             blob = open(outp, "rb").read() if os.path.exists(outp) else b""
             G.check_cli_against_golden(case, int(T), p.returncode, p.stdout, blob)
@@ -635,22 +636,24 @@ def test_cli_devices_matches_reference_golden(name):
 
 def test_cli_multi_device_output_identical(tmp_path):
     """C2 shape (2 Mbp, 12k reads) through the CLI: one context vs three
-    (-devices 0,0,0) with batches of 1000 reads -- identical .align bytes,
-    equal to the device results rendered record by record."""
+    (-devices 0,0,0) with batches of 1000 reads, one render thread, the
+    output through a shared mapping, and 4 lanes handing over their parts
+    out of order -- identical .align bytes."""
     ref, rst = synth.make_reference_arr(2_000_000, 2_000, seed=42)
     q, qs = synth.make_reads_arr(ref, 12_000, 150, seed=43)
     dbf, qf = str(tmp_path / "db.fa"), str(tmp_path / "q.fa")
     synth.write_fasta(dbf, ref, rst, "ref")
     synth.write_fasta(qf, q, qs, "read", width=0)
     outs = []
-    for extra in ([], ["-devices", "0,0,0", "-batch_reads", "1000"], ["-render_threads", "1"]):
+    for extra, env in (([], {}), (["-devices", "0,0,0", "-batch_reads", "1000"], {}), (["-render_threads", "1"], {}),
+                       (["-out_mmap", "1"], {"IMSAME_LANES": "4", "IMSAME_LANE_MIN": "1000"})):
         o = str(tmp_path / f"o{len(outs)}.align")
         p = subprocess.run([CLI, "-query", qf, "-db", dbf, "-out", o, "-n_threads", "16", *extra],
-                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=300)
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=300, env=dict(os.environ, **env))
         assert p.returncode == 0, p.stderr[-2000:]
         assert b'"accepted"' in p.stderr
         outs.append(open(o, "rb").read())
-    assert outs[0] == outs[1] == outs[2]
+    assert outs[0] == outs[1] == outs[2] == outs[3]
     assert outs[0].count(b" $$$$$$$ \n") > 10_000
 
 
@@ -695,6 +698,34 @@ def test_eight_skewed_lanes_equal_one_lane(dev, monkeypatch):
     monkeypatch.setenv("IMSAME_LANE_SKEW", "0.9")
     sk, _, _ = dev.align(n_threads=16)
     assert not _cmp(sk, one), _cmp(sk, one)
+
+
+def test_align_parts_hand_over_every_lane(dev, monkeypatch):
+    """imsame_dev_align_parts: the lanes' parts cover the range exactly, each
+    with its own paths, and give the rows and .align text of one call to
+    imsame_dev_align (the CLI renders parts as they arrive)."""
+    ref, rst = synth.make_reference_arr(4_000_000, 2_000, seed=61)
+    q, qs = synth.make_reads_arr(ref, 140_000, 150, seed=62, ins=0.003, dele=0.003)
+    dev.index(ref, rst)
+    dev.set_query(q, qs)
+    whole, pw, _ = dev.align(n_threads=7, want_paths=True)
+    for lanes in ("1", "4"):
+        monkeypatch.setenv("IMSAME_LANES", lanes)
+        res, parts, st = dev.align_parts(n_threads=7, want_paths=True)
+        assert st.lanes == int(lanes) and len(parts) == int(lanes)
+        cov = sorted((a, b) for a, b, *_ in parts)
+        assert cov[0][0] == 0 and cov[-1][1] == len(qs) and all(x[1] == y[0] for x, y in zip(cov, cov[1:]))
+        assert all(s == 0 and e == 2 ** 64 - 1 for _, _, s, e, _ in parts)
+        assert not _cmp(res, whole)
+        for a, b, _, _, pp in parts:
+            for k in np.flatnonzero(res["status"][a:b] == 1)[::97] + a:
+                r, r0 = res[k], whole[k]
+                s_ = int(r["db_seq"])
+                X = ref[int(rst[s_]):int(rst[s_]) + 2_000].tobytes()
+                Y = q[int(qs[k]):int(qs[k]) + 150].tobytes()
+                t1, _ = render(X, Y, r, pp[r["path_off"]:r["path_off"] + r["path_len"]])
+                t0, _ = render(X, Y, r0, pw[r0["path_off"]:r0["path_off"] + r0["path_len"]])
+                assert t1 == t0, k
 
 
 def test_lanes_equal_one_lane(dev, monkeypatch):
