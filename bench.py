@@ -415,8 +415,6 @@ def run_e2e(ref, rst, q, qs, a):
         out = outf if free > need else "/dev/null"
         t0 = time.monotonic()
         extra = os.environ.get("IMSAME_E2E_ARGS", "").split()          # experiments, e.g. -batch_reads N
-        if os.environ.get("IMSAME_E2E_MMAP"):
-            extra += ["-out_mmap", os.environ["IMSAME_E2E_MMAP"]]
         p = subprocess.run([cli, "-query", qf, "-db", dbf, "-out", out, "-n_threads", str(a.n_threads)] + extra,
                            stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=900)
         wall = time.monotonic() - t0

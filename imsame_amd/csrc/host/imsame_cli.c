@@ -12,8 +12,7 @@
  * reads are sharded over several device contexts, the multi-GPU form of the
  * reference's -n_threads fan-out, IMSAME.c:414-467), -max_read_size N (raise
  * the 3000-base NW cap of structs.h:19; the reference has it compile-time
- * only), -slice_bases N, -render_threads N, -batch_reads N, -out_mmap 0|1.
- * The .align records are rendered by a thread pool as the device hands over
+ * only), -slice_bases N, -render_threads N, -batch_reads N.  The .align records are rendered by a thread pool as the device hands over
  * finished parts of the reads, while it aligns the rest (imsame_pipe.c).  Timing lines report wall-clock seconds (the reference
  * prints clock(), i.e. CPU time summed over threads); a JSON phase line goes
  * to stderr.
@@ -74,7 +73,6 @@ static void usage(void) {
     printf("           -slice_bases [Integer: index the database in slices of at most this many bases]\n");
     printf("           -render_threads [Integer: host threads writing the .align records]\n");
     printf("           -batch_reads [Integer: reads per device call]\n");
-    printf("           -out_mmap   [0|1: write the .align through a shared mapping]\n");
     exit(1);
 }
 
@@ -87,7 +85,7 @@ int main(int argc, char **argv) {
     imsame_params prm;
     imsame_params_default(&prm);
     uint64_t T = 4;                                   /* IMSAME.c:49 */
-    int device = 0, render_threads = 0, out_mmap = 0;
+    int device = 0, render_threads = 0;
     uint64_t slice_bases = 0, batch_reads = 0;       /* 0: one index (the reference's) */
     /* init_args, IMSAME.c:520-578 (same strcmp scan over every argv slot) */
     for (int a = 0; a < argc; a++) {
@@ -117,11 +115,10 @@ int main(int argc, char **argv) {
         if (!strcmp(argv[a], "-slice_bases")) slice_bases = strtoull(argv[a + 1], NULL, 10);
         if (!strcmp(argv[a], "-render_threads")) render_threads = atoi(argv[a + 1]);
         if (!strcmp(argv[a], "-batch_reads")) batch_reads = strtoull(argv[a + 1], NULL, 10);
-        if (!strcmp(argv[a], "-out_mmap")) out_mmap = atoi(argv[a + 1]);
     }
     if (!qpath || !dpath) terror("A query and database is required");
     /* the reference fopen()s "wt" and never checks it (IMSAME.c:541-551) */
-    int out_fd = opath ? open(opath, (out_mmap ? O_RDWR : O_WRONLY) | O_CREAT | O_TRUNC, 0666) : -1;
+    int out_fd = opath ? open(opath, O_WRONLY | O_CREAT | O_TRUNC, 0666) : -1;
     int devs[PIPE_MAX_DEV], G = 1;
     devs[0] = device;
     if (devspec) G = pipe_parse_devices(devspec, devs, PIPE_MAX_DEV);
@@ -208,7 +205,7 @@ int main(int argc, char **argv) {
         free(paths);
     } else {
         pipe_opts po = {.T = T, .prm = prm, .out_fd = out_fd, .render_threads = render_threads,
-                        .batch_reads = batch_reads, .out_mmap = out_mmap};
+                        .batch_reads = batch_reads};
         rc = pipe_align_render(dv, G, &db, &q, &po, &pr);
         if (rc && rc != IMSAME_E_READ_TOO_LONG) terror(imsame_strerror(rc));
     }

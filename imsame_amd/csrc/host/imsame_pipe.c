@@ -17,7 +17,6 @@
 #include <fcntl.h>
 #include <inttypes.h>
 #include <pthread.h>
-#include <sys/mman.h>
 #include <time.h>
 #include <unistd.h>
 #include "imsame_pipe.h"
@@ -134,8 +133,6 @@ typedef struct {
     host_text text, scratch;           /* reused across batches */
     uint64_t off;
     int fd, err;
-    char *map;                         /* mmap output: the part's mapping, file offset map_base */
-    uint64_t map_base;
 } rtask;
 
 static void *render_task(void *a) {
@@ -180,12 +177,6 @@ static void *write_task(void *a) {
     return NULL;
 }
 
-static void *copy_task(void *a) {
-    rtask *t = a;
-    memcpy(t->map + (t->off - t->map_base), t->text.buf, t->text.len);
-    return NULL;
-}
-
 static void run_pool(rtask *t, int n, void *(*fn)(void *)) {
     pthread_t th[HOST_MAX_THREADS];
     int started[HOST_MAX_THREADS] = {0};
@@ -221,31 +212,15 @@ static int render_part(rtask *t, int *nt, const host_seqs *db, const host_seqs *
     return 0;
 }
 
-/* mmap output: the file grows to the part's end and the tasks copy their
- * buffers into a shared mapping of it in parallel (a write() of one file
- * copies into the page cache under the file's lock, one writer at a time;
- * page faults on a shared mapping run in parallel) */
-static int map_part(rtask *t, int nt, int fd) {
-    const uint64_t lo = t[0].off, hi = t[nt - 1].off + t[nt - 1].text.len;
-    if (hi <= lo) return 0;
-    if (ftruncate(fd, (off_t)hi) != 0) return errno;
-    const uint64_t pg = (uint64_t)sysconf(_SC_PAGESIZE), base = lo / pg * pg;
-    char *m = mmap(NULL, hi - base, PROT_READ | PROT_WRITE, MAP_SHARED, fd, (off_t)base);
-    if (m == MAP_FAILED) return errno;
-    for (int k = 0; k < nt; ++k) { t[k].map = m; t[k].map_base = base; }
-    run_pool(t, nt, copy_task);
-    return munmap(m, hi - base) ? errno : 0;
-}
-
-/* write what render_part left in t[0..nt): parallel pwrite at the offsets
- * (seekable 1), copies into a mapping of the file (seekable 2), or ordered
- * write() for pipes; returns an errno and the wall time in *secs */
+/* write what render_part left in t[0..nt): parallel pwrite at the offsets,
+ * or ordered write() for pipes; returns an errno and the wall time in *secs.
+ * (Writing through a shared mapping of the file instead -- parallel page
+ * faults, no file lock -- measured 3.6x slower on the GPU box's overlay
+ * filesystem: 1.42 s vs 0.40 s for the 3 GB of C2, profiles/r3c_e2e_*.) */
 static int write_part(rtask *t, int nt, int fd, int seekable, double *secs) {
     const double t0 = pipe_now();
     int err = 0;
-    if (seekable == 2) {
-        err = map_part(t, nt, fd);
-    } else if (seekable) {
+    if (seekable) {
         run_pool(t, nt, write_task);
         for (int k = 0; k < nt && !err; ++k) err = t[k].err;
     } else {
@@ -451,9 +426,8 @@ int pipe_align_render(pipe_dev *d, int G, const host_seqs *db, const host_seqs *
     for (int g = 0; g < G; ++g)
         if (!started[g]) align_worker(&W[g]);
     /* render the parts in read order as they arrive */
-    int seekable = prm.want_paths && lseek(o->out_fd, 0, SEEK_CUR) >= 0;
+    const int seekable = prm.want_paths && lseek(o->out_fd, 0, SEEK_CUR) >= 0;
     uint64_t off = seekable ? (uint64_t)lseek(o->out_fd, 0, SEEK_CUR) : 0;
-    if (seekable && o->out_mmap) seekable = 2;
     int rc = 0, werr = 0, nrend = 0;
     writer wr = {0};
     uint64_t nxt = 0;

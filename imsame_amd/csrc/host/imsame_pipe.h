@@ -30,8 +30,6 @@ typedef struct {
     int out_fd;                  /* -1: no .align output                     */
     int render_threads;          /* host threads rendering (0: host_threads) */
     uint64_t batch_reads;        /* reads per device call (0: the whole shard) */
-    int out_mmap;                /* 1: write a regular output file through a shared
-                                    mapping (parallel copies), 0: pwrite      */
 } pipe_opts;
 
 typedef struct {

@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # One GPU-box pass for round 3:  gpurun -- bash scripts/gpu_r3.sh <tag> [steps...]
 # A step "e:VAR=VAL,VAR2=VAL2:step" runs `step` with those variables set (its
-# outputs get a suffix from them).  Every GPU step runs under its own time
+# outputs get a suffix from them); "t:a+b" runs the GPU tests matching -k "a or b".  Every GPU step runs under its own time
 # limit; a step that fails with anything but pytest's "tests failed" (1) ends
 # the script (no GPU work after a fault).
 set -uo pipefail
@@ -23,7 +23,7 @@ run_step() {   # $1 = step, $2 = output suffix
     # the GPU suite once with every reused device arena poisoned (IMSAME_DEBUG_POISON)
     poison) IMSAME_DEBUG_POISON=1 timeout -k 10 1500 $PYT tests -m gpu > $O/pytest_poison_${TAG}$X.log 2>&1
             ok_or_stop $? poison$X ;;
-    t:*) K=${s#t:}; timeout -k 10 900 $PYT tests -m gpu -k "$K" > $O/pytest_sel_${TAG}$X.log 2>&1; ok_or_stop $? "$s$X" ;;
+    t:*) K=${s#t:}; K=${K//+/ or }; timeout -k 10 900 $PYT tests -m gpu -k "$K" > $O/pytest_sel_${TAG}$X.log 2>&1; ok_or_stop $? "$s$X" ;;
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_${TAG}$X.log 2>&1
            ok_or_stop $? smoke$X ;;
     bench) timeout -k 10 900 python -u bench.py > $O/bench_${TAG}$X.json 2> $O/bench_${TAG}$X.err; ok_or_stop $? bench$X ;;

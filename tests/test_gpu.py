@@ -620,15 +620,14 @@ def test_path_arena_overflow_rewalks_only_lost_reads(dev, monkeypatch):
 @pytest.mark.parametrize("name", G.e2e_cases())
 def test_cli_devices_matches_reference_golden(name):
     """imsame -devices 0,0 (two contexts, each holding one shard of the
-    query) with tiny batches, 3 render threads and the output written through
-    a shared mapping (-out_mmap 1): the reference's .align bytes and [INFO]
-    lines for every -n_threads."""
+    query) with tiny batches and 3 render threads: the reference's .align
+    bytes and [INFO] lines for every -n_threads."""
     case = G.e2e_case(name)
     for T in case["meta"]["runs"]:
         with tempfile.TemporaryDirectory() as td:
             outp = os.path.join(td, "o.align")
             p = subprocess.run([CLI, "-query", case["query"], "-db", case["db"], "-out", outp, "-n_threads", T,
-                                "-devices", "0,0", "-batch_reads", "7", "-render_threads", "3", "-out_mmap", "1",
+                                "-devices", "0,0", "-batch_reads", "7", "-render_threads", "3",
                                 *case["meta"]["extra"]], stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=300)
             blob = open(outp, "rb").read() if os.path.exists(outp) else b""
             G.check_cli_against_golden(case, int(T), p.returncode, p.stdout, blob)
@@ -636,9 +635,8 @@ def test_cli_devices_matches_reference_golden(name):
 
 def test_cli_multi_device_output_identical(tmp_path):
     """C2 shape (2 Mbp, 12k reads) through the CLI: one context vs three
-    (-devices 0,0,0) with batches of 1000 reads, one render thread, the
-    output through a shared mapping, and 4 lanes handing over their parts
-    out of order -- identical .align bytes."""
+    (-devices 0,0,0) with batches of 1000 reads, one render thread, and 4
+    lanes handing over their parts out of order -- identical .align bytes."""
     ref, rst = synth.make_reference_arr(2_000_000, 2_000, seed=42)
     q, qs = synth.make_reads_arr(ref, 12_000, 150, seed=43)
     dbf, qf = str(tmp_path / "db.fa"), str(tmp_path / "q.fa")
@@ -646,7 +644,7 @@ def test_cli_multi_device_output_identical(tmp_path):
     synth.write_fasta(qf, q, qs, "read", width=0)
     outs = []
     for extra, env in (([], {}), (["-devices", "0,0,0", "-batch_reads", "1000"], {}), (["-render_threads", "1"], {}),
-                       (["-out_mmap", "1"], {"IMSAME_LANES": "4", "IMSAME_LANE_MIN": "1000"})):
+                       ([], {"IMSAME_LANES": "4", "IMSAME_LANE_MIN": "1000"})):
         o = str(tmp_path / f"o{len(outs)}.align")
         p = subprocess.run([CLI, "-query", qf, "-db", dbf, "-out", o, "-n_threads", "16", *extra],
                            stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=300, env=dict(os.environ, **env))
