@@ -75,7 +75,9 @@ CONFIGS = {
 def nw_kernel_name(read_len, record_bp, igap=-5, egap=-2):
     """The NW kernel imsame_dev.hip:plan_nw picks for this shape (mirror of
     nw16_kernel.hip:nw16_fits for the default gap parameters)."""
-    if igap > 0 or egap > 0 or read_len > 160:
+    if read_len > 160:
+        return "nw_kernel" if igap > 0 or egap > 0 else "nwl_kernel"     # nwl_kernel.hip: long reads
+    if igap > 0 or egap > 0:
         return "nw_kernel"
     ycols = -(-read_len // 10) * 10
     R = 4 * ycols - igap - egap * (record_bp + 64 + ycols + 2) + 16
@@ -260,8 +262,7 @@ def main():
     # launches exceeds that time by launch_overlap (scripts/nw_busy.py
     # recomputes the union from the kernel trace)
     achieved = alg_bytes / (nw_busy / 1e3) / 1e9 if nw_busy else 0.0
-    kernel = nw_kernel_name(a.read_len, a.record_bp) if not stats[-1]["nw_launches"] or a.read_len <= 160 \
-        else "nw_kernel"
+    kernel = nw_kernel_name(a.read_len, a.record_bp)
     per_launch = alg_bytes / max(nw_launches, 1)
     traffic = bpc = None
     if os.path.exists(a.traffic_json):

@@ -27,6 +27,7 @@
 #include "tables.h"
 #include "nw_kernel.hip"
 #include "nw16_kernel.hip"
+#include "nwl_kernel.hip"
 #include "seed_kernel.hip"
 
 
@@ -783,8 +784,17 @@ static int build_tables(imsame_ctx *c, const imsame_params *p, uint32_t ymax, ui
     return 0;
 }
 
-struct NwPlan { int G, GPW, xcap, xstride, steps, nstr; bool pk, last4, two; size_t lds; unsigned blocks, max_blocks;
-                uint64_t tb_dw, ck_dw; int band_w; };
+struct NwPlan { int G, GPW, xcap, xstride, steps, nstr; bool pk, last4, two, lng; size_t lds; unsigned blocks, max_blocks;
+                uint64_t tb_dw, ck_dw, bnd_dw; int band_w; };
+
+// Long reads take the two-pass nwl_kernel (nwl_kernel.hip) unless the int32
+// kernel is forced (IMSAME_FLAG_NW32, or IMSAME_NWL=0 for A/B runs).
+static bool nwl_enabled() {
+    static std::once_flag f;
+    static bool on = true;
+    std::call_once(f, [] { const char *e = getenv("IMSAME_NWL"); on = !(e && !atoi(e)); });
+    return on;
+}
 
 // Rows above its best cell the second nw16 sweep keeps (nw16_kernel.hip).  A
 // path longer than that (rare: C2 paths span <= 209 rows) makes its wave redo
@@ -813,14 +823,22 @@ static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, 
     const char *op = getenv("IMSAME_NW_ONEPASS");
     pl->two = pl->pk && !(p->flags & IMSAME_FLAG_NW16_ONEPASS) && !(op && atoi(op));
     pl->band_w = nw16_band_rows();
-    const NwShape sh = pl->pk ? nw16_shape(ymax, xcap) : nw_shape(ymax, xcap);
+    pl->lng = !pl->pk && !(p->flags & IMSAME_FLAG_NW32) && nwl_enabled() && nwl_fits(p->igap, p->egap, ymax);
+    if (pl->lng) {                  // steps of a pass-2 band (IMSAME_NWL_BAND: tests use small ones)
+        const char *nb = getenv("IMSAME_NWL_BAND");
+        pl->band_w = nb ? std::max(1, std::min(NWL_BAND, atoi(nb))) : NWL_BAND;
+    }
+    const NwShape sh = pl->pk ? nw16_shape(ymax, xcap) : pl->lng ? nwl_shape(ymax, xcap) : nw_shape(ymax, xcap);
     pl->G = sh.G; pl->GPW = sh.GPW; pl->nstr = sh.nstr; pl->xcap = sh.xcap; pl->xstride = sh.xstride;
     pl->steps = sh.steps;
-    pl->tb_dw = pl->pk ? nw16_tb_words(sh) : nw_tb_words(sh);
-    pl->ck_dw = pl->two ? nw16_ck_words(sh) : 0;
-    pl->lds = (size_t)wpb * (pl->pk ? nw16_wave_lds(pl->GPW, pl->xstride) : nw_wave_lds(pl->GPW, pl->xstride));
+    pl->tb_dw = pl->pk ? nw16_tb_words(sh) : pl->lng ? nwl_tb_words(sh, ymax) : nw_tb_words(sh);
+    pl->ck_dw = pl->two ? nw16_ck_words(sh) : pl->lng ? nwl_ck_words(sh) : 0;
+    pl->bnd_dw = pl->lng ? nwl_seam_words(sh) : 3ull * pl->xcap;
+    pl->lds = (size_t)wpb * (pl->pk ? nw16_wave_lds(pl->GPW, pl->xstride)
+                             : pl->lng ? nwl_wave_lds(pl->xstride) : nw_wave_lds(pl->GPW, pl->xstride));
     int per_cu = 0;
-    hipError_t oe = pl->two ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw16_kernel<false, true>, wpb * 64, pl->lds)
+    hipError_t oe = pl->lng ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nwl_kernel, wpb * 64, pl->lds)
+                  : pl->two ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw16_kernel<false, true>, wpb * 64, pl->lds)
                   : pl->pk ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw16_kernel<false, false>, wpb * 64, pl->lds)
                   : (pl->nstr > 1)
                       ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw_kernel<true>, wpb * 64, pl->lds)
@@ -836,7 +854,7 @@ static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, 
     // queue, so fewer blocks finish the same work.  Budget: what is free
     // (counting the arena already held) less 8 GB of headroom -- the 288 GB
     // of HBM are there to keep waves resident.
-    const uint64_t per_block = (uint64_t)wpb * (pl->tb_dw * 4 + pl->ck_dw * 4 + 3ull * pl->xcap * 4);
+    const uint64_t per_block = (uint64_t)wpb * (pl->tb_dw * 4 + pl->ck_dw * 4 + pl->bnd_dw * 4);
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = 0;
     const uint64_t held = c->tb.cap + c->bnd.cap + c->ck.cap;
@@ -860,7 +878,7 @@ static int launch_nw(imsame_ctx *c, NwPlan pl, const uint32_t *cread, const uint
     hipStream_t s = c->stream;
     const uint64_t tb_dw = pl.tb_dw;
     // fewer resident waves if the arena cannot be had (the queue still drains)
-    const uint64_t per_slot = tb_dw * 4, bnd_slot = 3ull * pl.xcap * 4, ck_slot = pl.ck_dw * 4;
+    const uint64_t per_slot = tb_dw * 4, bnd_slot = pl.bnd_dw * 4, ck_slot = pl.ck_dw * 4;
     if (c->tb.cap < (uint64_t)pl.blocks * 4 * per_slot)       // grow once to this shape's full residency
         (void)c->tb.ensure((uint64_t)pl.max_blocks * 4 * per_slot);
     if (ck_slot && c->ck.cap < (uint64_t)pl.blocks * 4 * ck_slot)
@@ -882,7 +900,7 @@ static int launch_nw(imsame_ctx *c, NwPlan pl, const uint32_t *cread, const uint
     P.igap = (int32_t)ig; P.egap = (int32_t)eg;
     P.G = pl.G; P.GPW = pl.GPW; P.xcap = pl.xcap; P.xstride = pl.xstride; P.steps = pl.steps;
     P.tb = c->tb.as<uint32_t>(); P.tb_wave_dw = tb_dw;
-    P.bnd = c->bnd.as<int32_t>(); P.bnd_wave = (uint64_t)3 * pl.xcap;
+    P.bnd = c->bnd.as<int32_t>(); P.bnd_wave = pl.bnd_dw;
     P.minlen = c->minlen.as<uint32_t>(); P.n_minlen = ymax + 1;
     P.minident = c->minident.as<uint32_t>(); P.n_minident = xmax + ymax + 2;
     P.counter = work;
@@ -891,7 +909,7 @@ static int launch_nw(imsame_ctx *c, NwPlan pl, const uint32_t *cread, const uint
     P.paths = c->paths.as<uint32_t>(); P.paths_cap = paths_cap;
     P.paths_used = (uint32_t *)(ctr + C_PATHS); P.want_paths = p->want_paths;
     P.flags = (uint32_t *)(ctr + C_FLAGS);
-    P.ck = pl.two ? c->ck.as<uint32_t>() : nullptr; P.ck_wave_dw = pl.ck_dw;
+    P.ck = (pl.two || pl.lng) ? c->ck.as<uint32_t>() : nullptr; P.ck_wave_dw = pl.ck_dw;
     P.band_w = pl.band_w; P.redo = (uint32_t *)(ctr + C_REDO); P.win = (uint32_t *)(ctr + C_WIN);
     P.prof = getenv("IMSAME_NW_PROF") ? (unsigned long long *)(ctr + C_PROF) : nullptr;
     HIPCHK(hipMemsetAsync(work, 0, 4, s));
@@ -912,7 +930,8 @@ static int launch_nw(imsame_ctx *c, NwPlan pl, const uint32_t *cread, const uint
         const char *wb = getenv("IMSAME_NW_WIN_BOTTOM");
         P.win_bottom = wb ? atoi(wb) : NW16_WIN_BOTTOM;
     }
-    if (pl.two && pl.last4)     nw16_kernel<true, true><<<pl.blocks, 256, pl.lds, s>>>(P);
+    if (pl.lng)                 nwl_kernel<<<pl.blocks, 256, pl.lds, s>>>(P);
+    else if (pl.two && pl.last4) nw16_kernel<true, true><<<pl.blocks, 256, pl.lds, s>>>(P);
     else if (pl.two)            nw16_kernel<false, true><<<pl.blocks, 256, pl.lds, s>>>(P);
     else if (pl.pk && pl.last4) nw16_kernel<true, false><<<pl.blocks, 256, pl.lds, s>>>(P);
     else if (pl.pk)             nw16_kernel<false, false><<<pl.blocks, 256, pl.lds, s>>>(P);
@@ -920,7 +939,7 @@ static int launch_nw(imsame_ctx *c, NwPlan pl, const uint32_t *cread, const uint
     else                  nw_kernel<false><<<pl.blocks, 256, pl.lds, s>>>(P);
     HIPCHK(hipEventRecord(c->ev1, s));
     HIPCHK(hipGetLastError());
-    POISON_SYNC(s, pl.pk ? "nw16_kernel" : "nw_kernel", c);
+    POISON_SYNC(s, pl.pk ? "nw16_kernel" : pl.lng ? "nwl_kernel" : "nw_kernel", c);
     HIPCHK(hipEventSynchronize(c->ev1));
     float f = 0;
     HIPCHK(hipEventElapsedTime(&f, c->ev0, c->ev1));
@@ -1054,7 +1073,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     // (reads with a rejection emit <= n in all, S.spec below)
     const char *sw_env = getenv("IMSAME_SPEC_WEAK");
     const uint32_t spec_weak = (uint32_t)std::max(1, std::min(SPEC_MAX, sw_env ? atoi(sw_env) : SPEC_WEAK));
-    const uint64_t ccap = (uint64_t)n * (spec_weak > 1 ? spec_weak + 1 : 1);
+    const uint64_t ccap = (uint64_t)n * (spec_weak > 1 ? spec_weak + 1 : 2);
     if (c->res.ensure((uint64_t)n * 64) || c->cur_p.ensure((uint64_t)n * 8) || c->cur_h.ensure((uint64_t)n * 4) ||
         c->memo.ensure((uint64_t)n * 4 * MEMO) || c->nmemo.ensure(n) || c->rstat.ensure(n) ||
         c->act0.ensure((uint64_t)n * 4) || c->act1.ensure((uint64_t)n * 4) || c->cread.ensure(ccap * 4) ||
@@ -1120,7 +1139,8 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         S.nmemo = c->nmemo.as<uint8_t>(); S.rstat = c->rstat.as<uint8_t>();
         S.minraw = c->minraw.as<uint64_t>(); S.n_minraw = ymax + 1;
         S.max_rs = p->max_read_size; S.short_ylen = short_y; S.max_rec = c->max_rec;
-        S.spec = (st.rounds == 1) ? 1u : std::max<uint32_t>(1u, std::min<uint32_t>(spec_later, n / nact));
+        // (a round's candidates fit the ccap-entry lists: nact x spec <= ccap)
+        S.spec = (st.rounds == 1) ? 1u : (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(spec_later, ccap / nact));
         S.spec_weak = spec_weak;
         S.budget = seed_budget(budget1, (uint32_t)st.rounds, grow);
         S.next = nxt; S.nnext = (uint32_t *)(ctr + C_NNEXT);

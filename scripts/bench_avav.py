@@ -68,7 +68,10 @@ def main():
         runs = [dict(zip(("out", "reads", "accepted", "nw", "cells", "shards", "align_ms"),
                          (m[0], int(m[1]), int(m[2]), int(m[3]), int(m[4]), int(m[5]), float(m[6]))))
                 for m in re.findall(r"\] (\S+): reads=(\d+) accepted=(\d+) nw=(\d+) cells=(\d+) shards=(\d+) "
-                                    r"align_ms\(max\)=([\d.]+)", err)]
+                                    r"(?:batches=\d+ )?align_ms\(max\)=([\d.]+)", err)]
+        if not runs:
+            sys.stderr.write(err[-3000:])
+            raise SystemExit("no per-run lines in the driver's output")
         job = re.search(r"(\d+) runs, (\d+) skipped, (\d+) device contexts, ([\d.]+) s", err)
         total_reads = sum(r["reads"] for r in runs)
         align_s = sum(r["align_ms"] for r in runs) / 1e3

@@ -29,6 +29,7 @@ void sync() { t_wave->bar.arrive_and_wait(); }
 #include "../../imsame_amd/csrc/tables.h"
 #include "../../imsame_amd/csrc/nw_kernel.hip"
 #include "../../imsame_amd/csrc/nw16_kernel.hip"
+#include "../../imsame_amd/csrc/nwl_kernel.hip"
 #include "../../imsame_amd/csrc/seed_kernel.hip"
 
 static void run_wave(const std::function<void(int)> &f) {
@@ -59,13 +60,16 @@ static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, cons
     const bool pk = !(p->flags & IMSAME_FLAG_NW32) && nw16_fits(p->igap, p->egap, xmax, ymax);
     const char *op = getenv("IMSAME_NW_ONEPASS");
     const bool two = pk && !(p->flags & IMSAME_FLAG_NW16_ONEPASS) && !(op && atoi(op));
-    const NwShape sh = pk ? nw16_shape(ymax, xmax) : nw_shape(ymax, xmax);
-    std::vector<uint32_t> tb((pk ? nw16_tb_words(sh) : nw_tb_words(sh)) + 64, 0xABABABABu);
-    std::vector<uint32_t> ck(two ? nw16_ck_words(sh) : 1, 0xCDCDCDCDu);
+    const char *le = getenv("IMSAME_NWL");
+    const bool lng = !pk && !(p->flags & IMSAME_FLAG_NW32) && !(le && !atoi(le)) && nwl_fits(p->igap, p->egap, ymax);
+    const NwShape sh = pk ? nw16_shape(ymax, xmax) : lng ? nwl_shape(ymax, xmax) : nw_shape(ymax, xmax);
+    std::vector<uint32_t> tb((pk ? nw16_tb_words(sh) : lng ? nwl_tb_words(sh, ymax) : nw_tb_words(sh)) + 64, 0xABABABABu);
+    std::vector<uint32_t> ck(two ? nw16_ck_words(sh) : lng ? nwl_ck_words(sh) : 1, 0xCDCDCDCDu);
     const char *be = getenv("IMSAME_NW_BAND");
     // seam scratch poisoned like fresh device memory: a read before its write shows
-    std::vector<int32_t> bnd((size_t)3 * sh.xcap + 64, 0x70000000);
-    std::vector<uint8_t> lds((pk ? nw16_wave_lds(sh.GPW, sh.xstride) : nw_wave_lds(sh.GPW, sh.xstride)) + 64, 0xA5);
+    std::vector<int32_t> bnd((lng ? nwl_seam_words(sh) : (size_t)3 * sh.xcap) + 64, 0x70000000);
+    std::vector<uint8_t> lds((pk ? nw16_wave_lds(sh.GPW, sh.xstride)
+                              : lng ? nwl_wave_lds(sh.xstride) : nw_wave_lds(sh.GPW, sh.xstride)) + 64, 0xA5);
     uint32_t counter = 0;
     NwLaunch P;
     memset(&P, 0, sizeof P);
@@ -82,6 +86,10 @@ static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, cons
     P.flags = flags;
     P.ck = ck.data(); P.ck_wave_dw = ck.size();
     P.band_w = be ? std::max(0, atoi(be)) : 200;        // imsame_dev.hip:nw16_band_rows
+    if (lng) {                                            // imsame_dev.hip:plan_nw
+        const char *nb = getenv("IMSAME_NWL_BAND");
+        P.band_w = nb ? std::max(1, std::min(NWL_BAND, atoi(nb))) : NWL_BAND;
+    }
     P.redo = &g_redo;
     // queue order by predicted row, as imsame_dev.hip:launch_nw (row_bucket:
     // 8-row buckets, unpredicted first; stable here, any order is correct)
@@ -106,7 +114,8 @@ static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, cons
     P.win = &g_win;
     bool ymult = true;        // every read length a multiple of NW16_K (imsame_dev.hip: q_len_mult)
     for (uint32_t k = 0; k < n; ++k) ymult = ymult && (qs[cread[k] + 1] - qs[cread[k]]) % NW16_K == 0;
-    if (two && ymult)     run_wave([&](int lane) { nw16_wave<true, true>(P, lds.data(), lane, 0); });
+    if (lng)              run_wave([&](int lane) { nwl_wave(P, lds.data(), lane, 0); });
+    else if (two && ymult) run_wave([&](int lane) { nw16_wave<true, true>(P, lds.data(), lane, 0); });
     else if (two)         run_wave([&](int lane) { nw16_wave<false, true>(P, lds.data(), lane, 0); });
     else if (pk && ymult) run_wave([&](int lane) { nw16_wave<true, false>(P, lds.data(), lane, 0); });
     else if (pk)          run_wave([&](int lane) { nw16_wave<false, false>(P, lds.data(), lane, 0); });
@@ -215,7 +224,7 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
     // imsame_dev.hip:align_one -- speculation from a weak first candidate, candidate capacity
     const char *sw_env = getenv("IMSAME_SPEC_WEAK");
     const uint32_t spec_weak = (uint32_t)std::max(1, std::min(SPEC_MAX, sw_env ? atoi(sw_env) : SPEC_WEAK));
-    const size_t ccap = (size_t)n * (spec_weak > 1 ? spec_weak + 1 : 1);
+    const size_t ccap = (size_t)n * (spec_weak > 1 ? spec_weak + 1 : 2);
     std::vector<uint32_t> cur_h(n), memo((size_t)n * MEMO), act(n), nxt(n), cr(ccap), cs(ccap), cr2(ccap), cs2(ccap);
     std::vector<uint32_t> cbase(n), ccnt(n), perr(n);
     std::vector<int32_t> crow(ccap);
@@ -256,7 +265,7 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
         S.minlen = ml.data(); S.n_minlen = ymax + 1;
         S.minident = mi.data(); S.n_minident = xcap + ymax + 2;
         S.max_rs = p->max_read_size; S.short_ylen = short_y; S.max_rec = max_rec;
-        S.spec = (st.rounds == 1) ? 1u : std::max<uint32_t>(1u, std::min<uint32_t>(spec_later, n / nact));
+        S.spec = (st.rounds == 1) ? 1u : (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(spec_later, ccap / nact));
         S.spec_weak = spec_weak;
         S.budget = seed_budget(budget1, (uint32_t)st.rounds);
         S.next = nxt.data(); S.nnext = &nc[2];

@@ -270,6 +270,31 @@ def test_long_reads_multi_strip(dev, oracle):
     assert not _cmp(res, exp), _cmp(res, exp)
 
 
+@pytest.mark.parametrize("band", ["default", "70"])
+def test_long_two_pass_nw_vs_oracle(dev, oracle, band, monkeypatch):
+    """nwl_kernel.hip: reads of 161 .. 3000 columns (1-5 strips) in its
+    score-only pass and the walk over recomputed traceback bands -- every
+    field and every path's .align text equal to the oracle's and to the
+    one-pass int32 kernel (IMSAME_FLAG_NW32); a 70-step band makes the walks
+    cross many bands."""
+    from tests.test_host import _long_pairs
+    if band != "default":
+        monkeypatch.setenv("IMSAME_NWL_BAND", band)
+    for seed, (ig, eg) in ((21, (-5, -2)), (22, (0, 0)), (23, (-7, -1))):
+        X, Y = _long_pairs(seed, 24, 3001, 3001)
+        p = dev.params(igap=ig, egap=eg, min_coverage=1e-9, min_identity=1e-9)
+        res, paths, _ = dev.nw_pairs(X, Y, p, want_paths=True)
+        res32, _, _ = dev.nw_pairs(X, Y, dev.params(igap=ig, egap=eg, min_coverage=1e-9, min_identity=1e-9,
+                                                    flags=FLAG_NW32))
+        assert not _cmp(res, res32), _cmp(res, res32)
+        for k in range(len(X)):
+            o = oracle.nw(X[k], Y[k], igap=ig, egap=eg, text=True)
+            for f in ("score", "bx", "by", "length", "identities", "igaps", "egaps", "head_x", "head_y"):
+                assert int(res[k][f]) == int(o[f]), (f, k, ig, eg, len(X[k]), len(Y[k]))
+            txt, _ = render(X[k], Y[k], res[k], paths[res[k]["path_off"]:res[k]["path_off"] + res[k]["path_len"]])
+            assert txt == o["text"], k
+
+
 def _windows(n, w=1500, T=16):
     """start, middle (around a chunk head of -n_threads T) and end of a query"""
     rpt = n // T

@@ -217,6 +217,65 @@ def test_emulated_predicted_traceback_window(emu, oracle, seed_l, monkeypatch):
         assert np.array_equal(got0[f], exp[f]), f
 
 
+def _long_pairs(seed, n, ymax, xmax):
+    """Long reads (161 .. ymax, strip edges 639-641 included) against records,
+    70 % drawn from the record with substitutions and indels, 30 % random."""
+    rng = np.random.default_rng(seed)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    X, Y = [], []
+    for k in range(n):
+        xl = int(rng.integers(300, xmax))
+        yl = int(rng.choice([161, 170, 639, 640, 641, int(rng.integers(161, ymax))]))
+        x = acgt[rng.integers(0, 4, xl)]
+        if rng.random() < 0.7:
+            o0 = int(rng.integers(0, max(1, xl - yl)))
+            src, y = x[o0:o0 + yl], []
+            for b in src:
+                r = rng.random()
+                if r < 0.02:
+                    continue                                  # deletion
+                if r < 0.04:
+                    y.append(acgt[rng.integers(0, 4)])        # insertion
+                y.append(acgt[rng.integers(0, 4)] if rng.random() < 0.05 else b)
+            y = np.array(y[:yl], dtype=np.uint8)
+            if len(y) < yl:
+                y = np.concatenate([y, acgt[rng.integers(0, 4, yl - len(y))]])
+        else:
+            y = acgt[rng.integers(0, 4, yl)]
+        X.append(x.tobytes()); Y.append(y.tobytes())
+    return X, Y
+
+
+@pytest.mark.parametrize("band", ["default", "70"])
+def test_emulated_long_two_pass_nw_vs_oracle(emu, oracle, band, monkeypatch):
+    """nwl_kernel.hip (emulated): reads of 161 .. 1300 columns (1-3 strips of
+    640) in the score-only pass with seams and checkpoints, then the walk over
+    traceback bands recomputed on demand -- every field, and the .align text
+    of every path, equal to the oracle's.  A 70-step band makes every walk
+    span many bands (diagonal runs, up- and left-searches resumed across
+    them)."""
+    if band != "default":
+        monkeypatch.setenv("IMSAME_NWL_BAND", band)
+    redo = emu.lib.emu_redo_count
+    redo.restype = C.c_uint32
+    redo()
+    for seed, (ig, eg) in ((11, (-5, -2)), (12, (0, 0)), (13, (-3, -1))):
+        X, Y = _long_pairs(seed, 5, 1300, 1500)
+        p = oracle.params(igap=ig, egap=eg, want_paths=1, min_coverage=1e-9, min_identity=1e-9)
+        rc, res, paths, fl = emu.nw_pairs(X, Y, p, paths_cap=100_000)
+        assert rc == 0 and fl == 0
+        for k in range(len(X)):
+            o = oracle.nw(X[k], Y[k], igap=ig, egap=eg, text=True)
+            for f in ("score", "bx", "by", "length", "identities", "igaps", "egaps", "head_x", "head_y"):
+                assert int(res[k][f]) == int(o[f]), (f, k, ig, eg, len(X[k]), len(Y[k]))
+            assert res[k]["status"] == 1
+            txt, ident = imsame_amd.render(X[k], Y[k], res[k],
+                                           paths[res[k]["path_off"]:res[k]["path_off"] + res[k]["path_len"]])
+            assert txt == o["text"] and ident == o["identities"], k
+    extra = redo()                  # bands beyond one per strip
+    assert (extra > 20) if band == "70" else True
+
+
 def _strip_mix_pairs():
     """163- and 400-column reads in ONE launch: the launch takes the
     multi-strip kernel (ymax > 320) and the 163-column reads have one strip."""
