@@ -33,11 +33,11 @@
 // row), a search that leaves the band resuming where it stopped.
 #include "wave_ops.h"
 
-#define NWL_K    10                       // columns per lane
+#define NWL_K    10                       // columns per lane (<= 16: two traceback words)
 #define NWL_W    (64 * NWL_K)             // columns per strip
 #define NWL_BIG  (1 << 28)                // stands for INT64_MIN / "never"
 #define NWL_CK   128                      // checkpoint interval (steps; even: the rotation period)
-#define NWL_NST  (5 * NWL_K + 5)          // dwords of wave state per lane in a checkpoint
+#define NWL_NST  (4 * NWL_K + 5)          // dwords of wave state per lane in a checkpoint
 #define NWL_BAND 1024                     // steps a pass-2 band ends with (plus up to NWL_CK below)
 
 // the long kernel takes launches of reads longer than the packed kernel's
@@ -66,10 +66,13 @@ __host__ static inline uint64_t nwl_ck_words(const NwShape &s) {
 }
 __host__ static inline uint64_t nwl_seam_words(const NwShape &s) { return (uint64_t)s.nstr * (s.xcap + 1) * 3; }
 __host__ __device__ static inline uint64_t nwl_band_words() { return (uint64_t)(NWL_BAND + NWL_CK + 64) * 64 * 2; }
+// pass 2: band + path scratch; pass 1: the last column's strip cells (K per row)
 __host__ static inline uint64_t nwl_tb_words(const NwShape &s, uint32_t ymax) {
-    return nwl_band_words() + (uint64_t)s.xcap + ymax + 64;
+    return std::max<uint64_t>(nwl_band_words() + (uint64_t)s.xcap + ymax + 64, (uint64_t)s.xcap * NWL_K + 64);
 }
-__host__ __device__ static inline size_t nwl_wave_lds(int xstride) { return (size_t)xstride + 64 * 4 * 4; }
+// LDS per wave: the packed record, the last row of a strip (K ints per lane;
+// later the best-cell reduction)
+__host__ __device__ static inline size_t nwl_wave_lds(int xstride) { return (size_t)xstride + 64 * NWL_K * 4; }
 
 WV_DEVICE uint32_t nwl_code(const uint8_t *X4, int i) { return (X4[i >> 2] >> (2 * (i & 3))) & 3u; }
 
@@ -84,9 +87,12 @@ struct NwlBand {
     __device__ uint32_t nib(int i, int j) const {
         const int jj = j - bst * NWL_W, l = jj / NWL_K, s = jj - l * NWL_K, t = i + l;
         const uint32_t w = tb[((uint32_t)(t - bt0) * 64u + (uint32_t)l) * 2u + (uint32_t)(s >> 3)];
-        const uint32_t v = (w >> (4 * (s & 7))) & 0xFu;
-        // stored: bit0 not-diag, bit1 up > left, bit2 U, bit3 L -> nw_kernel.hip's nibble
-        return ((v & 1u) ? ((v & 2u) ? 1u : 2u) : 0u) | (v & 0xCu);
+        // cells shift in from the bottom, 4 bits each (not-diag, up > left, U,
+        // L): word 0 holds cells 0-7, word 1 cells 8..K-1, the first cell on top
+        const int top = (s < 8) ? 4 * min(NWL_K, 8) - 1 - 4 * s : 4 * (NWL_K - 8) - 1 - 4 * (s - 8);
+        const uint32_t v = (w >> (top - 3)) & 0xFu;     // bit 3 = not-diag ... bit 0 = L
+        // -> nw_kernel.hip's nibble: move (0 diag, 1 up, 2 left) | U << 2 | L << 3
+        return ((v & 8u) ? ((v & 4u) ? 1u : 2u) : 0u) | ((v & 2u) << 1) | ((v & 1u) << 3);
     }
     __device__ bool match(int i, int j) const { return nwl_code(X4, i) == base_code(Y[j]); }
 };
@@ -181,9 +187,11 @@ __device__ void nwl_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const 
     constexpr int K = NWL_K;
     const int ig = P.igap, eg = P.egap, IGE = ig + eg;
     uint8_t *X4 = wsm;
-    int *red = (int *)(wsm + P.xstride);                               // 64 lanes x 4 ints
+    int *lrow = (int *)(wsm + P.xstride);                              // 64 lanes x K ints
+    int *red = lrow;                                                   // 64 lanes x 4 ints, after pass 1
     uint32_t *tbw = P.tb + (uint64_t)slot * P.tb_wave_dw;              // band traceback, then path scratch
     uint32_t *pscr = tbw + nwl_band_words();
+    int *colbuf = (int *)tbw;                                          // pass 1: row i's last-lane cells at i * K
     int *seam = P.bnd + (uint64_t)slot * P.bnd_wave;
     uint32_t *ckw = P.ck + (uint64_t)slot * P.ck_wave_dw + lane;
     const int ncks = nwl_ncks(P.steps);
@@ -213,25 +221,47 @@ __device__ void nwl_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const 
         int bestR = INT_MIN, bestRj = 0, bestC = INT_MIN, bestCi = 0;
 
         // ---- state of one strip's sweep, shared by both passes
+        const int SP = xlen + 1;                  // seam plane stride: rows 0..xlen
         uint32_t yreg[K];
-        int A[K], B[K], dI[K], mcS[K], u0[K];
-        int I1 = 0, I2 = 0, outT = 0, outMS = 0, outL = 0, xrow = 0;
-        int sn0 = 0, sn1 = 0, sn2 = 0, sp0 = 0, sp1 = 0, sp2 = 0;   // seam rows i+1, i+2 (lead lane)
+        int A[K], B[K], mcS[K], u0[K];
+        int I1 = 0, I2 = 0, outT = 0, outMS = 0, outL = 0;
+        // score tables (v_perm sources: byte y = s(x, y), byte 4 + y its sign)
+        // of this lane's row (tL, tH) and of the block's rows, lane l = row
+        // t_b + l (xL, xH): every step the lead lane pops the next row's table
+        // and the other lanes take their left neighbour's
+        uint32_t tL = 0, tH = 0, xL = 0, xH = 0;
+        // the previous strip's right edge: R = this block's rows (lane l = row
+        // t_b + l, popped by the lead lane), N = the next block's (in flight);
+        // W collects the last lane's edge, flushed every block
+        int R0 = 0, R1 = 0, R2 = 0, N0 = 0, N1 = 0, N2 = 0, W0 = 0, W1 = 0, W2 = 0;
         int st = 0;
         bool leadc0 = false, seam_in = false, seam_out = false;
-        int *seam_rd = seam, *seam_wr = seam;
+        const int *seam_rd = seam;
+        int *seam_wr = seam;
         uint32_t *tbb = tbw;
         int bt0 = 0;
-        auto seam_row = [&](const int i) -> const int * { return seam_rd + 3 * min(max(i, 1), xl1); };
-        // strip setup: y codes, row 0 (:404-413), the flags of this lane
+        auto row_table = [&](const int r, uint32_t &L, uint32_t &H) {
+            const uint32_t xs = nwl_code(X4, min(max(r, 0), xl1)) * 0x01010101u;
+            L = wv_perm(NW16_TBL_HI, NW16_TBL_LO, xs ^ 0x03020100u);
+            H = wv_perm(NW16_TBL_HI, NW16_TBL_LO, xs ^ 0x07060504u);
+        };
+        auto seam_load = [&](const int r0) {      // edge rows r0 + lane (clamped into [1, xlen))
+            const int r = min(max(r0 + lane, 1), xl1);
+            N0 = seam_rd[r]; N1 = seam_rd[SP + r]; N2 = seam_rd[2 * SP + r];
+        };
+        auto seam_flush = [&](const int t, const int ts) {   // W = steps [t - 64, t): lane l row t - 127 + l
+            const int r = t - 127 + lane;
+            if (r >= 1 && r < xlen && r >= ts - 63) { seam_wr[r] = W0; seam_wr[SP + r] = W1; seam_wr[2 * SP + r] = W2; }
+        };
+        // strip setup: y codes, row 0 (:404-413), the flags of this strip
         auto strip_init = [&](const int s_) {
             st = s_;
             const int j0 = st * NWL_W + lane * K;
             leadc0 = st == 0 && lane == 0;
-            seam_in = st > 0 && lane == 0;
-            seam_out = st + 1 < nstr && lane == 63;
-            seam_rd = seam + (uint64_t)(st > 0 ? st - 1 : 0) * (xlen + 1) * 3;
-            seam_wr = seam + (uint64_t)st * (xlen + 1) * 3;
+            seam_in = st > 0;
+            seam_out = st + 1 < nstr;
+            seam_rd = seam + (uint64_t)(st > 0 ? st - 1 : 0) * 3 * SP;
+            seam_wr = seam + (uint64_t)st * 3 * SP;
             const uint32_t x0 = nwl_code(X4, 0), xs0 = x0 * 0x01010101u;
 #pragma unroll
             for (int s = 0; s < K; ++s) {
@@ -246,9 +276,8 @@ __device__ void nwl_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const 
 #pragma unroll
             for (int s = 0; s < K; ++s) {
                 // mc[j-1] = (T[0][j-1], row 0); row 0 stands in for rows -1 and -2
-                dI[s] = ((s == 0) ? t0prev : A[s - 1]) + IGE;
-                mcS[s] = dI[s];
-                u0[s] = dI[s];
+                mcS[s] = ((s == 0) ? t0prev : A[s - 1]) + IGE;
+                u0[s] = mcS[s];
                 if (j0 + s == 1) mcS[s] = NWL_BIG;          // mc[0] is never updated (:476)
             }
             I1 = t0prev; I2 = t0prev;
@@ -260,54 +289,57 @@ __device__ void nwl_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const 
         // the last row / last column (pass 1)
         auto step = [&](const bool HEAD, const bool TAIL, const bool TB, const bool BEST, const int t, int (&cur)[K],
                         const int (&own)[K], int &in0, const int in1) {
-            int sN = wv_shr1(outT), mS = wv_shr1(outMS), mL0 = wv_shr1(outL);
+            // row state from the left neighbour; the lead lane's from the
+            // previous strip's edge (strip 0: unused, column 0 below)
+            // (each queue shifts before its head is consumed as the DPP's old
+            // value, so the consumer takes over the head's register: no copies)
+            const int R0n = wv_shl1(R0), R1n = wv_shl1(R1), R2n = wv_shl1(R2);
+            const int sN = wv_shr1_fill(outT, R0), mS = wv_shr1_fill(outMS, R1), mL0 = wv_shr1_fill(outL, R2);
+            R0 = R0n; R1 = R1n; R2 = R2n;
+            const uint32_t xLn = (uint32_t)wv_shl1((int)xL), xHn = (uint32_t)wv_shl1((int)xH);
+            tL = (uint32_t)wv_shr1_fill((int)tL, (int)xL); tH = (uint32_t)wv_shr1_fill((int)tH, (int)xH);
+            xL = xLn; xH = xHn;
             const int i = t - lane;
-            if (seam_in) {                            // the previous strip's right edge, row i
-                sN = sp0; mS = sp1; mL0 = sp2;
-                sp0 = sn0; sp1 = sn1; sp2 = sn2;
-                const int *q = seam_row(i + 2);
-                sn0 = q[0]; sn1 = q[1]; sn2 = q[2];
-            }
-            const uint32_t xsel = (uint32_t)xrow * 0x01010101u;
-            xrow = (int)nwl_code(X4, (HEAD || TAIL) ? min(max(i + 1, 0), xl1) : i + 1);
             const bool pre = HEAD && i < 1;
             const bool row1 = HEAD && i <= 1;         // up invalid, mc frozen (:449, :476)
             int mfS = mS, l0 = mL0;
+            int dIn = in0 + IGE;                      // T[i-2][j-1] + ig + eg: cur before this step overwrites it
             uint32_t w0 = 0, w1 = 0;
 #pragma unroll
             for (int s = 0; s < K; ++s) {
                 const int d0 = (s == 0) ? in1 : own[s - 1];      // T[i-1][j-1]
                 const int tl = (s == 0) ? sN : cur[s - 1];       // T[i][j-1]
-                const int sc = (int)wv_perm(NW16_TBL_HI, NW16_TBL_LO, xsel ^ yreg[s]);
+                const int dI = dIn;
+                dIn = cur[s] + IGE;
+                const int sc = (int)wv_perm(tH, tL, yreg[s]);
                 const int up = row1 ? -NWL_BIG : u0[s];
                 int v;
-                uint32_t nb = 0;
+                uint32_t &tw = (s < 8) ? w0 : w1;
                 if (TB) {
                     // diag if >= both, else up if up > left, else left (:457-472)
                     const int lu = max(l0, up);
                     v = max(d0, lu) + sc;
-                    nb = (d0 < lu ? 1u : 0u) | (up > l0 ? 2u : 0u);
+                    tw = wv_shift_in(tw, d0 < lu);
+                    tw = wv_shift_in(tw, up > l0);
                 } else {
                     v = wv_max3(d0, l0, up) + sc;
                 }
                 if (s == 0 && leadc0) v = sc;                    // column 0 (:426)
                 cur[s] = pre ? own[s] : v;
                 // column max of column j-1 over rows <= i-2, strict > (:476-480), in
-                // the +ig+eg frame: dI[s] = T[i-2][j-1] + ig + eg
-                const bool mU = mcS[s] < dI[s];
-                const int u0n = (mU ? dI[s] : u0[s]) + eg;
+                // the +ig+eg frame: dI = T[i-2][j-1] + ig + eg
+                const bool mU = mcS[s] < dI;
+                const int u0n = (mU ? dI : u0[s]) + eg;
                 u0[s] = row1 ? u0[s] : u0n;
-                mcS[s] = mU ? dI[s] : mcS[s];
+                mcS[s] = mU ? dI : mcS[s];
                 // row state for column j+1: tested on row i, taken from row i-1 (:434-438)
                 const bool kept = tl < mfS;
-                dI[s] = d0 + IGE;
-                l0 = kept ? l0 + eg : dI[s];
+                l0 = kept ? l0 + eg : d0 + IGE;
                 mfS = kept ? mfS : d0;
                 if (s == 0 && leadc0) { mfS = -NWL_BIG; l0 = -NWL_BIG; }   // j = 1: no left move
                 if (TB) {
-                    nb |= (mU ? 4u : 0u) | (kept ? 0u : 8u);
-                    if (s < 8) w0 |= nb << (4 * s);
-                    else       w1 |= nb << (4 * (s - 8));
+                    tw = wv_shift_in(tw, mU);
+                    tw = wv_shift_in(tw, !kept);
                 }
             }
             if (TB) {                                 // rows outside [1, xlen) are never read
@@ -315,22 +347,18 @@ __device__ void nwl_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const 
                 rec[0] = w0; rec[1] = w1;
             }
             if (BEST) {
-                if (TAIL && i == xlen - 1) {          // last row (:481-484), columns in visiting order
-                    const int j0 = st * NWL_W + lane * K;
+                if (TAIL && i == xlen - 1) {          // last row: kept for the strip's end (last_row)
 #pragma unroll
-                    for (int s = 0; s < K; ++s)
-                        if (j0 + s >= 1 && j0 + s < ylen && cur[s] >= bestR) { bestR = cur[s]; bestRj = j0 + s; }
+                    for (int s = 0; s < K; ++s) lrow[lane * K + s] = cur[s];
                 }
-                if (st == lastst && lane == lastl && i >= 1 && i < xlen - 1) {     // last column
-                    int vl = cur[0];
+                if (st == lastst && lane == lastl && i >= 1 && i < xlen - 1) {     // last column: kept (colbuf)
+                    int *q = colbuf + (uint32_t)i * K;
 #pragma unroll
-                    for (int s = 1; s < K; ++s) vl = (lasts == s) ? cur[s] : vl;
-                    if (vl >= bestC) { bestC = vl; bestCi = i; }
+                    for (int s = 0; s < K; ++s) q[s] = cur[s];
                 }
             }
-            if (seam_out && i >= 1 && i < xlen) {
-                int *q = seam_wr + 3 * i;
-                q[0] = cur[K - 1]; q[1] = mfS; q[2] = l0;
+            if (seam_out) {                           // the last lane's edge, row i, into W
+                W0 = wv_shl1_fill(W0, cur[K - 1]); W1 = wv_shl1_fill(W1, mfS); W2 = wv_shl1_fill(W2, l0);
             }
             in0 = pre ? in1 : sN;
             outT = cur[K - 1]; outMS = mfS; outL = l0;
@@ -340,64 +368,81 @@ __device__ void nwl_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const 
             uint32_t *p = ckw + (uint32_t)((st * ncks + m) * NWL_NST) * 64u;
 #pragma unroll
             for (int s = 0; s < K; ++s) {
-                p[s * 64] = (uint32_t)A[s]; p[(K + s) * 64] = (uint32_t)B[s]; p[(2 * K + s) * 64] = (uint32_t)dI[s];
-                p[(3 * K + s) * 64] = (uint32_t)mcS[s]; p[(4 * K + s) * 64] = (uint32_t)u0[s];
+                p[s * 64] = (uint32_t)A[s]; p[(K + s) * 64] = (uint32_t)B[s];
+                p[(2 * K + s) * 64] = (uint32_t)mcS[s]; p[(3 * K + s) * 64] = (uint32_t)u0[s];
             }
-            p[5 * K * 64] = (uint32_t)I1; p[(5 * K + 1) * 64] = (uint32_t)I2;
-            p[(5 * K + 2) * 64] = (uint32_t)outT; p[(5 * K + 3) * 64] = (uint32_t)outMS;
-            p[(5 * K + 4) * 64] = (uint32_t)outL;
+            p[4 * K * 64] = (uint32_t)I1; p[(4 * K + 1) * 64] = (uint32_t)I2;
+            p[(4 * K + 2) * 64] = (uint32_t)outT; p[(4 * K + 3) * 64] = (uint32_t)outMS;
+            p[(4 * K + 4) * 64] = (uint32_t)outL;
         };
         auto restore = [&](const int m) {
             const uint32_t *p = ckw + (uint32_t)((st * ncks + m) * NWL_NST) * 64u;
 #pragma unroll
             for (int s = 0; s < K; ++s) {
-                A[s] = (int)p[s * 64]; B[s] = (int)p[(K + s) * 64]; dI[s] = (int)p[(2 * K + s) * 64];
-                mcS[s] = (int)p[(3 * K + s) * 64]; u0[s] = (int)p[(4 * K + s) * 64];
+                A[s] = (int)p[s * 64]; B[s] = (int)p[(K + s) * 64];
+                mcS[s] = (int)p[(2 * K + s) * 64]; u0[s] = (int)p[(3 * K + s) * 64];
             }
-            I1 = (int)p[5 * K * 64]; I2 = (int)p[(5 * K + 1) * 64];
-            outT = (int)p[(5 * K + 2) * 64]; outMS = (int)p[(5 * K + 3) * 64]; outL = (int)p[(5 * K + 4) * 64];
+            I1 = (int)p[4 * K * 64]; I2 = (int)p[(4 * K + 1) * 64];
+            outT = (int)p[(4 * K + 2) * 64]; outMS = (int)p[(4 * K + 3) * 64]; outL = (int)p[(4 * K + 4) * 64];
         };
-        // run steps [t, t1) from the state before step t (t odd): the head
-        // (rows <= 1 somewhere), the middle, the tail (rows past the record)
-        auto sweep = [&](int t, const int t1, const bool TB, const bool BEST, const bool CKS) {
-            xrow = (int)nwl_code(X4, min(max(t - lane, 0), xl1));
-            if (seam_in) {
-                const int *a = seam_row(t), *b = seam_row(t + 1);
-                sp0 = a[0]; sp1 = a[1]; sp2 = a[2]; sn0 = b[0]; sn1 = b[1]; sn2 = b[2];
-            }
+        // run steps [ts, t1) from the state before step ts (ts = 1 mod NWL_CK)
+        // in blocks of 64 steps; within a block the head (rows <= 1
+        // somewhere), the middle, the tail (rows past the record)
+        auto sweep = [&](const int ts, const int t1, const bool TB, const bool BEST, const bool CKS) {
+            row_table(ts - 1 - lane, tL, tH);         // as the left neighbour would hand it over
+            if (seam_in) seam_load(ts);
             const int head_end = 66, tail_beg = xlen - 2;          // fast steps: every lane in rows [2, xlen - 1)
-            auto ckpt = [&](const int tt) { if (CKS && (tt - 1) % NWL_CK == 0) save((tt - 1) / NWL_CK); };
-            for (; t + 1 < t1 && t + 1 < head_end; t += 2) {
-                ckpt(t);
-                step(true, true, TB, BEST, t, A, B, I2, I1);
-                step(true, true, TB, BEST, t + 1, B, A, I1, I2);
-            }
-            for (; t + 1 < t1 && t + 1 < tail_beg; t += 2) {
-                ckpt(t);
-                if (TB) {
-                    step(false, false, true, false, t, A, B, I2, I1);
-                    step(false, false, true, false, t + 1, B, A, I1, I2);
-                } else if (BEST && st == lastst) {
-                    step(false, false, false, true, t, A, B, I2, I1);
-                    step(false, false, false, true, t + 1, B, A, I1, I2);
-                } else {
-                    step(false, false, false, false, t, A, B, I2, I1);
-                    step(false, false, false, false, t + 1, B, A, I1, I2);
+            int t = ts;
+            while (t < t1) {
+                if (CKS && (t - 1) % NWL_CK == 0) save((t - 1) / NWL_CK);
+                row_table(t + lane, xL, xH);
+                if (seam_in) { R0 = N0; R1 = N1; R2 = N2; seam_load(t + 64); }
+                if (seam_out && t > ts) seam_flush(t, ts);
+                const int te = min(t + 64, t1);
+                for (; t + 1 < te && t + 1 < head_end; t += 2) {
+                    step(true, true, TB, BEST, t, A, B, I2, I1);
+                    step(true, true, TB, BEST, t + 1, B, A, I1, I2);
                 }
+                for (; t + 1 < te && t + 1 < tail_beg; t += 2) {
+                    if (TB) {
+                        step(false, false, true, false, t, A, B, I2, I1);
+                        step(false, false, true, false, t + 1, B, A, I1, I2);
+                    } else if (BEST && st == lastst) {
+                        step(false, false, false, true, t, A, B, I2, I1);
+                        step(false, false, false, true, t + 1, B, A, I1, I2);
+                    } else {
+                        step(false, false, false, false, t, A, B, I2, I1);
+                        step(false, false, false, false, t + 1, B, A, I1, I2);
+                    }
+                }
+                for (; t + 1 < te; t += 2) {
+                    step(true, true, TB, BEST, t, A, B, I2, I1);
+                    step(true, true, TB, BEST, t + 1, B, A, I1, I2);
+                }
+                if (t < te) { step(true, true, TB, BEST, t, A, B, I2, I1); ++t; }   // t1 odd: the sweep's end
             }
-            for (; t + 1 < t1; t += 2) {
-                ckpt(t);
-                step(true, true, TB, BEST, t, A, B, I2, I1);
-                step(true, true, TB, BEST, t + 1, B, A, I1, I2);
-            }
-            if (t < t1) step(true, true, TB, BEST, t, A, B, I2, I1);
+            if (seam_out) seam_flush(t, ts);
         };
 
         // ---------------------------------------------------- pass 1
         for (int s_ = 0; s_ < nstr; ++s_) {
             strip_init(s_);
             sweep(1, tend, false, true, true);
-            wv_mem_sync();                            // seam written by the last lane, read by the next lead
+            wv_mem_sync();                            // seams written by every lane, read by the next strip
+            // last row (:481-484): ">=" over the columns in visiting order
+            // keeps the largest j among equal scores
+            const int j0 = st * NWL_W + lane * K;
+#pragma unroll
+            for (int s = 0; s < K; ++s) {
+                const int v = lrow[lane * K + s];
+                if (j0 + s >= 1 && j0 + s < ylen && v >= bestR) { bestR = v; bestRj = j0 + s; }
+            }
+            wv_lds_sync();
+        }
+        // last column, rows [1, xlen - 1) (:481-484): ">=" in row order keeps the largest i
+        for (int r = 1 + lane; r < xlen - 1; r += 64) {
+            const int v = colbuf[(uint32_t)r * K + lasts];
+            if (v >= bestC) { bestC = v; bestCi = r; }
         }
         // best cell (:481-484): last-row cells are visited after every other
         // row's, so they win ties; within each, ">=" kept the last visited
@@ -415,17 +460,24 @@ __device__ void nwl_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const 
         else          { bscore = bC; bx = bCi; by = ylen - 1; }
 
         // ---------------------------------------------------- pass 2: the walk
-        NwlWalk w = {bx, by, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, false, false, false};
+        // the walk's state waits in LDS (every lane holds the same copy) while
+        // a band is recomputed, so the sweep keeps its registers
+        NwlWalk *ws = (NwlWalk *)red;
+        *ws = NwlWalk{bx, by, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, false, false, false};
         int guard = 4 * (xlen + ylen) + 64, nband = 0;
         NwlBand bd = {tbw, X4, Y, -1, 0, 0};
         for (;;) {
+            wv_lds_sync();
+            NwlWalk w = *ws;
             nwl_walk_band(bd, w, lane, pscr, guard);
-            if (!w.need) break;
+            if (!w.need) { *ws = w; break; }
             // recompute the band of strip need_j / NWL_W ending at the needed
             // cell's step, from the checkpoint below its first step
             const int s_ = w.need_j / NWL_W, lc = (w.need_j - s_ * NWL_W) / K, tc = w.need_i + lc;
             const int t1 = min(tc + 1, tend), m = max(t1 - band - 1, 0) / NWL_CK, t0 = 1 + m * NWL_CK;
-            if (++nband > 4 * (nstr + (xlen + ylen) / 64 + 8)) { w.bad = true; break; }
+            if (++nband > 4 * (nstr + (xlen + ylen) / 64 + 8)) { w.bad = true; *ws = w; break; }
+            *ws = w;
+            wv_lds_sync();
             strip_init(s_);
             seam_out = false;
             restore(m);
@@ -434,6 +486,8 @@ __device__ void nwl_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const 
             wv_mem_sync();                            // band written by all lanes, read by the walkers
             bd.bst = s_; bd.bt0 = t0; bd.bt1 = t1;
         }
+        wv_lds_sync();
+        const NwlWalk w = *ws;
         if (w.run && !w.bad && lane == 0) pscr[w.nent - 1] = (IMSAME_MOVE_DIAG << 30) | (uint32_t)w.run;
         wv_mem_sync();
         // ---------------------------------------------------- result (nw_finish)
@@ -477,7 +531,7 @@ __device__ void nwl_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const 
 
 #ifndef IMSAME_WAVE_EMU
 #ifndef NWL_WAVES_PER_EU
-#define NWL_WAVES_PER_EU 4
+#define NWL_WAVES_PER_EU 3                 // 168 VGPRs: the sweeps' state without spills
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NWL_WAVES_PER_EU)))
 void nwl_kernel(NwLaunch P) {

@@ -14,6 +14,12 @@
 // lane l receives lane l-1's value (lane 0 receives 0): DPP wave_shr:1 with
 // bound_ctrl zero fill (no v_mov to seed the destination's old value)
 WV_DEVICE int wv_shr1(int v) { return __builtin_amdgcn_mov_dpp(v, 0x138, 0xf, 0xf, true); }
+// lane l receives lane l+1's value (lane 63 receives 0): wave_shl:1, zero fill
+WV_DEVICE int wv_shl1(int v) { return __builtin_amdgcn_mov_dpp(v, 0x130, 0xf, 0xf, true); }
+// lane l receives lane l-1's v, lane 0 its own `fill` (wave_shr:1, bound_ctrl off: old = fill)
+WV_DEVICE int wv_shr1_fill(int v, int fill) { return __builtin_amdgcn_update_dpp(fill, v, 0x138, 0xf, 0xf, false); }
+// lane l receives lane l+1's v, lane 63 its own `fill` (wave_shl:1)
+WV_DEVICE int wv_shl1_fill(int v, int fill) { return __builtin_amdgcn_update_dpp(fill, v, 0x130, 0xf, 0xf, false); }
 // max of three signed ints in one VALU op (v_max3_i32)
 WV_DEVICE int wv_max3(int a, int b, int c) {
     int r;
@@ -76,6 +82,14 @@ WV_DEVICE uint32_t wv_bfi(uint32_t m, uint32_t a, uint32_t b) {
 }
 // byte permute of the 8 bytes {hi:lo}: selector byte k picks byte sel_k (0-3 of lo, 4-7 of hi)
 WV_DEVICE uint32_t wv_perm(uint32_t hi, uint32_t lo, uint32_t sel) { return __builtin_amdgcn_perm(hi, lo, sel); }
+// (w << 1) | c in one v_addc_co_u32 (w + w + carry): the compare's lane mask
+// is the carry-in
+WV_DEVICE uint32_t wv_shift_in(uint32_t w, bool c) {
+    uint32_t r;
+    unsigned long long co;
+    asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(r), "=s"(co) : "v"(w), "s"(__builtin_amdgcn_ballot_w64(c)));
+    return r;
+}
 
 #else  // ---------------------------------------------------------- CPU emu
 #include <stdint.h>
@@ -111,6 +125,27 @@ inline int wv_shr1(int v) {
     wvemu::t_xch[wvemu::t_lane] = (uint64_t)(uint32_t)v;
     wvemu::sync();
     int r = wvemu::t_lane ? (int)(uint32_t)wvemu::t_xch[wvemu::t_lane - 1] : 0;
+    wvemu::sync();
+    return r;
+}
+inline int wv_shl1(int v) {
+    wvemu::t_xch[wvemu::t_lane] = (uint64_t)(uint32_t)v;
+    wvemu::sync();
+    int r = wvemu::t_lane < 63 ? (int)(uint32_t)wvemu::t_xch[wvemu::t_lane + 1] : 0;
+    wvemu::sync();
+    return r;
+}
+inline int wv_shr1_fill(int v, int fill) {
+    wvemu::t_xch[wvemu::t_lane] = (uint64_t)(uint32_t)v;
+    wvemu::sync();
+    int r = wvemu::t_lane ? (int)(uint32_t)wvemu::t_xch[wvemu::t_lane - 1] : fill;
+    wvemu::sync();
+    return r;
+}
+inline int wv_shl1_fill(int v, int fill) {
+    wvemu::t_xch[wvemu::t_lane] = (uint64_t)(uint32_t)v;
+    wvemu::sync();
+    int r = wvemu::t_lane < 63 ? (int)(uint32_t)wvemu::t_xch[wvemu::t_lane + 1] : fill;
     wvemu::sync();
     return r;
 }
@@ -153,6 +188,7 @@ inline uint32_t pk_add(uint32_t a, uint32_t b) { return pk_map(a, b, [](int x, i
 inline uint32_t pk_sub(uint32_t a, uint32_t b) { return pk_map(a, b, [](int x, int y) { return x - y; }); }
 inline uint32_t pk_max(uint32_t a, uint32_t b) { return pk_map(a, b, [](int x, int y) { return x > y ? x : y; }); }
 inline uint32_t pk_neg_mask(uint32_t a) { return pk_map(a, 0, [](int x, int) { return x < 0 ? -1 : 0; }); }
+inline uint32_t wv_shift_in(uint32_t w, bool c) { return (w << 1) | (c ? 1u : 0u); }
 inline uint32_t wv_and_or(uint32_t m, uint32_t c, uint32_t w) { return (m & c) | w; }
 inline uint32_t wv_bfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
 inline uint32_t wv_perm(uint32_t hi, uint32_t lo, uint32_t sel) {
