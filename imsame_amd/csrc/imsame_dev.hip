@@ -826,7 +826,7 @@ static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, 
     pl->lng = !pl->pk && !(p->flags & IMSAME_FLAG_NW32) && nwl_enabled() && nwl_fits(p->igap, p->egap, ymax);
     if (pl->lng) {                  // steps of a pass-2 band (IMSAME_NWL_BAND: tests use small ones)
         const char *nb = getenv("IMSAME_NWL_BAND");
-        pl->band_w = nb ? std::max(1, std::min(NWL_BAND, atoi(nb))) : NWL_BAND;
+        pl->band_w = nb ? std::max(1, std::min(NWL_BAND, atoi(nb))) : NWL_BAND_DEF;
     }
     const NwShape sh = pl->pk ? nw16_shape(ymax, xcap) : pl->lng ? nwl_shape(ymax, xcap) : nw_shape(ymax, xcap);
     pl->G = sh.G; pl->GPW = sh.GPW; pl->nstr = sh.nstr; pl->xcap = sh.xcap; pl->xstride = sh.xstride;
@@ -1073,7 +1073,10 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     // (reads with a rejection emit <= n in all, S.spec below)
     const char *sw_env = getenv("IMSAME_SPEC_WEAK");
     const uint32_t spec_weak = (uint32_t)std::max(1, std::min(SPEC_MAX, sw_env ? atoi(sw_env) : SPEC_WEAK));
-    const uint64_t ccap = (uint64_t)n * (spec_weak > 1 ? spec_weak + 1 : 2);
+    // candidate lists: 2 per read (up to SPEC_MAX for small calls -- long
+    // reads, few per call, fill launches by speculating)
+    const uint64_t ccap = std::max<uint64_t>((uint64_t)n * (spec_weak > 1 ? spec_weak + 1 : 2),
+                                             std::min<uint64_t>((uint64_t)n * SPEC_MAX, 1u << 20));
     if (c->res.ensure((uint64_t)n * 64) || c->cur_p.ensure((uint64_t)n * 8) || c->cur_h.ensure((uint64_t)n * 4) ||
         c->memo.ensure((uint64_t)n * 4 * MEMO) || c->nmemo.ensure(n) || c->rstat.ensure(n) ||
         c->act0.ensure((uint64_t)n * 4) || c->act1.ensure((uint64_t)n * 4) || c->cread.ensure(ccap * 4) ||

@@ -38,7 +38,8 @@
 #define NWL_BIG  (1 << 28)                // stands for INT64_MIN / "never"
 #define NWL_CK   128                      // checkpoint interval (steps; even: the rotation period)
 #define NWL_NST  (4 * NWL_K + 5)          // dwords of wave state per lane in a checkpoint
-#define NWL_BAND 1024                     // steps a pass-2 band ends with (plus up to NWL_CK below)
+#define NWL_BAND 1024                     // most steps a pass-2 band ends with (plus up to NWL_CK below)
+#define NWL_BAND_DEF 768                  // the default: a diagonal path crosses a strip in ~W + 64 steps
 
 // the long kernel takes launches of reads longer than the packed kernel's
 // columns with non-positive gap parameters (the drifting terms only fall)

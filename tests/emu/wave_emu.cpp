@@ -88,7 +88,7 @@ static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, cons
     P.band_w = be ? std::max(0, atoi(be)) : 200;        // imsame_dev.hip:nw16_band_rows
     if (lng) {                                            // imsame_dev.hip:plan_nw
         const char *nb = getenv("IMSAME_NWL_BAND");
-        P.band_w = nb ? std::max(1, std::min(NWL_BAND, atoi(nb))) : NWL_BAND;
+        P.band_w = nb ? std::max(1, std::min(NWL_BAND, atoi(nb))) : NWL_BAND_DEF;
     }
     P.redo = &g_redo;
     // queue order by predicted row, as imsame_dev.hip:launch_nw (row_bucket:
@@ -224,7 +224,8 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
     // imsame_dev.hip:align_one -- speculation from a weak first candidate, candidate capacity
     const char *sw_env = getenv("IMSAME_SPEC_WEAK");
     const uint32_t spec_weak = (uint32_t)std::max(1, std::min(SPEC_MAX, sw_env ? atoi(sw_env) : SPEC_WEAK));
-    const size_t ccap = (size_t)n * (spec_weak > 1 ? spec_weak + 1 : 2);
+    const size_t ccap = std::max<size_t>((size_t)n * (spec_weak > 1 ? spec_weak + 1 : 2),
+                                         std::min<size_t>((size_t)n * SPEC_MAX, 1u << 20));
     std::vector<uint32_t> cur_h(n), memo((size_t)n * MEMO), act(n), nxt(n), cr(ccap), cs(ccap), cr2(ccap), cs2(ccap);
     std::vector<uint32_t> cbase(n), ccnt(n), perr(n);
     std::vector<int32_t> crow(ccap);
