@@ -310,6 +310,12 @@ struct imsame_ctx {
     // NW scratch; the path arena of the last align (device, or host for the
     // sliced form) until imsame_dev_fetch_paths
     DBuf tb, bnd, paths, ck;
+    // non-persistent nw16 launches: free-slot bitmap of the arena, 8 XCD
+    // partitions (nw16_kernel.hip:nw_slot_claim); xcc_ok: 1 when the XCC_ID
+    // register was seen to name 8 XCDs (nw_xcc_check), 0 no, -1 not probed
+    DBuf slotbits;
+    uint32_t slot_words = 0;
+    int xcc_ok = -1;
     uint64_t paths_cap_dev = 0, paths_n = 0;
     double paths_hint = 0;     // path entries per read of the last call
     std::vector<uint32_t> paths_host;
@@ -330,6 +336,10 @@ struct imsame_ctx {
     // NW launch intervals (ms since the call's origin event) for the busy time
     hipEvent_t origin = nullptr;
     std::vector<std::pair<float, float>> nw_iv;
+    // IMSAME_DEBUG_TIMELINE: (kind 'S' seed / 'N' NW, round, items, start, end)
+    struct TlEv { char kind; int round; uint32_t n; float a, b; };
+    std::vector<TlEv> tl;
+    int cur_round = 0;
     int nlanes = 1;                   // lanes of the running call (the seed scan's group size
                                       // follows the reads scanned across all of them)
     std::vector<uint32_t> part_paths; // host copy of this lane's paths for an imsame_dev_align_parts callback
@@ -784,7 +794,24 @@ static int build_tables(imsame_ctx *c, const imsame_params *p, uint32_t ymax, ui
     return 0;
 }
 
-struct NwPlan { int G, GPW, xcap, xstride, steps, nstr; bool pk, last4, two, lng; size_t lds; unsigned blocks, max_blocks;
+// IMSAME_DEBUG_TIMELINE=1: every lane's seed scans and NW launches on the
+// call's common clock, printed to stderr when the call ends (diagnostics)
+static bool timeline_on() {
+    static std::once_flag f;
+    static bool on = false;
+    std::call_once(f, [] { const char *e = getenv("IMSAME_DEBUG_TIMELINE"); on = e && atoi(e); });
+    return on;
+}
+static void timeline_print(const std::vector<imsame_ctx *> &L) {
+    for (size_t k = 0; k < L.size(); ++k) {
+        for (const auto &e : L[k]->tl)
+            fprintf(stderr, "[timeline] lane %zu %c round %d n %u %.3f %.3f\n", k, e.kind, e.round, e.n, e.a, e.b);
+        L[k]->tl.clear();
+    }
+}
+
+struct NwPlan { int G, GPW, xcap, xstride, steps, nstr, k; bool pk, last4, two, lng, np; size_t lds; unsigned blocks, max_blocks;
+                uint32_t slot_words;   // np: bitmap words per XCD partition (arena slots = 8 x 32 x slot_words)
                 uint64_t tb_dw, ck_dw, bnd_dw; int band_w; };
 
 // Long reads take the two-pass nwl_kernel (nwl_kernel.hip) unless the int32
@@ -803,6 +830,49 @@ static bool nwl_enabled() {
 static int nw16_band_rows() {
     const char *e = getenv("IMSAME_NW_BAND");
     return e ? std::max(0, atoi(e)) : 200;
+}
+
+// Non-persistent packed launches need the XCD of each wave (nw_slot_claim):
+// a probe kernel reads XCC_ID in 512 blocks, which must name each of 8 XCDs.
+// Off when the check fails (persistent launches then), or IMSAME_NW_PERSIST=1.
+static bool nw_xcc_check(imsame_ctx *c) {
+    const char *pe = getenv("IMSAME_NW_PERSIST");
+    if (pe && atoi(pe)) return false;
+    if (c->xcc_ok >= 0) return c->xcc_ok == 1;
+    c->xcc_ok = 0;
+    if (c->ncu % 8 || c->ncu < 64) return false;
+    const unsigned nb = 512;
+    DBuf d;
+    if (d.ensure(nb * 4)) return false;
+    std::vector<uint32_t> h(nb, 0xFFFFFFFFu);
+    xcc_probe_kernel<<<nb, 64, 0, c->stream>>>(d.as<uint32_t>());
+    bool ok = hipGetLastError() == hipSuccess &&
+              hipMemcpyAsync(h.data(), d.p, nb * 4, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+              hipStreamSynchronize(c->stream) == hipSuccess;
+    uint32_t seen = 0;
+    for (uint32_t v : h) { if (v >= 8) ok = false; else seen |= 1u << v; }
+    d.release();
+    c->xcc_ok = ok && seen == 0xFFu ? 1 : 0;
+    return c->xcc_ok == 1;
+}
+
+// Columns per lane of a packed launch.  A launch is a queue of tasks (8
+// candidates x all rows at K = 10) pulled by one wave per resident slot
+// (4 per SIMD); a launch of a few slots' worth (a lane's later rounds, every
+// round of an 8-GPU shard) spends most of its time in its last tasks with
+// the chip mostly idle.  K = 5 halves a task (4 candidates, each wave half
+// the columns per step) and doubles their number, for ~8 % more
+// instructions per cell.  Chosen when the launch holds fewer than
+// k5_fill x (the chip's K = 10 slots / the lanes running) tasks.
+// IMSAME_NW_K=5|10 forces one; IMSAME_NW_K5_FILL sets k5_fill.
+static int nw16_k(imsame_ctx *c, uint32_t ncand, bool rounds) {
+    const char *e = getenv("IMSAME_NW_K"), *fe = getenv("IMSAME_NW_K5_FILL");
+    const int force = e ? atoi(e) : 0;
+    const double fill = fe ? atof(fe) : 2.0;
+    if (force == NW16_K5 || force == NW16_K) return force;
+    if (!rounds) return NW16_K;
+    const double slots = (double)c->ncu * 4.0 * 4.0 / std::max(1, c->nlanes);
+    return (double)ncand / 8.0 < fill * slots ? NW16_K5 : NW16_K;
 }
 
 // pk: the packed-pair int16 kernel (nw16_kernel.hip) when the launch fits it
@@ -828,7 +898,8 @@ static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, 
         const char *nb = getenv("IMSAME_NWL_BAND");
         pl->band_w = nb ? std::max(1, std::min(NWL_BAND, atoi(nb))) : NWL_BAND_DEF;
     }
-    const NwShape sh = pl->pk ? nw16_shape(ymax, xcap) : pl->lng ? nwl_shape(ymax, xcap) : nw_shape(ymax, xcap);
+    pl->k = pl->pk ? nw16_k(c, ncand, rounds) : 0;
+    const NwShape sh = pl->pk ? nw16_shape(ymax, xcap, pl->k) : pl->lng ? nwl_shape(ymax, xcap) : nw_shape(ymax, xcap);
     pl->G = sh.G; pl->GPW = sh.GPW; pl->nstr = sh.nstr; pl->xcap = sh.xcap; pl->xstride = sh.xstride;
     pl->steps = sh.steps;
     pl->tb_dw = pl->pk ? nw16_tb_words(sh) : pl->lng ? nwl_tb_words(sh, ymax) : nw_tb_words(sh);
@@ -837,17 +908,29 @@ static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, 
     pl->lds = (size_t)wpb * (pl->pk ? nw16_wave_lds(pl->GPW, pl->xstride)
                              : pl->lng ? nwl_wave_lds(pl->xstride) : nw_wave_lds(pl->GPW, pl->xstride));
     int per_cu = 0;
+    const bool k5 = pl->k == NW16_K5;
     hipError_t oe = pl->lng ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nwl_kernel, wpb * 64, pl->lds)
-                  : pl->two ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw16_kernel<false, true>, wpb * 64, pl->lds)
-                  : pl->pk ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw16_kernel<false, false>, wpb * 64, pl->lds)
+                  : pl->two ? (k5 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw16_kernel<NW16_K5, false, true>, wpb * 64, pl->lds)
+                                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw16_kernel<NW16_K, false, true>, wpb * 64, pl->lds))
+                  : pl->pk ? (k5 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw16_kernel<NW16_K5, false, false>, wpb * 64, pl->lds)
+                                 : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw16_kernel<NW16_K, false, false>, wpb * 64, pl->lds))
                   : (pl->nstr > 1)
                       ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw_kernel<true>, wpb * 64, pl->lds)
                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw_kernel<false>, wpb * 64, pl->lds);
     if (oe != hipSuccess || per_cu < 1) per_cu = 1;
-    per_cu = std::min(per_cu, 8);
+    // Non-persistent packed launches (one wave per task, arena slots from a
+    // per-XCD free bitmap): waves leave as their tasks end, so other lanes'
+    // seed scans and small kernels get wave slots during a long launch
+    // instead of after its last task (a persistent wave holds its slot until
+    // the queue is empty).  The partitions must hold the kernel's full
+    // residency, so per_cu is the true occupancy here.
+    pl->np = pl->pk && rounds && nw_xcc_check(c);
+    if (!pl->np) per_cu = std::min(per_cu, 8);
     const uint32_t cpw = pl->pk ? 2 * pl->GPW : pl->GPW;            // candidates per wave pull
     const uint64_t waves_needed = (ncand + cpw - 1) / cpw;
-    pl->blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)c->ncu * per_cu, (waves_needed + wpb - 1) / wpb));
+    pl->slot_words = (uint32_t)((((uint64_t)c->ncu / 8) * per_cu * wpb + 31) / 32);
+    pl->blocks = (unsigned)std::max<uint64_t>(1, pl->np ? (waves_needed + wpb - 1) / wpb
+                                                         : std::min<uint64_t>((uint64_t)c->ncu * per_cu, (waves_needed + wpb - 1) / wpb));
     // Traceback arena: one slot per resident wave.  Long reads against long
     // records (C5w, 10 kbp x 12 kbp = 99 MB per slot) would ask for more than
     // the card holds at full residency; the kernel pulls candidates from a
@@ -862,6 +945,15 @@ static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, 
     const uint64_t budget = avail > 2 * headroom ? avail - headroom : avail / 2;
     const uint64_t fit = budget / per_block;
     if (fit < 1) return IMSAME_E_OOM;
+    if (pl->np && (uint64_t)8 * 32 * pl->slot_words > fit * wpb) {   // arena short of the residency
+        pl->np = false;
+        pl->blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)c->ncu * std::min(per_cu, 8),
+                                                                        (waves_needed + wpb - 1) / wpb));
+    }
+    if (pl->np) {                           // the arena holds 8 x 32 x slot_words slots
+        pl->max_blocks = (unsigned)(((uint64_t)8 * 32 * pl->slot_words + wpb - 1) / wpb);
+        return 0;
+    }
     if (pl->blocks > fit) pl->blocks = (unsigned)fit;
     // the arena is sized for a full-residency launch of this shape, so the
     // launches of later rounds (fewer or more candidates) reuse it instead of
@@ -871,7 +963,7 @@ static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, 
     return 0;
 }
 
-static int launch_nw(imsame_ctx *c, NwPlan pl, const uint32_t *cread, const uint32_t *csid, uint32_t n,
+static int launch_nw(imsame_ctx *c, NwPlan &pl, const uint32_t *cread, const uint32_t *csid, uint32_t n,
                      imsame_read_result *outp, int64_t ig, int64_t eg, const imsame_params *p, uint32_t ymax,
                      uint32_t xmax, uint32_t *work, const uint8_t *dbp, const uint64_t *dbs, const uint8_t *qp,
                      const uint64_t *qs, uint32_t paths_cap, double *ms, const int32_t *crow = nullptr) {
@@ -879,14 +971,26 @@ static int launch_nw(imsame_ctx *c, NwPlan pl, const uint32_t *cread, const uint
     const uint64_t tb_dw = pl.tb_dw;
     // fewer resident waves if the arena cannot be had (the queue still drains)
     const uint64_t per_slot = tb_dw * 4, bnd_slot = pl.bnd_dw * 4, ck_slot = pl.ck_dw * 4;
-    if (c->tb.cap < (uint64_t)pl.blocks * 4 * per_slot)       // grow once to this shape's full residency
-        (void)c->tb.ensure((uint64_t)pl.max_blocks * 4 * per_slot);
-    if (ck_slot && c->ck.cap < (uint64_t)pl.blocks * 4 * ck_slot)
-        (void)c->ck.ensure((uint64_t)pl.max_blocks * 4 * ck_slot);
-    while (c->tb.ensure((uint64_t)pl.blocks * 4 * per_slot) || c->bnd.ensure((uint64_t)pl.blocks * 4 * bnd_slot + 64) ||
-           (ck_slot && c->ck.ensure((uint64_t)pl.blocks * 4 * ck_slot))) {
-        if (pl.blocks == 1) return IMSAME_E_OOM;
-        pl.blocks = (pl.blocks + 1) / 2;
+    if (pl.np) {                                 // every slot of the 8 partitions, and their bitmap
+        const uint64_t ns = (uint64_t)pl.max_blocks * 4, nbits = (uint64_t)8 * pl.slot_words * 4;
+        if (c->tb.ensure(ns * per_slot) || c->bnd.ensure(ns * bnd_slot + 64) || (ck_slot && c->ck.ensure(ns * ck_slot))) {
+            pl.np = false;                       // persistent, with what can be had
+            pl.blocks = std::min(pl.blocks, pl.max_blocks);
+        } else if (c->slotbits.cap < nbits) {    // all free: waves clear their bits as they leave
+            if (c->slotbits.ensure(nbits)) return IMSAME_E_OOM;
+            HIPCHK(hipMemsetAsync(c->slotbits.p, 0, c->slotbits.cap, s));
+        }
+    }
+    if (!pl.np) {
+        if (c->tb.cap < (uint64_t)pl.blocks * 4 * per_slot)       // grow once to this shape's full residency
+            (void)c->tb.ensure((uint64_t)pl.max_blocks * 4 * per_slot);
+        if (ck_slot && c->ck.cap < (uint64_t)pl.blocks * 4 * ck_slot)
+            (void)c->ck.ensure((uint64_t)pl.max_blocks * 4 * ck_slot);
+        while (c->tb.ensure((uint64_t)pl.blocks * 4 * per_slot) || c->bnd.ensure((uint64_t)pl.blocks * 4 * bnd_slot + 64) ||
+               (ck_slot && c->ck.ensure((uint64_t)pl.blocks * 4 * ck_slot))) {
+            if (pl.blocks == 1) return IMSAME_E_OOM;
+            pl.blocks = (pl.blocks + 1) / 2;
+        }
     }
     if (poison_on()) {                           // slots hold nothing from earlier launches
         const DBuf *scr[] = {&c->tb, &c->ck, &c->bnd};
@@ -912,6 +1016,7 @@ static int launch_nw(imsame_ctx *c, NwPlan pl, const uint32_t *cread, const uint
     P.ck = (pl.two || pl.lng) ? c->ck.as<uint32_t>() : nullptr; P.ck_wave_dw = pl.ck_dw;
     P.band_w = pl.band_w; P.redo = (uint32_t *)(ctr + C_REDO); P.win = (uint32_t *)(ctr + C_WIN);
     P.prof = getenv("IMSAME_NW_PROF") ? (unsigned long long *)(ctr + C_PROF) : nullptr;
+    P.slot_bits = pl.np ? c->slotbits.as<uint32_t>() : nullptr; P.slot_words = pl.slot_words;
     HIPCHK(hipMemsetAsync(work, 0, 4, s));
     HIPCHK(hipEventRecord(c->ev0, s));           // the launch's time includes its ordering
     if (crow && pl.two && n >= 64) {
@@ -930,11 +1035,16 @@ static int launch_nw(imsame_ctx *c, NwPlan pl, const uint32_t *cread, const uint
         const char *wb = getenv("IMSAME_NW_WIN_BOTTOM");
         P.win_bottom = wb ? atoi(wb) : NW16_WIN_BOTTOM;
     }
-    if (pl.lng)                 nwl_kernel<<<pl.blocks, 256, pl.lds, s>>>(P);
-    else if (pl.two && pl.last4) nw16_kernel<true, true><<<pl.blocks, 256, pl.lds, s>>>(P);
-    else if (pl.two)            nw16_kernel<false, true><<<pl.blocks, 256, pl.lds, s>>>(P);
-    else if (pl.pk && pl.last4) nw16_kernel<true, false><<<pl.blocks, 256, pl.lds, s>>>(P);
-    else if (pl.pk)             nw16_kernel<false, false><<<pl.blocks, 256, pl.lds, s>>>(P);
+    const bool k5 = pl.k == NW16_K5;
+    if (pl.lng)                        nwl_kernel<<<pl.blocks, 256, pl.lds, s>>>(P);
+    else if (pl.two && pl.last4 && k5) nw16_kernel<NW16_K5, true, true><<<pl.blocks, 256, pl.lds, s>>>(P);
+    else if (pl.two && k5)             nw16_kernel<NW16_K5, false, true><<<pl.blocks, 256, pl.lds, s>>>(P);
+    else if (pl.pk && pl.last4 && k5)  nw16_kernel<NW16_K5, true, false><<<pl.blocks, 256, pl.lds, s>>>(P);
+    else if (pl.pk && k5)              nw16_kernel<NW16_K5, false, false><<<pl.blocks, 256, pl.lds, s>>>(P);
+    else if (pl.two && pl.last4)       nw16_kernel<NW16_K, true, true><<<pl.blocks, 256, pl.lds, s>>>(P);
+    else if (pl.two)                   nw16_kernel<NW16_K, false, true><<<pl.blocks, 256, pl.lds, s>>>(P);
+    else if (pl.pk && pl.last4)        nw16_kernel<NW16_K, true, false><<<pl.blocks, 256, pl.lds, s>>>(P);
+    else if (pl.pk)                    nw16_kernel<NW16_K, false, false><<<pl.blocks, 256, pl.lds, s>>>(P);
     else if (pl.nstr > 1) nw_kernel<true><<<pl.blocks, 256, pl.lds, s>>>(P);
     else                  nw_kernel<false><<<pl.blocks, 256, pl.lds, s>>>(P);
     HIPCHK(hipEventRecord(c->ev1, s));
@@ -947,8 +1057,10 @@ static int launch_nw(imsame_ctx *c, NwPlan pl, const uint32_t *cread, const uint
     if (c->origin) {                             // interval on the call's common clock
         float a = 0, b = 0;
         if (hipEventElapsedTime(&a, c->origin, c->ev0) == hipSuccess &&
-            hipEventElapsedTime(&b, c->origin, c->ev1) == hipSuccess)
+            hipEventElapsedTime(&b, c->origin, c->ev1) == hipSuccess) {
             c->nw_iv.push_back({a, b});
+            if (timeline_on()) c->tl.push_back({'N', c->cur_round, n, a, b});
+        }
     }
     return 0;
 }
@@ -1128,6 +1240,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     uint32_t *act = c->act0.as<uint32_t>(), *nxt = c->act1.as<uint32_t>();
     while (nact) {
         st.rounds++;
+        c->cur_round = (int)st.rounds;
         HIPCHK(hipMemsetAsync(ctr + C_NCAND, 0, 3 * 8, s));     // NCAND, NCAND2, NNEXT
         SeedLaunch S;
         S.db = c->db.as<uint8_t>(); S.db_start = c->db_start.as<uint64_t>(); S.n_db = c->n_db; S.db_len = c->db_len;
@@ -1177,6 +1290,11 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         float fs = 0;
         HIPCHK(hipEventElapsedTime(&fs, c->ev0, c->ev1));
         st.ms_seed += fs;
+        if (c->origin && timeline_on()) {
+            float a = 0;
+            if (hipEventElapsedTime(&a, c->origin, c->ev0) == hipSuccess)
+                c->tl.push_back({'S', (int)st.rounds, nact, a, a + fs});
+        }
         const uint32_t n1 = (uint32_t)hc[0], n2 = (uint32_t)hc[1];
         if (n1 + n2 + hc[2] == 0) break;                          // no candidates, nobody paused
         struct Cls { uint32_t n; uint32_t *cr, *cs; imsame_read_result *o; uint32_t ylim; int work; };
@@ -1195,11 +1313,14 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
                 st.launch_cand[st.nw_launches] = cls[k].n;
                 st.launch_ms[st.nw_launches] = ms;
                 if (pl.pk) st.launch_pk |= 1ull << st.nw_launches;
+                if (pl.pk && pl.k == NW16_K5) st.launch_k5 |= 1ull << st.nw_launches;
+                if (pl.np) st.launch_np |= 1ull << st.nw_launches;
             }
             st.ms_nw += ms; st.nw_launches++; st.n_nw += cls[k].n;
             UpdLaunch U = {cls[k].cr, cls[k].cs, cls[k].n, cls[k].o, read_from, c->res.as<imsame_read_result>(),
                            c->rstat.as<uint8_t>(), c->memo.as<uint32_t>(), c->nmemo.as<uint8_t>(),
-                           c->cbase.as<uint32_t>(), c->ccnt.as<uint32_t>(), c->perr.as<uint32_t>(), nxt,
+                           c->cbase.as<uint32_t>(), c->ccnt.as<uint32_t>(), c->perr.as<uint32_t>(),
+                           c->cur_p.as<uint64_t>(), nxt,
                            (uint32_t *)(ctr + C_NNEXT), (unsigned long long *)(ctr + C_CELLS),
                            (unsigned long long *)(ctr + C_NACC), (unsigned long long *)(ctr + C_ERR),
                            c->db_start.as<uint64_t>()};
@@ -1247,6 +1368,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     st.nw_launch_ms = st.nw_launches ? st.ms_nw / st.nw_launches : 0;
     st.nw_bytes = 2 * st.nw_cells;       // 2 B/cell traceback floor; bench.py adds xlen + ylen per NW
     int ret = IMSAME_OK;
+    if (hc[C_FLAGS] & 4) return IMSAME_E_HIP;     // a non-persistent NW wave found no arena slot (never)
     if (hc[C_ERR] != ~0ull) {
         st.err_read = hc[C_ERR] >> 32; st.err_dbseq = hc[C_ERR] & 0xFFFFFFFFull;
         ret = IMSAME_E_READ_TOO_LONG;
@@ -1375,6 +1497,7 @@ static int align_impl(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint6
         int rc = align_one(c, read_from, read_to, n_threads_semantic, p, res, paths, paths_cap, paths_used, &s1);
         s1.ms_nw_busy = union_ms(c->nw_iv);
         span_ms(c->nw_iv, &s1.ms_nw_first, &s1.ms_nw_last);
+        if (timeline_on()) timeline_print({c});
         if (stats) *stats = s1;
         if (fn) {
             const int rd = deliver_part(c, p, read_from, read_to, rc, paths_used ? *paths_used : 0, s1.err_read, fn, user);
@@ -1423,6 +1546,7 @@ static int align_impl(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint6
     for (int k = 1; k < nl; ++k) th.emplace_back(lane_run, k);
     lane_run(0);
     for (auto &t : th) t.join();
+    if (timeline_on()) timeline_print(L);
     for (int k = 1; k < nl; ++k) L[k]->origin = nullptr;
     for (int k = 0; k < nl; ++k) L[k]->nlanes = 1;
     for (int r : R)
@@ -1443,7 +1567,7 @@ static int align_impl(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint6
     }
     imsame_stats st = S[0];
     std::vector<std::pair<float, float>> iv = c->nw_iv;
-    st.nw_launches = 0; st.launch_pk = 0;
+    st.nw_launches = 0; st.launch_pk = 0; st.launch_k5 = 0; st.launch_np = 0;
     for (int k = 0; k < nl; ++k) {
         const imsame_stats &x = S[k];
         if (k) {
@@ -1459,6 +1583,8 @@ static int align_impl(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint6
             if (st.nw_launches + j >= IMSAME_LAUNCH_STATS) break;
             st.launch_cand[st.nw_launches + j] = x.launch_cand[j]; st.launch_ms[st.nw_launches + j] = x.launch_ms[j];
             if ((x.launch_pk >> j) & 1) st.launch_pk |= 1ull << (st.nw_launches + j);
+            if ((x.launch_k5 >> j) & 1) st.launch_k5 |= 1ull << (st.nw_launches + j);
+            if ((x.launch_np >> j) & 1) st.launch_np |= 1ull << (st.nw_launches + j);
         }
         st.nw_launches += x.nw_launches;
     }

@@ -14,7 +14,8 @@
 // price of one and the instruction count is the cost model.
 //
 // Mapping: a group of G lanes carries candidates 2g and 2g+1 of its wave's
-// share; lane gl owns NW16_K = 10 consecutive columns and walks the rows with
+// share; lane gl owns K = 10 consecutive columns (K = 5 for latency-bound
+// launches: twice the waves, each half as long -- nw16_k) and walks the rows with
 // a one-lane skew (step t: row i = t - gl); the row state crosses lanes by
 // DPP wave_shr:1.  The two halves share the row and column indices, so every
 // row/column constant is common; only the bases differ.  Records are staged
@@ -30,7 +31,7 @@
 // codes; each decision is the sign of a packed difference, turned into a
 // 0xFFFF mask (v_pk_ashrrev 15) where a select (v_bitop3) needs it.
 //
-// Traceback, three dwords per lane per step (0.6 B/cell):
+// Traceback, three dwords per lane per step (0.6 B/cell; K = 5: WM and WU only):
 //   WM  cells 0-7: bit s = NOT-diag(A), 8+s NOT-diag(B), 16+s up(A), 24+s up(B)
 //       -- one v_perm turns the four signs of (d0 - lu, l0 - u0) into 0xFF/0x00
 //          bytes (selectors 8-11 replicate bits 15/31/47/63)
@@ -72,10 +73,13 @@
 // within +-R, R <= 8191, so values, sentinels (NW16_BIG = 2^14) and every
 // compared difference fit (nw16_fits); otherwise nw_kernel.hip runs.
 
-#define NW16_K   10               // columns per lane
+#define NW16_K   10               // columns per lane (the full-chip launches)
+#define NW16_K5  5                // columns per lane of the latency-bound launches (nw16_k)
 #define NW16_BIG 16384
 #define NW16_CK  24               // checkpoint interval of the first sweep (steps, even: the rotation period)
-#define NW16_NST (5 * NW16_K + 5) // dwords of wave state per lane in a checkpoint
+// dwords of wave state per lane in a checkpoint; traceback dwords per lane per step
+__host__ __device__ constexpr int nw16_nst(int K) { return 5 * K + 5; }
+__host__ __device__ constexpr int nw16_nrec(int K) { return K > 8 ? 3 : 2; }
 #define NW16_NOROW INT32_MIN      // cand_row: no prediction
 #define NW16_WIN_UP 32            // window rows above the predicted first row
 #define NW16_WIN_DOWN 24          // ... and below the predicted last row
@@ -91,7 +95,8 @@ __host__ static inline bool nw16_fits(int64_t ig, int64_t eg, uint64_t xcap, uin
     if (aig > 8191 || aeg > 8191) return false;
     // |T| <= 4*ycols; l0 >= -T - |ig| - |eg|*ycols; u0 drifts at most over
     // xcap + 64 rows (lockstep garbage rows included -- a second sweep runs at
-    // most NW16_CK + G <= 40 rows past the first one) and takes u2 + ig + 2eg
+    // most NW16_CK + G <= 24 + 32 rows past the first one, G <= 32 at K = 5)
+    // and takes u2 + ig + 2eg.  ycols at K = 10 bounds ycols at K = 5.
     const uint64_t R = 4 * ycols + aig + aeg * (xcap + 64 + ycols + 2) + 16;
     return R <= 8191;
 }
@@ -109,13 +114,14 @@ WV_DEVICE uint32_t base_code(uint8_t b) { return (b >> 1) & 3u; }          // A0
 // traceback of half h of group g (layout above) -> nw_kernel.hip's nibble
 // t0: step of the sweep that wrote record 0 (0: one pass, steps indexed by t;
 // two passes: the half's restart step, cells before it were not written)
+template <int K>
 struct TbAcc16 {
     const uint32_t *tb; const uint8_t *X; const uint8_t *Y; int g, G, h, t0;
     int t1 = INT_MAX;                      // steps [t0, t1) were written
-    __device__ bool has(int i, int j) const { const int t = i + j / NW16_K; return t >= t0 && t < t1; }
+    __device__ bool has(int i, int j) const { const int t = i + j / K; return t >= t0 && t < t1; }
     __device__ uint32_t nib(int i, int j) const {
-        const int l = j / NW16_K, s = j - l * NW16_K;
-        const uint32_t *w = tb + ((uint32_t)(i + l - t0) * 64u + (uint32_t)(g * G + l)) * 3u;
+        const int l = j / K, s = j - l * K;
+        const uint32_t *w = tb + ((uint32_t)(i + l - t0) * 64u + (uint32_t)(g * G + l)) * (uint32_t)nw16_nrec(K);
         uint32_t nd, up, U, nL;
         if (s < 8) {
             const uint32_t wm = w[0], wu = w[1];
@@ -135,12 +141,13 @@ __host__ __device__ static inline size_t nw16_wave_lds(int GPW, int xstride) {
     return (size_t)GPW * xstride + 64 * 8 * 4;
 }
 
-// LAST: every read length of the launch is a multiple of NW16_K, so each
-// candidate's last column is slot NW16_K-1 of its owner lane (no select).
+// LAST: every read length of the launch is a multiple of K, so each
+// candidate's last column is slot K-1 of its owner lane (no select).
 // TWO: score-only sweep + checkpoints, then the traceback band (header).
-template <bool LAST, bool TWO>
+template <int K, bool LAST, bool TWO>
 __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const uint32_t slot) {
-    constexpr int K = NW16_K;
+    constexpr int NST = nw16_nst(K), NREC = nw16_nrec(K);
+    constexpr uint32_t RECB = 64u * 4u * NREC;     // traceback bytes per step
     const int G = P.G, GPW = P.GPW;
     const int g = lane / G, gl = lane - g * G;
     const bool in_group = g < GPW;
@@ -156,7 +163,8 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
     auto mark = [&](const int k) {
         if (P.prof) { const unsigned long long n = wv_clock(); ph[k] += n - tq; tq = n; }
     };
-    for (;;) {
+    for (uint32_t ntask = 0;; ++ntask) {
+        if (P.slot_bits && ntask) break;          // non-persistent launch: one task per wave
         uint32_t base = 0;
         if (lane == 0) base = wv_atomic_add(P.counter, (uint32_t)(2 * GPW));
         base = wv_first(base);
@@ -369,8 +377,9 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
             // rows outside [1, xlen) are never read; 32-bit byte offset from the
             // wave-uniform slot base (global_store saddr form)
             if (TB) {
-                uint32_t *rec = (uint32_t *)(tb3 + ((uint32_t)(t - tb0) * 768u + (uint32_t)lane * 12u));
-                rec[0] = wm; rec[1] = wu; rec[2] = wx;
+                uint32_t *rec = (uint32_t *)(tb3 + ((uint32_t)(t - tb0) * RECB + (uint32_t)lane * (4u * NREC)));
+                rec[0] = wm; rec[1] = wu;
+                if (NREC > 2) rec[2] = wx;
             }
             // last column (rows 1 .. xlen-2) and last row (:481-484)
             uint32_t vl = cur[LAST ? K - 1 : 0];
@@ -399,10 +408,10 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
         };
         // Checkpoint m = the state before step 1 + m*NW16_CK, where the roles
         // are (cur, own) = (A, B), (in0, in1) = (I2, I1); register r of lane l
-        // at ckw[(m*NW16_NST + r)*64] (coalesced).
+        // at ckw[(m*NST + r)*64] (coalesced).
         constexpr bool TB1 = !TWO;                // the first sweep writes traceback only in one-pass mode
         auto save = [&](const int m) {
-            uint32_t *p = ckw + (uint32_t)m * (NW16_NST * 64u);
+            uint32_t *p = ckw + (uint32_t)m * (NST * 64u);
 #pragma unroll
             for (int s = 0; s < K; ++s) {
                 p[s * 64] = A[s]; p[(K + s) * 64] = B[s]; p[(2 * K + s) * 64] = dI[s];
@@ -486,7 +495,7 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
         mark(2);
         if (!TWO) {
             for (int h = 0; h < 2; ++h) {
-                const TbAcc16 acc16 = {tbw, X8, Yp[h], gg, G, h, 0};
+                const TbAcc16<K> acc16 = {tbw, X8, Yp[h], gg, G, h, 0};
                 nw_finish(P, acc16, xl[h], yl[h], valid[h], gg, gl, G, bscore[h], bx[h], by[h], cidx[h], sid[h]);
             }
             wv_lds_sync();
@@ -505,7 +514,7 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
             for (int h = 0; h < 2; ++h) cov[h] = todo[h] && bx[h] + G <= tw1;
             if (wv_any(cov[0] || cov[1])) {
                 for (int h = 0; h < 2; ++h) {
-                    TbAcc16 acc16 = {tbw, X8, Yp[h], gg, G, h, tw0};
+                    TbAcc16<K> acc16 = {tbw, X8, Yp[h], gg, G, h, tw0};
                     acc16.t1 = tw1;
                     const bool lost = nw_finish(P, acc16, xl[h], yl[h], cov[h], gg, gl, G, bscore[h], bx[h], by[h],
                                                 cidx[h], sid[h]);
@@ -560,8 +569,9 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
                     wx = wv_and_or(mnL, 0x00100010u << q, wx);
                 }
             }
-            uint32_t *rec = (uint32_t *)(tb3 + ((uint32_t)tau * 768u + (uint32_t)lane * 12u));
-            rec[0] = wm; rec[1] = wu; rec[2] = wx;
+            uint32_t *rec = (uint32_t *)(tb3 + ((uint32_t)tau * RECB + (uint32_t)lane * (4u * NREC)));
+            rec[0] = wm; rec[1] = wu;
+            if (NREC > 2) rec[2] = wx;
             in0 = MASK ? wv_bfi(pm, in1, sN) : sN;
             outT = cur[K - 1]; outMS = mfS; outL = l0;
         };
@@ -576,8 +586,8 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
             }
             for (int o = 32; o > 0; o >>= 1) n2 = max(n2, wv_shfl_xor(n2, o));
             {   // restore: half A from its checkpoint, half B from its own
-                const uint32_t *pa = ckw + (uint32_t)((t0h[0] - 1) / NW16_CK) * (NW16_NST * 64u);
-                const uint32_t *pb = ckw + (uint32_t)((t0h[1] - 1) / NW16_CK) * (NW16_NST * 64u);
+                const uint32_t *pa = ckw + (uint32_t)((t0h[0] - 1) / NW16_CK) * (NST * 64u);
+                const uint32_t *pb = ckw + (uint32_t)((t0h[1] - 1) / NW16_CK) * (NST * 64u);
                 auto ld = [&](const int r) { return wv_bfi(0x0000FFFFu, pa[r * 64], pb[r * 64]); };
 #pragma unroll
                 for (int s = 0; s < K; ++s) {
@@ -606,7 +616,7 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
             wv_mem_sync();                        // band traceback written by all lanes, read by the walkers
             mark(3);
             for (int h = 0; h < 2; ++h) {
-                const TbAcc16 acc16 = {tbw, X8, Yp[h], gg, G, h, t0h[h]};
+                const TbAcc16<K> acc16 = {tbw, X8, Yp[h], gg, G, h, t0h[h]};
                 todo[h] = nw_finish(P, acc16, xl[h], yl[h], todo[h], gg, gl, G, bscore[h], bx[h], by[h], cidx[h],
                                     sid[h]);
             }
@@ -621,10 +631,12 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
         for (int k = 0; k < 5; ++k) wv_atomic_add64(P.prof + k, ph[k]);
 }
 
-// Launch shape: G lanes per group, GPW groups (2*GPW candidates) per wave
-__host__ static inline NwShape nw16_shape(uint32_t ymax, uint32_t xcap) {
+// Launch shape: G lanes per group, GPW groups (2*GPW candidates) per wave,
+// K columns per lane
+__host__ static inline NwShape nw16_shape(uint32_t ymax, uint32_t xcap, int K = NW16_K) {
     NwShape s;
-    s.G = (int)((ymax + NW16_K - 1) / NW16_K);
+    s.k = K;
+    s.G = (int)((ymax + K - 1) / K);
     if (s.G < 1) s.G = 1;
     s.GPW = 64 / s.G; s.nstr = 1;
     s.xcap = xcap < 2 ? 2 : (int)xcap;
@@ -633,23 +645,82 @@ __host__ static inline NwShape nw16_shape(uint32_t ymax, uint32_t xcap) {
     s.steps = s.xcap + s.G;
     return s;
 }
-// traceback dwords per wave slot (three per lane per step)
-__host__ static inline uint64_t nw16_tb_words(const NwShape &s) { return (uint64_t)s.steps * 64 * 3; }
+// traceback dwords per wave slot (NREC per lane per step)
+__host__ static inline uint64_t nw16_tb_words(const NwShape &s) { return (uint64_t)s.steps * 64 * nw16_nrec(s.k); }
 // checkpoint dwords per wave slot (two-pass mode): one per NW16_CK steps + the start
 __host__ static inline uint64_t nw16_ck_words(const NwShape &s) {
-    return (uint64_t)((s.steps + NW16_CK - 1) / NW16_CK + 1) * NW16_NST * 64;
+    return (uint64_t)((s.steps + NW16_CK - 1) / NW16_CK + 1) * nw16_nst(s.k) * 64;
 }
 
 #ifndef IMSAME_WAVE_EMU
+// The XCD (accelerator complex die) a wave runs on: each of the 8 has its own
+// L2, so an arena slot is reused only by waves of the XCD that wrote it last
+// (a store that reached one L2 is not visible to, nor ordered against, the
+// others until that L2 writes it back).
+__device__ __forceinline__ uint32_t nw_xcc_id() {
+    uint32_t v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(v));
+    return v;
+}
+// Non-persistent launches (NwLaunch::slot_bits): a wave takes a free slot of
+// its XCD's partition (lane 0 sets a bit; partitions hold the XCD's whole
+// residency of the kernel, so one is always free once the wave is resident)
+// and frees it when its stores have completed.  Returns ~0u only if no slot
+// turned up after 2^22 probes.
+__device__ uint32_t nw_slot_claim(const NwLaunch &P, const int lane) {
+    const uint32_t part = nw_xcc_id() & 7u, nw = P.slot_words;
+    uint32_t *bits = P.slot_bits + part * nw;
+    uint32_t got = ~0u;
+    if (lane == 0) {
+        uint32_t w = blockIdx.x % nw;
+        for (uint32_t it = 0; it < (1u << 22) && got == ~0u; ++it) {
+            uint32_t v = __hip_atomic_load(bits + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            while (v != 0xFFFFFFFFu) {
+                const uint32_t b = (uint32_t)__builtin_ctz(~v);
+                const uint32_t old = __hip_atomic_fetch_or(bits + w, 1u << b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (!(old & (1u << b))) { got = (part * nw + w) * 32u + b; break; }
+                v = old | (1u << b);
+            }
+            if (got == ~0u && ++w == nw) { w = 0; __builtin_amdgcn_s_sleep(4); }
+        }
+    }
+    return __builtin_amdgcn_readfirstlane(wv_shfl((int)got, 0));
+}
+__device__ __forceinline__ void nw_slot_release(const NwLaunch &P, const int lane, const uint32_t slot) {
+    __builtin_amdgcn_s_waitcnt(0);                 // every store of this wave has reached the XCD's L2
+    if (lane == 0)
+        __hip_atomic_fetch_and(P.slot_bits + (slot >> 5), ~(1u << (slot & 31u)), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// XCC_ID of every block (imsame_dev.hip checks it before it trusts the
+// partitions above)
+__global__ void xcc_probe_kernel(uint32_t *out) {
+    if (threadIdx.x == 0) out[blockIdx.x] = nw_xcc_id();
+}
+
 #ifndef NW16_WAVES_PER_EU
 #define NW16_WAVES_PER_EU 4
 #endif
-template <bool LAST, bool TWO>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NW16_WAVES_PER_EU)))
+#ifndef NW16_K5_WAVES_PER_EU
+#define NW16_K5_WAVES_PER_EU 5
+#endif
+template <int K, bool LAST, bool TWO>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? NW16_WAVES_PER_EU : NW16_K5_WAVES_PER_EU)))
 void nw16_kernel(NwLaunch P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
+    if (P.slot_bits) {                          // non-persistent: one task, a slot of this XCD
+        const uint32_t slot = nw_slot_claim(P, lane);
+        if (slot == ~0u) {                      // never (partitions hold the residency); the queue
+            if (lane == 0) wv_atomic_or(P.flags, 4u);     // is drained by the other waves
+            return;
+        }
+        nw16_wave<K, LAST, TWO>(P, smem + wib * nw16_wave_lds(P.GPW, P.xstride), lane, slot);
+        nw_slot_release(P, lane, slot);
+        return;
+    }
     const uint32_t slot = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + wib);   // wave-uniform
-    nw16_wave<LAST, TWO>(P, smem + wib * nw16_wave_lds(P.GPW, P.xstride), lane, slot);
+    nw16_wave<K, LAST, TWO>(P, smem + wib * nw16_wave_lds(P.GPW, P.xstride), lane, slot);
 }
 #endif

@@ -70,6 +70,10 @@ struct NwLaunch {
     int32_t  band_w;
     uint32_t *redo;
     unsigned long long *prof;    // optional (IMSAME_NW_PROF): shader cycles per phase, summed over waves
+    // non-persistent launches (nw16_kernel): one wave per task, its arena slot
+    // taken from a bitmap of free slots in the partition of the XCD it runs on
+    // (NULL: persistent launch, slot = the wave's index in the grid)
+    uint32_t *slot_bits; uint32_t slot_words;   // words per XCD partition
 };
 
 // LDS bytes one wave needs
@@ -482,7 +486,7 @@ __device__ void nw_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const u
 // Launch shape for reads up to ymax and records up to xcap: short reads pack
 // 64/G candidates per wave, long reads take a wave each over several strips;
 // X staging is capped at 16 KB of LDS per wave.
-struct NwShape { int G, GPW, nstr, xcap, xstride, steps; };
+struct NwShape { int G, GPW, nstr, xcap, xstride, steps, k = 0; };   // k: nw16 columns per lane
 __host__ static inline NwShape nw_shape(uint32_t ymax, uint32_t xcap) {
     NwShape s;
     if (ymax <= NW_W / 2) {

@@ -13,6 +13,10 @@
 #define MEMO 16
 #define NBUCKETS (1u << 24)
 enum { RS_ACTIVE = 0, RS_DONE = 1, RS_ACCEPTED = 2, RS_ERROR = 3 };
+// cursor of a read whose scan reached its last window (above every up_to):
+// when its pending candidates are all rejected it is "not found" at once
+// (update_one), instead of a next round whose scan finds nothing
+#define CUR_EXHAUSTED (~1ull)
 
 __device__ __forceinline__ uint32_t base2(uint32_t c) { return ((c >> 1) ^ (c >> 2)) & 3u; }  // A0 C1 G2 T3
 
@@ -298,7 +302,7 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint
         }
         return;
     }
-    if (ne < spec && !perr && !paused) { S.cur_p[k] = up_to; S.cur_h[k] = 0; }   // scan exhausted
+    if (ne < spec && !perr && !paused) { S.cur_p[k] = CUR_EXHAUSTED; S.cur_h[k] = 0; }   // scan exhausted
     S.perr[k] = perr;
     const bool shortc = ylen <= S.short_ylen;
     const uint32_t o = wv_atomic_add(shortc ? S.ncand : S.ncand2, ne);
@@ -471,7 +475,7 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
         }
         return;
     }
-    if (exhausted && !perr) { S.cur_p[k] = up_to; S.cur_h[k] = 0; }   // scan exhausted
+    if (exhausted && !perr) { S.cur_p[k] = CUR_EXHAUSTED; S.cur_h[k] = 0; }   // scan exhausted
     S.perr[k] = perr;
     const bool shortc = ylen <= S.short_ylen;
     const uint32_t o = wv_atomic_add(shortc ? S.ncand : S.ncand2, ne);
@@ -533,6 +537,7 @@ struct UpdLaunch {
     imsame_read_result *res;
     uint8_t *rstat; uint32_t *memo; uint8_t *nmemo;
     const uint32_t *cbase, *ccnt, *perr;
+    const uint64_t *cur_p;                 // CUR_EXHAUSTED: nothing left to scan
     uint32_t *next; uint32_t *nnext;
     unsigned long long *cells; unsigned long long *nacc;
     unsigned long long *err;
@@ -569,6 +574,7 @@ __device__ __forceinline__ void update_one(const UpdLaunch &U, uint32_t c, uint6
         wv_atomic_min64(U.err, (unsigned long long)(((uint64_t)r << 32) | (U.perr[k] - 1)));
         return;
     }
+    if (U.cur_p[k] == CUR_EXHAUSTED) { U.rstat[k] = RS_DONE; return; }      // no hit left: not found
     U.next[wv_atomic_add(U.nnext, 1u)] = r;
 }
 

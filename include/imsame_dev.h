@@ -134,6 +134,10 @@ typedef struct imsame_stats {
     double   ms_nw_first;   /* first NW launch start / last NW launch end, ms
                                after the call's first device operation     */
     double   ms_nw_last;
+    uint64_t launch_k5;     /* bit k: packed NW launch k ran 5 columns per lane
+                               (latency-bound launches), else 10           */
+    uint64_t launch_np;     /* bit k: NW launch k was non-persistent (one wave
+                               per task, arena slots per XCD)             */
 } imsame_stats;
 
 typedef struct imsame_ctx imsame_ctx;

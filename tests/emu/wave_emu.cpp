@@ -62,7 +62,11 @@ static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, cons
     const bool two = pk && !(p->flags & IMSAME_FLAG_NW16_ONEPASS) && !(op && atoi(op));
     const char *le = getenv("IMSAME_NWL");
     const bool lng = !pk && !(p->flags & IMSAME_FLAG_NW32) && !(le && !atoi(le)) && nwl_fits(p->igap, p->egap, ymax);
-    const NwShape sh = pk ? nw16_shape(ymax, xmax) : lng ? nwl_shape(ymax, xmax) : nw_shape(ymax, xmax);
+    // columns per lane of the packed kernel: imsame_dev.hip:nw16_k picks by the
+    // chip's fill; here IMSAME_NW_K=5 selects the latency-bound form
+    const char *ke = getenv("IMSAME_NW_K");
+    const int K = (ke && atoi(ke) == NW16_K5) ? NW16_K5 : NW16_K;
+    const NwShape sh = pk ? nw16_shape(ymax, xmax, K) : lng ? nwl_shape(ymax, xmax) : nw_shape(ymax, xmax);
     std::vector<uint32_t> tb((pk ? nw16_tb_words(sh) : lng ? nwl_tb_words(sh, ymax) : nw_tb_words(sh)) + 64, 0xABABABABu);
     std::vector<uint32_t> ck(two ? nw16_ck_words(sh) : lng ? nwl_ck_words(sh) : 1, 0xCDCDCDCDu);
     const char *be = getenv("IMSAME_NW_BAND");
@@ -115,10 +119,16 @@ static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, cons
     bool ymult = true;        // every read length a multiple of NW16_K (imsame_dev.hip: q_len_mult)
     for (uint32_t k = 0; k < n; ++k) ymult = ymult && (qs[cread[k] + 1] - qs[cread[k]]) % NW16_K == 0;
     if (lng)              run_wave([&](int lane) { nwl_wave(P, lds.data(), lane, 0); });
-    else if (two && ymult) run_wave([&](int lane) { nw16_wave<true, true>(P, lds.data(), lane, 0); });
-    else if (two)         run_wave([&](int lane) { nw16_wave<false, true>(P, lds.data(), lane, 0); });
-    else if (pk && ymult) run_wave([&](int lane) { nw16_wave<true, false>(P, lds.data(), lane, 0); });
-    else if (pk)          run_wave([&](int lane) { nw16_wave<false, false>(P, lds.data(), lane, 0); });
+    else if (pk && K == NW16_K5) {
+        if (two && ymult)     run_wave([&](int lane) { nw16_wave<NW16_K5, true, true>(P, lds.data(), lane, 0); });
+        else if (two)         run_wave([&](int lane) { nw16_wave<NW16_K5, false, true>(P, lds.data(), lane, 0); });
+        else if (pk && ymult) run_wave([&](int lane) { nw16_wave<NW16_K5, true, false>(P, lds.data(), lane, 0); });
+        else if (pk)          run_wave([&](int lane) { nw16_wave<NW16_K5, false, false>(P, lds.data(), lane, 0); });
+    }
+    else if (two && ymult) run_wave([&](int lane) { nw16_wave<NW16_K, true, true>(P, lds.data(), lane, 0); });
+    else if (two)         run_wave([&](int lane) { nw16_wave<NW16_K, false, true>(P, lds.data(), lane, 0); });
+    else if (pk && ymult) run_wave([&](int lane) { nw16_wave<NW16_K, true, false>(P, lds.data(), lane, 0); });
+    else if (pk)          run_wave([&](int lane) { nw16_wave<NW16_K, false, false>(P, lds.data(), lane, 0); });
     else if (sh.nstr > 1) run_wave([&](int lane) { nw_wave<true>(P, lds.data(), lane, 0); });
     else             run_wave([&](int lane) { nw_wave<false>(P, lds.data(), lane, 0); });
     return 0;
@@ -300,7 +310,7 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
                    (uint32_t)paths_cap, &pused, &flags, c.row);
             st.n_nw += c.n;
             UpdLaunch U = {c.r, c.s, c.n, c.o, read_from, res, rstat.data(), memo.data(), nmemo.data(),
-                           cbase.data(), ccnt.data(), perr.data(), nxt.data(), &nc[2], &cells, &nacc, &err,
+                           cbase.data(), ccnt.data(), perr.data(), cur_p.data(), nxt.data(), &nc[2], &cells, &nacc, &err,
                            dbs.data()};
             for (uint32_t k = 0; k < c.n; ++k) { uint64_t ce = 0, ac = 0; update_one(U, k, ce, ac); cells += ce; nacc += ac; }
         }

@@ -751,6 +751,51 @@ def test_align_parts_hand_over_every_lane(dev, monkeypatch):
                 assert t1 == t0, k
 
 
+@pytest.mark.timeout(300)
+def test_nw16_launch_forms_equal(dev, oracle, monkeypatch):
+    """nw16_kernel's launch forms on a 1/8-shard-sized call (3 lanes):
+    10 or 5 columns per lane (imsame_dev.hip:nw16_k) and persistent or
+    non-persistent launches (one wave per task, arena slots from a per-XCD
+    free bitmap, nw16_kernel.hip:nw_slot_claim).  Every per-read field and
+    every accepted path's text equal across the forms, and the default run
+    equals the oracle on three windows."""
+    ref, rst = synth.make_reference_arr(4_000_000, 2_000, seed=71)
+    q, qs = synth.make_reads_arr(ref, 125_000, 150, seed=72, ins=0.003, dele=0.003)
+    dev.index(ref, rst)
+    dev.set_query(q, qs)
+    base, pb, sb = dev.align(n_threads=16, want_paths=True)
+    assert sb.launch_np != 0                      # the XCC probe passed: non-persistent launches ran
+    runs = {}
+    for name, env in [("k10_persistent", {"IMSAME_NW_K": "10", "IMSAME_NW_PERSIST": "1"}),
+                      ("k5_all", {"IMSAME_NW_K": "5"}),
+                      ("k10_np", {"IMSAME_NW_K": "10"})]:
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        runs[name] = dev.align(n_threads=16, want_paths=True)
+        for k in env:
+            monkeypatch.delenv(k)
+    st = runs["k10_persistent"][2]
+    assert st.launch_np == 0 and st.launch_k5 == 0
+    st = runs["k5_all"][2]
+    assert st.launch_k5 == st.launch_pk and st.launch_pk != 0
+    for name, (res, pp, st) in runs.items():
+        assert not _cmp(res, base), (name, _cmp(res, base))
+        assert st.n_nw == sb.n_nw
+        for k in np.flatnonzero(base["status"] == 1)[::97]:
+            r, r0 = res[k], base[k]
+            s_ = int(r0["db_seq"])
+            X = ref[int(rst[s_]):int(rst[s_]) + 2_000].tobytes()
+            Y = q[int(qs[k]):int(qs[k]) + 150].tobytes()
+            t1, _ = render(X, Y, r, pp[r["path_off"]:r["path_off"] + r["path_len"]])
+            t0, _ = render(X, Y, r0, pb[r0["path_off"]:r0["path_off"] + r0["path_len"]])
+            assert t1 == t0, (name, k)
+    wins = _windows(len(qs))
+    rc, exp, _ = oracle.align_windows(ref, rst, q, qs, wins, None, 16)
+    assert rc == 0
+    for (a, b), e in zip(wins, exp):
+        assert not _cmp(base[a:b], e), ((a, b), _cmp(base[a:b], e))
+
+
 def test_lanes_equal_one_lane(dev, monkeypatch):
     """Three concurrent lanes (parts of a call on three streams) against one
     lane: identical per-read rows and identical .align text for every

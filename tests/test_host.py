@@ -100,9 +100,12 @@ def test_emulated_nw_kernel_matches_reference_golden(emu, oracle, flags):
                 assert int(res[k][f]) == r[f], (f, ig, eg, len(r["X"]), len(r["Y"]))
 
 
-def test_emulated_packed_nw_mixed_shapes(emu, oracle):
+@pytest.mark.parametrize("cols", ["10", "5"])
+def test_emulated_packed_nw_mixed_shapes(emu, oracle, cols, monkeypatch):
     """nw16_kernel.hip (emulated) on launches mixing record lengths, read
-    lengths (unequal halves of a pair, idle groups) and gap parameters."""
+    lengths (unequal halves of a pair, idle groups) and gap parameters, with
+    10 and 5 columns per lane (imsame_dev.hip:nw16_k)."""
+    monkeypatch.setenv("IMSAME_NW_K", cols)
     rng = np.random.default_rng(77)
     acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
     for ig, eg, mult5 in [(-5, -2, False), (0, 0, False), (-40, -2, False), (-5, -2, True), (-3, -1, True)]:
@@ -133,8 +136,8 @@ def test_emulated_packed_nw_mixed_shapes(emu, oracle):
                 assert int(res[k][f]) == int(o[f]), (f, k, ig, eg, len(X[k]), len(Y[k]))
 
 
-@pytest.mark.parametrize("band", ["200", "40", "0"])
-def test_emulated_two_pass_band(emu, oracle, band, monkeypatch):
+@pytest.mark.parametrize("band,cols", [("200", "10"), ("40", "10"), ("0", "10"), ("200", "5"), ("0", "5")])
+def test_emulated_two_pass_band(emu, oracle, band, cols, monkeypatch):
     """nw16_kernel.hip's two passes (emulated): the score-only sweep with
     checkpoints, then the traceback band restored per half from its own
     checkpoint.  Records long enough that the band starts past row 1; small
@@ -159,6 +162,7 @@ def test_emulated_two_pass_band(emu, oracle, band, monkeypatch):
             y = acgt[rng.integers(0, 4, yl)]
         X.append(x.tobytes()); Y.append(y.tobytes())
     monkeypatch.setenv("IMSAME_NW_BAND", band)
+    monkeypatch.setenv("IMSAME_NW_K", cols)
     redo = emu.lib.emu_redo_count
     redo.restype = C.c_uint32
     redo()
