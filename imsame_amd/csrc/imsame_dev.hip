@@ -270,6 +270,9 @@ struct imsame_ctx {
     hipStream_t stream = nullptr;
     hipStream_t ustream = nullptr;    // query uploads (imsame_dev_set_query_range_async)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // round 1b (align_one): a second stream and event pair, created on first use
+    hipStream_t stream_b = nullptr;
+    hipEvent_t evb0 = nullptr, evb1 = nullptr;
     // database + index
     DBuf db, db_start, off, ent, brk, codes, fill, big;
     uint64_t n_db = 0, db_len = 0, n_ent = 0;
@@ -295,7 +298,7 @@ struct imsame_ctx {
     std::vector<uint64_t> q_part_end;
     bool q_len_mult = false;         // every read length is a multiple of NW16_K
     // per-read state
-    DBuf res, cur_p, cur_h, memo, nmemo, rstat, act0, act1, cbase, ccnt, perr;
+    DBuf res, cur_p, cur_h, memo, nmemo, rstat, act0, act1, act2, cbase, ccnt, perr;
     // candidates
     DBuf cread, csid, cread2, csid2, cout, cout2;
     DBuf crow, cperm, rhist;          // predicted rows of class-0 candidates, their launch order
@@ -368,8 +371,9 @@ static inline const uint64_t *dev_qs(const imsame_ctx *c) {
 #define QPAD 64
 
 // counters block layout (u64 slots)
-enum { C_NCAND = 0, C_NCAND2, C_NNEXT, C_WORK, C_WORK2, C_PATHS, C_FLAGS, C_ERR, C_HITS, C_CELLS, C_NACC, C_REDO,
-       C_PROF, C_WIN = C_PROF + 5, C_NSLOTS };
+enum { C_NCAND = 0, C_NCAND2, C_NNEXT, C_NCANDB, C_NCAND2B, C_NNEXT2, C_WORKB,   // (round 1b: B, 2)
+       C_WORK, C_WORK2, C_PATHS, C_FLAGS, C_ERR, C_HITS, C_CELLS, C_NACC, C_REDO,
+       C_PROF, C_WIN = C_PROF + 5, C_DBG, C_NSLOTS = C_DBG + 8 };
 
 static double now_ms() {
     struct timespec ts; clock_gettime(CLOCK_MONOTONIC, &ts);
@@ -486,10 +490,13 @@ extern "C" void imsame_dev_close(imsame_ctx *c) {
                     &c->act1, &c->cread, &c->csid, &c->cread2, &c->csid2, &c->cout, &c->cout2, &c->ctr,
                     &c->minraw, &c->minlen, &c->minident, &c->tb, &c->bnd, &c->paths, &c->ck, &c->rc_in, &c->rc_out,
                     &c->rc_a, &c->rc_b, &c->rc_c, &c->cbase, &c->ccnt, &c->perr, &c->wcap, &c->wout, &c->wstart,
-                    &c->crow, &c->cperm, &c->rhist};
+                    &c->crow, &c->cperm, &c->rhist, &c->act2, &c->slotbits};
     for (DBuf *b : bufs) b->release();
     (void)hipEventDestroy(c->ev0);
     (void)hipEventDestroy(c->ev1);
+    if (c->evb0) (void)hipEventDestroy(c->evb0);
+    if (c->evb1) (void)hipEventDestroy(c->evb1);
+    if (c->stream_b) (void)hipStreamDestroy(c->stream_b);
     if (c->origin && !c->is_sub) (void)hipEventDestroy(c->origin);     // a lane borrows its parent's
     if (!c->is_sub)
         for (hipEvent_t e : c->q_part_ev) (void)hipEventDestroy(e);
@@ -926,9 +933,29 @@ static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, 
     // residency, so per_cu is the true occupancy here.
     pl->np = pl->pk && rounds && nw_xcc_check(c);
     if (!pl->np) per_cu = std::min(per_cu, 8);
+    int part_cu = per_cu;                   // np: blocks per CU the XCD partitions hold
+    if (pl->np) {
+        // One slot layout for both column forms: round 1b runs two packed
+        // launches of a lane at once (align_one), possibly of different
+        // forms, on one arena and bitmap.  Strides of the larger form;
+        // partitions for the larger residency without LDS (LDS only lowers it).
+        const NwShape so = nw16_shape(ymax, xcap, pl->k == NW16_K ? NW16_K5 : NW16_K);
+        pl->tb_dw = std::max(pl->tb_dw, nw16_tb_words(so));
+        if (pl->two) pl->ck_dw = std::max(pl->ck_dw, nw16_ck_words(so));
+        pl->bnd_dw = std::max<uint64_t>(pl->bnd_dw, 3ull * so.xcap);
+        int a10 = 0, a5 = 0;
+        if (pl->two) {
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&a10, nw16_kernel<NW16_K, false, true>, wpb * 64, 0);
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&a5, nw16_kernel<NW16_K5, false, true>, wpb * 64, 0);
+        } else {
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&a10, nw16_kernel<NW16_K, false, false>, wpb * 64, 0);
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&a5, nw16_kernel<NW16_K5, false, false>, wpb * 64, 0);
+        }
+        part_cu = std::max(per_cu, std::max(a10, a5));
+    }
     const uint32_t cpw = pl->pk ? 2 * pl->GPW : pl->GPW;            // candidates per wave pull
     const uint64_t waves_needed = (ncand + cpw - 1) / cpw;
-    pl->slot_words = (uint32_t)((((uint64_t)c->ncu / 8) * per_cu * wpb + 31) / 32);
+    pl->slot_words = (uint32_t)((((uint64_t)c->ncu / 8) * part_cu * wpb + 31) / 32);
     pl->blocks = (unsigned)std::max<uint64_t>(1, pl->np ? (waves_needed + wpb - 1) / wpb
                                                          : std::min<uint64_t>((uint64_t)c->ncu * per_cu, (waves_needed + wpb - 1) / wpb));
     // Traceback arena: one slot per resident wave.  Long reads against long
@@ -963,11 +990,32 @@ static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, 
     return 0;
 }
 
+// end of an NW launch enqueued by launch_nw on queue qi: its duration and
+// its interval on the call's common clock
+static int nw_launch_done(imsame_ctx *c, int qi, uint32_t n, double *ms) {
+    hipEvent_t e0 = qi ? c->evb0 : c->ev0, e1 = qi ? c->evb1 : c->ev1;
+    HIPCHK(hipEventSynchronize(e1));
+    float f = 0;
+    HIPCHK(hipEventElapsedTime(&f, e0, e1));
+    *ms = f;
+    if (c->origin) {
+        float a = 0, b = 0;
+        if (hipEventElapsedTime(&a, c->origin, e0) == hipSuccess && hipEventElapsedTime(&b, c->origin, e1) == hipSuccess) {
+            c->nw_iv.push_back({a, b});
+            if (timeline_on()) c->tl.push_back({'N', c->cur_round, n, a, b});
+        }
+    }
+    return 0;
+}
+
 static int launch_nw(imsame_ctx *c, NwPlan &pl, const uint32_t *cread, const uint32_t *csid, uint32_t n,
                      imsame_read_result *outp, int64_t ig, int64_t eg, const imsame_params *p, uint32_t ymax,
                      uint32_t xmax, uint32_t *work, const uint8_t *dbp, const uint64_t *dbs, const uint8_t *qp,
-                     const uint64_t *qs, uint32_t paths_cap, double *ms, const int32_t *crow = nullptr) {
-    hipStream_t s = c->stream;
+                     const uint64_t *qs, uint32_t paths_cap, double *ms, const int32_t *crow = nullptr, int qi = 0,
+                     bool wait = true) {
+    // qi 1: round 1b's stream; wait false: enqueue only (nw_launch_done)
+    hipStream_t s = qi ? c->stream_b : c->stream;
+    hipEvent_t e0 = qi ? c->evb0 : c->ev0, e1 = qi ? c->evb1 : c->ev1;
     const uint64_t tb_dw = pl.tb_dw;
     // fewer resident waves if the arena cannot be had (the queue still drains)
     const uint64_t per_slot = tb_dw * 4, bnd_slot = pl.bnd_dw * 4, ck_slot = pl.ck_dw * 4;
@@ -1018,7 +1066,7 @@ static int launch_nw(imsame_ctx *c, NwPlan &pl, const uint32_t *cread, const uin
     P.prof = getenv("IMSAME_NW_PROF") ? (unsigned long long *)(ctr + C_PROF) : nullptr;
     P.slot_bits = pl.np ? c->slotbits.as<uint32_t>() : nullptr; P.slot_words = pl.slot_words;
     HIPCHK(hipMemsetAsync(work, 0, 4, s));
-    HIPCHK(hipEventRecord(c->ev0, s));           // the launch's time includes its ordering
+    HIPCHK(hipEventRecord(e0, s));               // the launch's time includes its ordering
     if (crow && pl.two && n >= 64) {
         // queue order by predicted row (first-sweep traceback windows)
         const uint32_t nb = ((uint32_t)pl.xcap + 512) / 8 + 2;
@@ -1047,22 +1095,10 @@ static int launch_nw(imsame_ctx *c, NwPlan &pl, const uint32_t *cread, const uin
     else if (pl.pk)                    nw16_kernel<NW16_K, false, false><<<pl.blocks, 256, pl.lds, s>>>(P);
     else if (pl.nstr > 1) nw_kernel<true><<<pl.blocks, 256, pl.lds, s>>>(P);
     else                  nw_kernel<false><<<pl.blocks, 256, pl.lds, s>>>(P);
-    HIPCHK(hipEventRecord(c->ev1, s));
+    HIPCHK(hipEventRecord(e1, s));
     HIPCHK(hipGetLastError());
     POISON_SYNC(s, pl.pk ? "nw16_kernel" : pl.lng ? "nwl_kernel" : "nw_kernel", c);
-    HIPCHK(hipEventSynchronize(c->ev1));
-    float f = 0;
-    HIPCHK(hipEventElapsedTime(&f, c->ev0, c->ev1));
-    *ms = f;
-    if (c->origin) {                             // interval on the call's common clock
-        float a = 0, b = 0;
-        if (hipEventElapsedTime(&a, c->origin, c->ev0) == hipSuccess &&
-            hipEventElapsedTime(&b, c->origin, c->ev1) == hipSuccess) {
-            c->nw_iv.push_back({a, b});
-            if (timeline_on()) c->tl.push_back({'N', c->cur_round, n, a, b});
-        }
-    }
-    return 0;
+    return wait ? nw_launch_done(c, qi, n, ms) : 0;
 }
 
 static int paths_setup(imsame_ctx *c, const imsame_params *p, uint64_t paths_cap, uint32_t *cap32) {
@@ -1191,13 +1227,14 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
                                              std::min<uint64_t>((uint64_t)n * SPEC_MAX, 1u << 20));
     if (c->res.ensure((uint64_t)n * 64) || c->cur_p.ensure((uint64_t)n * 8) || c->cur_h.ensure((uint64_t)n * 4) ||
         c->memo.ensure((uint64_t)n * 4 * MEMO) || c->nmemo.ensure(n) || c->rstat.ensure(n) ||
-        c->act0.ensure((uint64_t)n * 4) || c->act1.ensure((uint64_t)n * 4) || c->cread.ensure(ccap * 4) ||
+        c->act0.ensure((uint64_t)n * 4) || c->act1.ensure((uint64_t)n * 4) || c->act2.ensure((uint64_t)n * 4) ||
+        c->cread.ensure(ccap * 4) ||
         c->csid.ensure(ccap * 4) || c->cread2.ensure(ccap * 4) || c->csid2.ensure(ccap * 4) ||
         c->cout.ensure(ccap * 64) || c->cout2.ensure(ccap * 64) || c->cbase.ensure((uint64_t)n * 4) ||
         c->ccnt.ensure((uint64_t)n * 4) || c->perr.ensure((uint64_t)n * 4) || c->crow.ensure(ccap * 4))
         return IMSAME_E_OOM;
     if (poison_on()) {                        // this call's scratch holds nothing it may read
-        const DBuf *scr[] = {&c->res, &c->cur_p, &c->cur_h, &c->memo, &c->nmemo, &c->rstat, &c->act0, &c->act1,
+        const DBuf *scr[] = {&c->res, &c->cur_p, &c->cur_h, &c->memo, &c->nmemo, &c->rstat, &c->act0, &c->act1, &c->act2,
                              &c->cread, &c->csid, &c->cread2, &c->csid2, &c->cout, &c->cout2, &c->cbase, &c->ccnt,
                              &c->perr, &c->crow, &c->cperm, &c->rhist, &c->paths, &c->tb, &c->ck, &c->bnd};
         for (const DBuf *b : scr)
@@ -1236,6 +1273,8 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     st.ms_setup = now_ms() - t_start;
 
     const uint32_t short_y = std::min<uint32_t>(ycap, NW_W / 2);
+    const char *r1b_env = getenv("IMSAME_ROUND1B");
+    const bool r1b_on = !(r1b_env && !atoi(r1b_env)) && ycap <= short_y && !crow && !poison_on();
     uint32_t nact = n;
     uint32_t *act = c->act0.as<uint32_t>(), *nxt = c->act1.as<uint32_t>();
     while (nact) {
@@ -1265,6 +1304,8 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         S.crow = crow;
         S.cread2 = c->cread2.as<uint32_t>(); S.csid2 = c->csid2.as<uint32_t>(); S.ncand2 = (uint32_t *)(ctr + C_NCAND2);
         S.err = (unsigned long long *)(ctr + C_ERR); S.nhits = (unsigned long long *)(ctr + C_HITS);
+        S.dbg = getenv("IMSAME_DEBUG_ROUNDS") ? (unsigned long long *)(ctr + C_DBG) : nullptr;
+        if (S.dbg) HIPCHK(hipMemsetAsync(S.dbg, 0, 8 * 8, s));
         S.wcap = c->use_wcap ? c->wcap.as<uint64_t>() : nullptr;
         S.wstart = c->use_wstart ? c->wstart.as<uint64_t>() : nullptr;
         S.minlen = c->minlen.as<uint32_t>(); S.n_minlen = ymax + 1;
@@ -1274,29 +1315,148 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         // times the call's lanes (C2, 8 lanes of 125k: 4 lanes per read in
         // round 1 instead of 16, whose extra windows a true read never needs;
         // +1.9 %, profiles/r2am_*)
-        const int L = l_env ? atoi(l_env) : seed_lanes((uint32_t)std::min<uint64_t>((uint64_t)nact * c->nlanes, 0xFFFFFFFFu));
-        const size_t slds = 256 * SEED_LDS_PER_LANE;
-        HIPCHK(hipEventRecord(c->ev0, s));
-        if (L >= 16)     seed_group_kernel<16><<<nblk((uint64_t)nact * 16, 256), 256, slds, s>>>(S);
-        else if (L >= 4) seed_group_kernel<4><<<nblk((uint64_t)nact * 4, 256), 256, slds, s>>>(S);
-        else if (L >= 2) seed_group_kernel<2><<<nblk((uint64_t)nact * 2, 256), 256, slds, s>>>(S);
-        else             seed_kernel<<<nblk(nact, 256), 256, 0, s>>>(S);
-        POISON_SYNC(s, "seed kernel", c);
-        HIPCHK(hipEventRecord(c->ev1, s));
-        HIPCHK(hipGetLastError());
+        auto seed_launch = [&](const SeedLaunch &SL, uint32_t na, hipStream_t ss, hipEvent_t e0, hipEvent_t e1) -> int {
+            const int L = l_env ? atoi(l_env) : seed_lanes((uint32_t)std::min<uint64_t>((uint64_t)na * c->nlanes, 0xFFFFFFFFu));
+            const size_t slds = 256 * SEED_LDS_PER_LANE;
+            HIPCHK(hipEventRecord(e0, ss));
+            if (L >= 16)     seed_group_kernel<16><<<nblk((uint64_t)na * 16, 256), 256, slds, ss>>>(SL);
+            else if (L >= 4) seed_group_kernel<4><<<nblk((uint64_t)na * 4, 256), 256, slds, ss>>>(SL);
+            else if (L >= 2) seed_group_kernel<2><<<nblk((uint64_t)na * 2, 256), 256, slds, ss>>>(SL);
+            else             seed_kernel<<<nblk(na, 256), 256, 0, ss>>>(SL);
+            POISON_SYNC(ss, "seed kernel", c);
+            HIPCHK(hipEventRecord(e1, ss));
+            HIPCHK(hipGetLastError());
+            return 0;
+        };
+        auto seed_time = [&](hipEvent_t e0, hipEvent_t e1, uint32_t na) -> int {
+            float fs = 0;
+            HIPCHK(hipEventElapsedTime(&fs, e0, e1));
+            st.ms_seed += fs;
+            if (c->origin && timeline_on()) {
+                float a = 0;
+                if (hipEventElapsedTime(&a, c->origin, e0) == hipSuccess)
+                    c->tl.push_back({'S', (int)st.rounds, na, a, a + fs});
+            }
+            return 0;
+        };
+        auto rec_launch = [&](const NwPlan &pl, uint32_t nc, double ms) {
+            if (st.nw_launches < IMSAME_LAUNCH_STATS) {
+                st.launch_cand[st.nw_launches] = nc;
+                st.launch_ms[st.nw_launches] = ms;
+                if (pl.pk) st.launch_pk |= 1ull << st.nw_launches;
+                if (pl.pk && pl.k == NW16_K5) st.launch_k5 |= 1ull << st.nw_launches;
+                if (pl.np) st.launch_np |= 1ull << st.nw_launches;
+            }
+            st.ms_nw += ms; st.nw_launches++; st.n_nw += nc;
+        };
+        auto upd_launch = [&](const uint32_t *cr, const uint32_t *cs, uint32_t nc, const imsame_read_result *o,
+                              uint32_t *next, int nnext_slot, hipStream_t ss) -> int {
+            UpdLaunch U = {cr, cs, nc, o, read_from, c->res.as<imsame_read_result>(),
+                           c->rstat.as<uint8_t>(), c->memo.as<uint32_t>(), c->nmemo.as<uint8_t>(),
+                           c->cbase.as<uint32_t>(), c->ccnt.as<uint32_t>(), c->perr.as<uint32_t>(),
+                           c->cur_p.as<uint64_t>(), next,
+                           (uint32_t *)(ctr + nnext_slot), (unsigned long long *)(ctr + C_CELLS),
+                           (unsigned long long *)(ctr + C_NACC), (unsigned long long *)(ctr + C_ERR),
+                           c->db_start.as<uint64_t>()};
+            update_kernel<<<nblk(nc, 256), 256, 0, ss>>>(U);
+            POISON_SYNC(ss, "update_kernel", c);
+            HIPCHK(hipGetLastError());
+            return 0;
+        };
+        if ((rc = seed_launch(S, nact, s, c->ev0, c->ev1))) return rc;
         uint64_t hc[3];
         HIPCHK(hipMemcpyAsync(hc, ctr + C_NCAND, 24, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
-        float fs = 0;
-        HIPCHK(hipEventElapsedTime(&fs, c->ev0, c->ev1));
-        st.ms_seed += fs;
-        if (c->origin && timeline_on()) {
-            float a = 0;
-            if (hipEventElapsedTime(&a, c->origin, c->ev0) == hipSuccess)
-                c->tl.push_back({'S', (int)st.rounds, nact, a, a + fs});
-        }
+        if ((rc = seed_time(c->ev0, c->ev1, nact))) return rc;
         const uint32_t n1 = (uint32_t)hc[0], n2 = (uint32_t)hc[1];
         if (n1 + n2 + hc[2] == 0) break;                          // no candidates, nobody paused
+        // Round 1b.  Reads that paused in round 1 without a candidate (budget
+        // spent: at C2 the 10 % random reads, which scan every window) need
+        // none of round 1's NW results, so their scan goes on at once on a
+        // second stream, with speculation from a weak first pass, while the
+        // round-1 NW launch runs; their candidates' NW launch joins it on
+        // the chip.  Round 2 then holds the reads whose round-1 candidates
+        // were rejected and the few the 1b scan paused (C2 shard 1/8: ~70 per
+        // lane instead of ~6.3k, profiles/r3*).  Same visiting order per read,
+        // so the same results (tests).  Short reads, both NW launches
+        // non-persistent (they share the arena and its slot bitmap);
+        // IMSAME_ROUND1B=0 turns it off.
+        NwPlan pla;
+        bool r1b = st.rounds == 1 && r1b_on && hc[2] > 0 && n2 == 0 && ccap > n1;
+        if (r1b && n1 && (rc = plan_nw(c, short_y, xcap, n1, p, c->q_len_mult, &pla))) return rc;
+        if (r1b && n1 && !pla.np) r1b = false;
+        if (r1b) {
+            if (!c->stream_b) {
+                HIPCHK(hipStreamCreateWithFlags(&c->stream_b, hipStreamNonBlocking));
+                HIPCHK(hipEventCreate(&c->evb0));
+                HIPCHK(hipEventCreate(&c->evb1));
+            }
+            hipStream_t sb = c->stream_b;
+            uint32_t *act2 = c->act2.as<uint32_t>();
+            const uint32_t npz = (uint32_t)hc[2];
+            SeedLaunch Sb = S;
+            Sb.active = nxt; Sb.n_active = npz;
+            Sb.spec = 1;
+            Sb.spec_weak = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(SPEC_MAX, (ccap - n1) / npz));
+            Sb.budget = seed_budget(budget1, 2, grow);
+            Sb.next = act2; Sb.nnext = (uint32_t *)(ctr + C_NNEXT2);
+            Sb.cread = c->cread.as<uint32_t>() + n1; Sb.csid = c->csid.as<uint32_t>() + n1;
+            Sb.ncand = (uint32_t *)(ctr + C_NCANDB); Sb.crow = nullptr;
+            Sb.ncand2 = (uint32_t *)(ctr + C_NCAND2B);
+            Sb.dbg = nullptr;
+            HIPCHK(hipMemsetAsync(ctr + C_NCANDB, 0, 3 * 8, sb));     // NCANDB, NCAND2B, NNEXT2
+            if ((rc = seed_launch(Sb, npz, sb, c->evb0, c->evb1))) return rc;
+            double msa = 0, msb = 0;
+            if (n1) {
+                rc = launch_nw(c, pla, c->cread.as<uint32_t>(), c->csid.as<uint32_t>(), n1, c->cout.as<imsame_read_result>(),
+                               p->igap, p->egap, p, ymax, xcap, (uint32_t *)(ctr + C_WORK), c->db.as<uint8_t>(),
+                               c->db_start.as<uint64_t>(), qd, qsd, pcap, &msa, nullptr, 0, false);
+                if (rc) return rc;
+                if ((rc = upd_launch(c->cread.as<uint32_t>(), c->csid.as<uint32_t>(), n1, c->cout.as<imsame_read_result>(),
+                                     act2, C_NNEXT2, s))) return rc;
+            }
+            uint64_t hb[2];
+            HIPCHK(hipMemcpyAsync(hb, ctr + C_NCANDB, 16, hipMemcpyDeviceToHost, sb));
+            HIPCHK(hipStreamSynchronize(sb));                         // the 1b scan only: N1a runs on
+            if ((rc = seed_time(c->evb0, c->evb1, npz))) return rc;
+            const uint32_t nb = (uint32_t)hb[0];
+            if (hb[1]) return IMSAME_E_STATE;                         // short reads only: cannot happen
+            NwPlan plb;
+            bool a_done = n1 == 0;
+            if (nb) {
+                if ((rc = plan_nw(c, short_y, xcap, nb, p, c->q_len_mult, &plb))) return rc;
+                if (!plb.np && !a_done) {                             // its slots are not N1a's: after it
+                    if ((rc = nw_launch_done(c, 0, n1, &msa))) return rc;
+                    rec_launch(pla, n1, msa);
+                    a_done = true;
+                }
+                rc = launch_nw(c, plb, c->cread.as<uint32_t>() + n1, c->csid.as<uint32_t>() + n1, nb,
+                               c->cout.as<imsame_read_result>() + n1, p->igap, p->egap, p, ymax, xcap,
+                               (uint32_t *)(ctr + C_WORKB), c->db.as<uint8_t>(), c->db_start.as<uint64_t>(), qd, qsd,
+                               pcap, &msb, nullptr, 1, false);
+                if (rc) return rc;
+                if ((rc = upd_launch(c->cread.as<uint32_t>() + n1, c->csid.as<uint32_t>() + n1, nb,
+                                     c->cout.as<imsame_read_result>() + n1, act2, C_NNEXT2, sb))) return rc;
+            }
+            if (!a_done) {
+                if ((rc = nw_launch_done(c, 0, n1, &msa))) return rc;
+                rec_launch(pla, n1, msa);
+            }
+            if (nb) {
+                if ((rc = nw_launch_done(c, 1, nb, &msb))) return rc;
+                rec_launch(plb, nb, msb);
+            }
+            HIPCHK(hipStreamSynchronize(sb));
+            uint64_t nn = 0;
+            HIPCHK(hipMemcpyAsync(&nn, ctr + C_NNEXT2, 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            if (getenv("IMSAME_DEBUG_ROUNDS"))
+                fprintf(stderr, "[round 1b] paused=%u spec_weak=%u budget=%u cand=%u+%u next=%llu\n", npz, Sb.spec_weak,
+                        Sb.budget, n1, nb, (unsigned long long)nn);
+            nact = (uint32_t)nn;
+            nxt = act; act = act2;                                    // round 2 scans act2; act0 is free
+            continue;
+        }
         struct Cls { uint32_t n; uint32_t *cr, *cs; imsame_read_result *o; uint32_t ylim; int work; };
         Cls cls[2] = {{n1, c->cread.as<uint32_t>(), c->csid.as<uint32_t>(), c->cout.as<imsame_read_result>(), short_y, C_WORK},
                       {n2, c->cread2.as<uint32_t>(), c->csid2.as<uint32_t>(), c->cout2.as<imsame_read_result>(), ycap, C_WORK2}};
@@ -1309,24 +1469,8 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
                            (uint32_t *)(ctr + cls[k].work), c->db.as<uint8_t>(), c->db_start.as<uint64_t>(), qd, qsd,
                            pcap, &ms, k == 0 ? crow : nullptr);
             if (rc) return rc;
-            if (st.nw_launches < IMSAME_LAUNCH_STATS) {
-                st.launch_cand[st.nw_launches] = cls[k].n;
-                st.launch_ms[st.nw_launches] = ms;
-                if (pl.pk) st.launch_pk |= 1ull << st.nw_launches;
-                if (pl.pk && pl.k == NW16_K5) st.launch_k5 |= 1ull << st.nw_launches;
-                if (pl.np) st.launch_np |= 1ull << st.nw_launches;
-            }
-            st.ms_nw += ms; st.nw_launches++; st.n_nw += cls[k].n;
-            UpdLaunch U = {cls[k].cr, cls[k].cs, cls[k].n, cls[k].o, read_from, c->res.as<imsame_read_result>(),
-                           c->rstat.as<uint8_t>(), c->memo.as<uint32_t>(), c->nmemo.as<uint8_t>(),
-                           c->cbase.as<uint32_t>(), c->ccnt.as<uint32_t>(), c->perr.as<uint32_t>(),
-                           c->cur_p.as<uint64_t>(), nxt,
-                           (uint32_t *)(ctr + C_NNEXT), (unsigned long long *)(ctr + C_CELLS),
-                           (unsigned long long *)(ctr + C_NACC), (unsigned long long *)(ctr + C_ERR),
-                           c->db_start.as<uint64_t>()};
-            update_kernel<<<nblk(cls[k].n, 256), 256, 0, s>>>(U);
-            POISON_SYNC(s, "update_kernel", c);
-            HIPCHK(hipGetLastError());
+            rec_launch(pl, cls[k].n, ms);
+            if ((rc = upd_launch(cls[k].cr, cls[k].cs, cls[k].n, cls[k].o, nxt, C_NNEXT, s))) return rc;
         }
         uint64_t nn = 0;
         HIPCHK(hipMemcpyAsync(&nn, ctr + C_NNEXT, 8, hipMemcpyDeviceToHost, s));
@@ -1338,8 +1482,15 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
                 HIPCHK(hipMemcpy(o.data(), c->cout.p, o.size() * 64, hipMemcpyDeviceToHost));
                 HIPCHK(hipMemcpy(cr.data(), c->cread.p, o.size() * 4, hipMemcpyDeviceToHost));
             }
-            fprintf(stderr, "[round %llu] active=%u spec=%u cand=%u+%u next=%llu seed_ms=%.3f |",
-                    (unsigned long long)st.rounds, nact, S.spec, n1, n2, (unsigned long long)nn, fs);
+            uint64_t dg[8], nacc = 0;
+            HIPCHK(hipMemcpy(dg, ctr + C_DBG, sizeof dg, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(&nacc, ctr + C_NACC, 8, hipMemcpyDeviceToHost));
+            fprintf(stderr, "[round %llu] active=%u spec=%u budget=%u cand=%u+%u next=%llu acc_total=%llu "
+                    "outcomes(err0 pause0 done0 err pause exh full)=%llu %llu %llu %llu %llu %llu %llu |",
+                    (unsigned long long)st.rounds, nact, S.spec, S.budget, n1, n2, (unsigned long long)nn,
+                    (unsigned long long)nacc, (unsigned long long)dg[0], (unsigned long long)dg[1],
+                    (unsigned long long)dg[2], (unsigned long long)dg[3], (unsigned long long)dg[4],
+                    (unsigned long long)dg[5], (unsigned long long)dg[6]);
             for (size_t k = 0; k < o.size(); ++k)
                 fprintf(stderr, " r%u/s%llu st%u len%u id%u y%u", cr[k], (unsigned long long)o[k].db_seq, o[k].status,
                         o[k].length, o[k].identities, o[k].ylen);

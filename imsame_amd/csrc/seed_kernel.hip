@@ -50,7 +50,18 @@ struct SeedLaunch {
     uint32_t *cread2, *csid2, *ncand2;     // class 1: longer reads
     unsigned long long *err;               // min (read << 32 | record)
     unsigned long long *nhits;
+    unsigned long long *dbg;               // diagnostics (IMSAME_DEBUG_ROUNDS): reads per scan outcome
+                                           // (seed_outcome), NULL: off
 };
+// scan outcome classes of a read (diagnostics): no candidate + size error /
+// paused / done; candidates + size error / paused / exhausted / spec full
+#ifndef IMSAME_WAVE_EMU
+__device__ __forceinline__ void seed_outcome(const SeedLaunch &S, uint32_t ne, bool perr, bool paused, bool exh) {
+    if (!S.dbg) return;
+    const int c = ne == 0 ? (perr ? 0 : paused ? 1 : 2) : (perr ? 3 : paused ? 4 : exh ? 5 : 6);
+    atomicAdd(S.dbg + c, 1ull);
+}
+#endif
 #define SPEC_MAX 8
 // speculation width from a weak first candidate on (spec_after_first); 1 = off
 #ifndef SPEC_WEAK
@@ -291,6 +302,9 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint
         }
         if (stop) break;
     }
+#ifndef IMSAME_WAVE_EMU
+    seed_outcome(S, ne, perr != 0, paused, ne < spec && !perr && !paused);
+#endif
     if (ne == 0) {
         if (perr) {
             S.rstat[k] = RS_ERROR;
@@ -464,6 +478,9 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
         wv_lds_sync();                                    // lists read before the next scan rewrites them
     }
     if (!gvalid || wl != 0) return;
+#ifndef IMSAME_WAVE_EMU
+    seed_outcome(S, ne, perr != 0, paused, exhausted);
+#endif
     if (ne == 0) {
         if (perr) {
             S.rstat[k] = RS_ERROR;

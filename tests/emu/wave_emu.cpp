@@ -47,6 +47,9 @@ static void run_wave(const std::function<void(int)> &f) {
 // waves whose nw16 traceback band missed a path (NwLaunch::redo), since the last emu_redo_count()
 static uint32_t g_redo;
 extern "C" uint32_t emu_redo_count(void) { const uint32_t r = g_redo; g_redo = 0; return r; }
+// reads the round-1b scan took over (imsame_dev.hip:align_one), since the last emu_r1b_count()
+static uint32_t g_r1b;
+extern "C" uint32_t emu_r1b_count(void) { const uint32_t r = g_r1b; g_r1b = 0; return r; }
 // candidates walked inside their first-sweep traceback window (NwLaunch::win), since the last call
 static uint32_t g_win;
 extern "C" uint32_t emu_win_count(void) { const uint32_t r = g_win; g_win = 0; return r; }
@@ -236,7 +239,7 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
     const uint32_t spec_weak = (uint32_t)std::max(1, std::min(SPEC_MAX, sw_env ? atoi(sw_env) : SPEC_WEAK));
     const size_t ccap = std::max<size_t>((size_t)n * (spec_weak > 1 ? spec_weak + 1 : 2),
                                          std::min<size_t>((size_t)n * SPEC_MAX, 1u << 20));
-    std::vector<uint32_t> cur_h(n), memo((size_t)n * MEMO), act(n), nxt(n), cr(ccap), cs(ccap), cr2(ccap), cs2(ccap);
+    std::vector<uint32_t> cur_h(n), memo((size_t)n * MEMO), act(n), nxt(n), act2(n), cr(ccap), cs(ccap), cr2(ccap), cs2(ccap);
     std::vector<uint32_t> cbase(n), ccnt(n), perr(n);
     std::vector<int32_t> crow(ccap);
     const char *win_env = getenv("IMSAME_NW_WINDOW");
@@ -256,6 +259,8 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
     uint32_t nc[3] = {0, 0, 0}, pused = 0, flags = 0;
     unsigned long long err = ~0ull, nhits = 0, cells = 0, nacc = 0;
     const uint32_t short_y = std::min<uint32_t>(ycap, NW_W / 2);
+    const char *r1b_env = getenv("IMSAME_ROUND1B");
+    const bool r1b_on = !(r1b_env && !atoi(r1b_env)) && ycap <= short_y && !crowp;
     uint32_t nact = n;
     imsame_stats st;
     memset(&st, 0, sizeof st);
@@ -285,35 +290,64 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
         S.cread2 = cr2.data(); S.csid2 = cs2.data(); S.ncand2 = &nc[1];
         S.err = &err; S.nhits = &nhits;
         const char *l_env = getenv("IMSAME_SEED_L");
-        const int L = l_env ? atoi(l_env) : seed_lanes(nact);
-        if (L <= 1) {
-            for (uint32_t i = 0; i < nact; ++i) { uint64_t h = 0; seed_one(S, i, h); nhits += h; }
-        } else {                   // seed_group_kernel: one 64-lane wave at a time
-            std::vector<uint2> lds(64 * SPEC_MAX);
-            std::atomic<unsigned long long> wh{0};
-            for (uint64_t w0 = 0; w0 < (uint64_t)nact * L; w0 += 64)
-                run_wave([&](int lane) {
-                    uint64_t h = 0;
-                    const uint32_t gidx = (uint32_t)((w0 + lane) / L);
-                    if (L == 16) seed_group<16>(S, gidx, lane % 16, lane, lds.data() + lane * SPEC_MAX, h);
-                    else         seed_group<4>(S, gidx, lane % 4, lane, lds.data() + lane * SPEC_MAX, h);
-                    wh += h;
-                });
-            nhits += wh;
-        }
+        auto run_seed = [&](const SeedLaunch &SL, uint32_t na) {
+            const int L = l_env ? atoi(l_env) : seed_lanes(na);
+            if (L <= 1) {
+                for (uint32_t i = 0; i < na; ++i) { uint64_t h = 0; seed_one(SL, i, h); nhits += h; }
+            } else {                   // seed_group_kernel: one 64-lane wave at a time
+                std::vector<uint2> lds(64 * SPEC_MAX);
+                std::atomic<unsigned long long> wh{0};
+                for (uint64_t w0 = 0; w0 < (uint64_t)na * L; w0 += 64)
+                    run_wave([&](int lane) {
+                        uint64_t h = 0;
+                        const uint32_t gidx = (uint32_t)((w0 + lane) / L);
+                        if (L == 16) seed_group<16>(SL, gidx, lane % 16, lane, lds.data() + lane * SPEC_MAX, h);
+                        else         seed_group<4>(SL, gidx, lane % 4, lane, lds.data() + lane * SPEC_MAX, h);
+                        wh += h;
+                    });
+                nhits += wh;
+            }
+        };
+        auto nw_upd = [&](uint32_t *r, uint32_t *s_, uint32_t nc_, imsame_read_result *o, uint32_t y, const int32_t *row,
+                          uint32_t *next, uint32_t *nnext) {
+            run_nw(db, dbs.data(), q, qsv.data(), r, s_, nc_, p, y, xcap, ml, mi, o, paths,
+                   (uint32_t)paths_cap, &pused, &flags, row);
+            st.n_nw += nc_;
+            UpdLaunch U = {r, s_, nc_, o, read_from, res, rstat.data(), memo.data(), nmemo.data(),
+                           cbase.data(), ccnt.data(), perr.data(), cur_p.data(), next, nnext, &cells, &nacc, &err,
+                           dbs.data()};
+            for (uint32_t k = 0; k < nc_; ++k) { uint64_t ce = 0, ac = 0; update_one(U, k, ce, ac); cells += ce; nacc += ac; }
+        };
+        run_seed(S, nact);
         if (nc[0] + nc[1] + nc[2] == 0) break;
+        // round 1b (imsame_dev.hip:align_one): the reads round 1 paused scan on
+        // (weak-first speculation, round 2's budget) before round 1's NW results
+        if (st.rounds == 1 && r1b_on && nc[2] > 0 && nc[1] == 0 && ccap > nc[0]) {
+            const uint32_t n1 = nc[0], npz = nc[2];
+            uint32_t nb[3] = {0, 0, 0};
+            SeedLaunch Sb = S;
+            Sb.active = nxt.data(); Sb.n_active = npz;
+            Sb.spec = 1;
+            Sb.spec_weak = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(SPEC_MAX, (ccap - n1) / npz));
+            Sb.budget = seed_budget(budget1, 2);
+            Sb.next = act2.data(); Sb.nnext = &nb[2];
+            Sb.cread = cr.data() + n1; Sb.csid = cs.data() + n1; Sb.ncand = &nb[0]; Sb.crow = nullptr;
+            Sb.ncand2 = &nb[1];
+            run_seed(Sb, npz);
+            if (nb[1]) return IMSAME_E_STATE;
+            if (n1) nw_upd(cr.data(), cs.data(), n1, o1.data(), short_y, nullptr, act2.data(), &nb[2]);
+            if (nb[0]) nw_upd(cr.data() + n1, cs.data() + n1, nb[0], o1.data() + n1, short_y, nullptr, act2.data(), &nb[2]);
+            g_r1b += npz;
+            if (getenv("IMSAME_DEBUG_ROUNDS"))
+                fprintf(stderr, "[emu round 1b] paused=%u cand=%u+%u next=%u\n", npz, n1, nb[0], nb[2]);
+            nact = nb[2];
+            std::swap(act, act2);
+            continue;
+        }
         struct { uint32_t n; uint32_t *r, *s; imsame_read_result *o; uint32_t y; const int32_t *row; } cls[2] = {
             {nc[0], cr.data(), cs.data(), o1.data(), short_y, crowp}, {nc[1], cr2.data(), cs2.data(), o2.data(), ycap, nullptr}};
-        for (auto &c : cls) {
-            if (!c.n) continue;
-            run_nw(db, dbs.data(), q, qsv.data(), c.r, c.s, c.n, p, c.y, xcap, ml, mi, c.o, paths,
-                   (uint32_t)paths_cap, &pused, &flags, c.row);
-            st.n_nw += c.n;
-            UpdLaunch U = {c.r, c.s, c.n, c.o, read_from, res, rstat.data(), memo.data(), nmemo.data(),
-                           cbase.data(), ccnt.data(), perr.data(), cur_p.data(), nxt.data(), &nc[2], &cells, &nacc, &err,
-                           dbs.data()};
-            for (uint32_t k = 0; k < c.n; ++k) { uint64_t ce = 0, ac = 0; update_one(U, k, ce, ac); cells += ce; nacc += ac; }
-        }
+        for (auto &c : cls)
+            if (c.n) nw_upd(c.r, c.s, c.n, c.o, c.y, c.row, nxt.data(), &nc[2]);
         nact = nc[2];
         std::swap(act, nxt);
     }

@@ -221,6 +221,31 @@ def test_emulated_predicted_traceback_window(emu, oracle, seed_l, monkeypatch):
         assert np.array_equal(got0[f], exp[f]), f
 
 
+@pytest.mark.parametrize("r1b", ["1", "0"])
+def test_emulated_round1b(emu, oracle, r1b, monkeypatch):
+    """Round 1b (imsame_dev.hip:align_one): reads that round 1 paused without
+    a candidate (random reads against a 20 Mbp database spend the 32-hit
+    budget) scan on at once with weak-first speculation, before round 1's
+    NW results, on the device's second stream; both NW launches update the
+    same per-read state.  Every field equals the oracle with and without it,
+    and the 1b scan took reads over."""
+    from tests import synth
+    monkeypatch.setenv("IMSAME_ROUND1B", r1b)
+    cnt = emu.lib.emu_r1b_count
+    cnt.restype = C.c_uint32
+    cnt()
+    ref, rst = synth.make_reference_arr(20_000_000, 2_000, seed=5)
+    q, qs = synth.make_reads_arr(ref, 240, 150, seed=6)
+    rc0, exp, _ = oracle.align(ref, rst, q, qs, oracle.params(), 4)
+    assert rc0 == 0
+    rc, got, _, st = emu.align(ref, rst, q, qs, oracle.params(), 4)
+    assert rc == 0
+    for f in PARITY_FIELDS:
+        assert np.array_equal(got[f], exp[f]), f
+    taken = cnt()
+    assert (taken > 0) == (r1b == "1"), taken
+
+
 def _long_pairs(seed, n, ymax, xmax):
     """Long reads (161 .. ymax, strip edges 639-641 included) against records,
     70 % drawn from the record with substitutions and indels, 30 % random."""
