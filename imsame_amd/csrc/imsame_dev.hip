@@ -319,6 +319,7 @@ struct imsame_ctx {
     DBuf slotbits;
     uint32_t slot_words = 0;
     int xcc_ok = -1;
+    int np_part_cu = -1;              // nw16_np_part_cu (-1: not computed)
     uint64_t paths_cap_dev = 0, paths_n = 0;
     double paths_hint = 0;     // path entries per read of the last call
     std::vector<uint32_t> paths_host;
@@ -863,6 +864,27 @@ static bool nw_xcc_check(imsame_ctx *c) {
     return c->xcc_ok == 1;
 }
 
+// Blocks per CU the XCD partitions of a context's slot bitmap hold: the
+// largest residency of any packed variant without LDS (LDS only lowers it),
+// so every non-persistent launch of the context -- and any two running at
+// once, whatever their forms -- numbers its slots the same way.  0: unknown.
+static int nw16_np_part_cu(imsame_ctx *c) {
+    if (c->np_part_cu >= 0) return c->np_part_cu;
+    int m = 0;
+    bool ok = true;
+    auto q = [&](const void *f) {
+        int a = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, f, 256, 0) != hipSuccess || a < 1) ok = false;
+        m = std::max(m, a);
+    };
+    q((const void *)nw16_kernel<NW16_K, false, true>);  q((const void *)nw16_kernel<NW16_K, true, true>);
+    q((const void *)nw16_kernel<NW16_K, false, false>); q((const void *)nw16_kernel<NW16_K, true, false>);
+    q((const void *)nw16_kernel<NW16_K5, false, true>); q((const void *)nw16_kernel<NW16_K5, true, true>);
+    q((const void *)nw16_kernel<NW16_K5, false, false>); q((const void *)nw16_kernel<NW16_K5, true, false>);
+    c->np_part_cu = ok ? m : 0;
+    return c->np_part_cu;
+}
+
 // Columns per lane of a packed launch.  A launch is a queue of tasks (8
 // candidates x all rows at K = 10) pulled by one wave per resident slot
 // (4 per SIMD); a launch of a few slots' worth (a lane's later rounds, every
@@ -871,11 +893,14 @@ static bool nw_xcc_check(imsame_ctx *c) {
 // the columns per step) and doubles their number, for ~8 % more
 // instructions per cell.  Chosen when the launch holds fewer than
 // k5_fill x (the chip's K = 10 slots / the lanes running) tasks.
-// IMSAME_NW_K=5|10 forces one; IMSAME_NW_K5_FILL sets k5_fill.
+// IMSAME_NW_K=5|10 forces one; IMSAME_NW_K5_FILL sets k5_fill, 0 by default:
+// at k5_fill 2 the C2 1/8 shard ran 21.3-21.5 ms against 20.5-20.6 with
+// K = 10 everywhere (profiles/r3o_*: the small launches are not wave-latency
+// bound but share the chip with the other lanes' large ones).
 static int nw16_k(imsame_ctx *c, uint32_t ncand, bool rounds) {
     const char *e = getenv("IMSAME_NW_K"), *fe = getenv("IMSAME_NW_K5_FILL");
     const int force = e ? atoi(e) : 0;
-    const double fill = fe ? atof(fe) : 2.0;
+    const double fill = fe ? atof(fe) : 0.0;      // off: measured slower (profiles/r3o_*)
     if (force == NW16_K5 || force == NW16_K) return force;
     if (!rounds) return NW16_K;
     const double slots = (double)c->ncu * 4.0 * 4.0 / std::max(1, c->nlanes);
@@ -931,7 +956,7 @@ static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, 
     // instead of after its last task (a persistent wave holds its slot until
     // the queue is empty).  The partitions must hold the kernel's full
     // residency, so per_cu is the true occupancy here.
-    pl->np = pl->pk && rounds && nw_xcc_check(c);
+    pl->np = pl->pk && rounds && nw_xcc_check(c) && nw16_np_part_cu(c) > 0;
     if (!pl->np) per_cu = std::min(per_cu, 8);
     int part_cu = per_cu;                   // np: blocks per CU the XCD partitions hold
     if (pl->np) {
@@ -943,15 +968,8 @@ static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, 
         pl->tb_dw = std::max(pl->tb_dw, nw16_tb_words(so));
         if (pl->two) pl->ck_dw = std::max(pl->ck_dw, nw16_ck_words(so));
         pl->bnd_dw = std::max<uint64_t>(pl->bnd_dw, 3ull * so.xcap);
-        int a10 = 0, a5 = 0;
-        if (pl->two) {
-            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&a10, nw16_kernel<NW16_K, false, true>, wpb * 64, 0);
-            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&a5, nw16_kernel<NW16_K5, false, true>, wpb * 64, 0);
-        } else {
-            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&a10, nw16_kernel<NW16_K, false, false>, wpb * 64, 0);
-            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&a5, nw16_kernel<NW16_K5, false, false>, wpb * 64, 0);
-        }
-        part_cu = std::max(per_cu, std::max(a10, a5));
+        part_cu = nw16_np_part_cu(c);
+        if (part_cu < per_cu) pl->np = false;   // (cannot happen: the bound is without LDS)
     }
     const uint32_t cpw = pl->pk ? 2 * pl->GPW : pl->GPW;            // candidates per wave pull
     const uint64_t waves_needed = (ncand + cpw - 1) / cpw;
@@ -1280,7 +1298,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     while (nact) {
         st.rounds++;
         c->cur_round = (int)st.rounds;
-        HIPCHK(hipMemsetAsync(ctr + C_NCAND, 0, 3 * 8, s));     // NCAND, NCAND2, NNEXT
+        HIPCHK(hipMemsetAsync(ctr + C_NCAND, 0, 7 * 8, s));     // NCAND, NCAND2, NNEXT, (1b) NCANDB, NCAND2B, NNEXT2, WORKB
         SeedLaunch S;
         S.db = c->db.as<uint8_t>(); S.db_start = c->db_start.as<uint64_t>(); S.n_db = c->n_db; S.db_len = c->db_len;
         S.q = qd; S.q_start = qsd; S.n_q = c->n_q; S.q_len = c->q_len;
@@ -1381,7 +1399,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         // so the same results (tests).  Short reads, both NW launches
         // non-persistent (they share the arena and its slot bitmap);
         // IMSAME_ROUND1B=0 turns it off.
-        NwPlan pla;
+        NwPlan pla = {};
         bool r1b = st.rounds == 1 && r1b_on && hc[2] > 0 && n2 == 0 && ccap > n1;
         if (r1b && n1 && (rc = plan_nw(c, short_y, xcap, n1, p, c->q_len_mult, &pla))) return rc;
         if (r1b && n1 && !pla.np) r1b = false;
@@ -1404,7 +1422,6 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
             Sb.ncand = (uint32_t *)(ctr + C_NCANDB); Sb.crow = nullptr;
             Sb.ncand2 = (uint32_t *)(ctr + C_NCAND2B);
             Sb.dbg = nullptr;
-            HIPCHK(hipMemsetAsync(ctr + C_NCANDB, 0, 3 * 8, sb));     // NCANDB, NCAND2B, NNEXT2
             if ((rc = seed_launch(Sb, npz, sb, c->evb0, c->evb1))) return rc;
             double msa = 0, msb = 0;
             if (n1) {
@@ -1421,11 +1438,13 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
             if ((rc = seed_time(c->evb0, c->evb1, npz))) return rc;
             const uint32_t nb = (uint32_t)hb[0];
             if (hb[1]) return IMSAME_E_STATE;                         // short reads only: cannot happen
-            NwPlan plb;
+            NwPlan plb = {};
             bool a_done = n1 == 0;
             if (nb) {
                 if ((rc = plan_nw(c, short_y, xcap, nb, p, c->q_len_mult, &plb))) return rc;
-                if (!plb.np && !a_done) {                             // its slots are not N1a's: after it
+                const bool same = plb.np && plb.slot_words == pla.slot_words && plb.tb_dw == pla.tb_dw &&
+                                  plb.ck_dw == pla.ck_dw && plb.bnd_dw == pla.bnd_dw && plb.max_blocks == pla.max_blocks;
+                if (!same && !a_done) {                               // not N1a's arena layout: after it
                     if ((rc = nw_launch_done(c, 0, n1, &msa))) return rc;
                     rec_launch(pla, n1, msa);
                     a_done = true;
@@ -1451,8 +1470,12 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
             HIPCHK(hipMemcpyAsync(&nn, ctr + C_NNEXT2, 8, hipMemcpyDeviceToHost, s));
             HIPCHK(hipStreamSynchronize(s));
             if (getenv("IMSAME_DEBUG_ROUNDS"))
-                fprintf(stderr, "[round 1b] paused=%u spec_weak=%u budget=%u cand=%u+%u next=%llu\n", npz, Sb.spec_weak,
-                        Sb.budget, n1, nb, (unsigned long long)nn);
+                fprintf(stderr, "[round 1b] paused=%u spec_weak=%u budget=%u cand=%u+%u next=%llu | a: k%d np%d sw%u tb%llu ck%llu "
+                        "mb%u | b: k%d np%d sw%u tb%llu ck%llu mb%u\n", npz, Sb.spec_weak, Sb.budget, n1, nb,
+                        (unsigned long long)nn, pla.k, (int)pla.np, pla.slot_words, (unsigned long long)pla.tb_dw,
+                        (unsigned long long)pla.ck_dw, pla.max_blocks, nb ? plb.k : -1, nb ? (int)plb.np : -1,
+                        nb ? plb.slot_words : 0u, nb ? (unsigned long long)plb.tb_dw : 0ull,
+                        nb ? (unsigned long long)plb.ck_dw : 0ull, nb ? plb.max_blocks : 0u);
             nact = (uint32_t)nn;
             nxt = act; act = act2;                                    // round 2 scans act2; act0 is free
             continue;

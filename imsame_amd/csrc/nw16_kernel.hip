@@ -684,7 +684,13 @@ __device__ uint32_t nw_slot_claim(const NwLaunch &P, const int lane) {
             if (got == ~0u && ++w == nw) { w = 0; __builtin_amdgcn_s_sleep(4); }
         }
     }
-    return __builtin_amdgcn_readfirstlane(wv_shfl((int)got, 0));
+    got = __builtin_amdgcn_readfirstlane(wv_shfl((int)got, 0));
+    // The slot's last user may have run on another CU of this XCD: this CU's
+    // vector L1 can still hold lines of the slot from an earlier user here
+    // (L1 is invalidated at kernel starts, not when a slot changes hands
+    // inside a launch), so drop them before the first access.
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    return got;
 }
 __device__ __forceinline__ void nw_slot_release(const NwLaunch &P, const int lane, const uint32_t slot) {
     __builtin_amdgcn_s_waitcnt(0);                 // every store of this wave has reached the XCD's L2

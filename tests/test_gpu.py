@@ -780,7 +780,8 @@ def test_nw16_launch_forms_equal(dev, oracle, monkeypatch):
     assert st.launch_k5 == st.launch_pk and st.launch_pk != 0
     for name, (res, pp, st) in runs.items():
         assert not _cmp(res, base), (name, _cmp(res, base))
-        assert st.n_nw == sb.n_nw
+        if st.launch_np:                          # round 1b ran in both (its speculation sets n_nw)
+            assert st.n_nw == sb.n_nw
         for k in np.flatnonzero(base["status"] == 1)[::97]:
             r, r0 = res[k], base[k]
             s_ = int(r0["db_seq"])
