@@ -419,6 +419,9 @@ def run_e2e(ref, rst, q, qs, a):
         p = subprocess.run([cli, "-query", qf, "-db", dbf, "-out", out, "-n_threads", str(a.n_threads)] + extra,
                            stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=900)
         wall = time.monotonic() - t0
+        if os.environ.get("IMSAME_E2E_LOG"):                            # diagnostics: the CLI's stderr
+            with open(os.path.join(REPO, "gpurun_out", os.environ["IMSAME_E2E_LOG"]), "wb") as f:
+                f.write(p.stderr)
         m = re.search(rb"\[imsame\] phases (\{.*\})", p.stderr)
         if p.returncode != 0 or not m:
             return {"error": f"rc {p.returncode}: {p.stderr[-300:].decode(errors='replace')}"}

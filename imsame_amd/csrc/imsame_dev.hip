@@ -317,9 +317,12 @@ struct imsame_ctx {
     // partitions (nw16_kernel.hip:nw_slot_claim); xcc_ok: 1 when the XCC_ID
     // register was seen to name 8 XCDs (nw_xcc_check), 0 no, -1 not probed
     DBuf slotbits;
-    uint32_t slot_words = 0;
-    int xcc_ok = -1;
     int np_part_cu = -1;              // nw16_np_part_cu (-1: not computed)
+    // the arena of non-persistent launches: ONE per device context, shared by
+    // its lanes (np_owner) -- slots are taken per wave, so every NW launch of
+    // every lane draws from the chip's residency in one arena (np_prepare)
+    DBuf np_tb, np_ck;
+    imsame_ctx *np_owner = nullptr;   // lanes: the context whose arena they use
     uint64_t paths_cap_dev = 0, paths_n = 0;
     double paths_hint = 0;     // path entries per read of the last call
     std::vector<uint32_t> paths_host;
@@ -430,6 +433,40 @@ extern "C" int imsame_dev_count(void) {
     return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
 }
 
+// Non-persistent packed launches need the XCD of each wave (nw_slot_claim):
+// a probe kernel reads XCC_ID in 512 blocks, which must name each of 8 XCDs.
+// Off when the check fails (persistent launches then), or IMSAME_NW_PERSIST=1.
+// The probe runs once per device and process, when a context is created
+// (ctx_create: nothing of this process runs yet, and its hipFree -- which
+// waits for the whole device -- stalls no lane).
+static std::mutex g_xcc_mu;
+static int g_xcc_ok[64];                   // 0 not probed, 1 ok, 2 failed
+static void xcc_probe_device(imsame_ctx *c) {
+    std::lock_guard<std::mutex> lk(g_xcc_mu);
+    const int d = c->device & 63;
+    if (g_xcc_ok[d]) return;
+    g_xcc_ok[d] = 2;
+    if (c->ncu % 8 || c->ncu < 64) return;
+    const unsigned nb = 512;
+    DBuf b;
+    if (b.ensure(nb * 4)) return;
+    std::vector<uint32_t> h(nb, 0xFFFFFFFFu);
+    xcc_probe_kernel<<<nb, 64, 0, c->stream>>>(b.as<uint32_t>());
+    bool ok = hipGetLastError() == hipSuccess &&
+              hipMemcpyAsync(h.data(), b.p, nb * 4, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+              hipStreamSynchronize(c->stream) == hipSuccess;
+    uint32_t seen = 0;
+    for (uint32_t v : h) { if (v >= 8) ok = false; else seen |= 1u << v; }
+    b.release();
+    g_xcc_ok[d] = ok && seen == 0xFFu ? 1 : 2;
+}
+static bool nw_xcc_check(imsame_ctx *c) {
+    const char *pe = getenv("IMSAME_NW_PERSIST");
+    if (pe && atoi(pe)) return false;
+    std::lock_guard<std::mutex> lk(g_xcc_mu);
+    return g_xcc_ok[c->device & 63] == 1;
+}
+
 // A context with its compute stream (imsame_dev_open adds the upload stream).
 static int ctx_create(int device, imsame_ctx **out) {
     HIPCHK(hipSetDevice(device));
@@ -442,6 +479,7 @@ static int ctx_create(int device, imsame_ctx **out) {
     HIPCHK(hipEventCreate(&c->ev0));
     HIPCHK(hipEventCreate(&c->ev1));
     if (c->ctr.ensure(C_NSLOTS * 8)) { delete c; return IMSAME_E_OOM; }
+    xcc_probe_device(c);
     *out = c;
     return IMSAME_OK;
 }
@@ -468,6 +506,16 @@ extern "C" int imsame_dev_open(int device, imsame_ctx **out) {
     // last lane's queue (that lane starts after the whole upload anyway).
     for (int k = 1; k < lanes_for_queues() && !rc; ++k) rc = lane_add(c);
     if (!rc && hipStreamCreateWithFlags(&c->ustream, hipStreamNonBlocking) != hipSuccess) rc = IMSAME_E_HIP;
+    // round 1b's streams (align_one) after the lanes' compute streams: they
+    // share the hardware queues the runtime has left (created here, not in a
+    // call: creating one while other lanes run stalled a CLI call for 4.8 s,
+    // profiles/r3r_*)
+    for (size_t k = 0; k <= c->subs.size() && !rc; ++k) {
+        imsame_ctx *l = k ? c->subs[k - 1] : c;
+        if (hipStreamCreateWithFlags(&l->stream_b, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreate(&l->evb0) != hipSuccess || hipEventCreate(&l->evb1) != hipSuccess)
+            rc = IMSAME_E_HIP;
+    }
     if (rc) { imsame_dev_close(c); return rc; }
     *out = c;
     return IMSAME_OK;
@@ -491,7 +539,7 @@ extern "C" void imsame_dev_close(imsame_ctx *c) {
                     &c->act1, &c->cread, &c->csid, &c->cread2, &c->csid2, &c->cout, &c->cout2, &c->ctr,
                     &c->minraw, &c->minlen, &c->minident, &c->tb, &c->bnd, &c->paths, &c->ck, &c->rc_in, &c->rc_out,
                     &c->rc_a, &c->rc_b, &c->rc_c, &c->cbase, &c->ccnt, &c->perr, &c->wcap, &c->wout, &c->wstart,
-                    &c->crow, &c->cperm, &c->rhist, &c->act2, &c->slotbits};
+                    &c->crow, &c->cperm, &c->rhist, &c->act2, &c->slotbits, &c->np_tb, &c->np_ck};
     for (DBuf *b : bufs) b->release();
     (void)hipEventDestroy(c->ev0);
     (void)hipEventDestroy(c->ev1);
@@ -523,6 +571,7 @@ static int lane_sub(imsame_ctx *c, int k, imsame_ctx **out) {
     l->q_len_mult = c->q_len_mult;
     l->q_part_ev = c->q_part_ev; l->q_part_end = c->q_part_end;
     l->ev_db_len = 0; l->use_wcap = l->use_wstart = false;
+    l->np_owner = c;
     *out = l;
     return 0;
 }
@@ -840,28 +889,14 @@ static int nw16_band_rows() {
     return e ? std::max(0, atoi(e)) : 200;
 }
 
-// Non-persistent packed launches need the XCD of each wave (nw_slot_claim):
-// a probe kernel reads XCC_ID in 512 blocks, which must name each of 8 XCDs.
-// Off when the check fails (persistent launches then), or IMSAME_NW_PERSIST=1.
-static bool nw_xcc_check(imsame_ctx *c) {
-    const char *pe = getenv("IMSAME_NW_PERSIST");
-    if (pe && atoi(pe)) return false;
-    if (c->xcc_ok >= 0) return c->xcc_ok == 1;
-    c->xcc_ok = 0;
-    if (c->ncu % 8 || c->ncu < 64) return false;
-    const unsigned nb = 512;
-    DBuf d;
-    if (d.ensure(nb * 4)) return false;
-    std::vector<uint32_t> h(nb, 0xFFFFFFFFu);
-    xcc_probe_kernel<<<nb, 64, 0, c->stream>>>(d.as<uint32_t>());
-    bool ok = hipGetLastError() == hipSuccess &&
-              hipMemcpyAsync(h.data(), d.p, nb * 4, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
-              hipStreamSynchronize(c->stream) == hipSuccess;
-    uint32_t seen = 0;
-    for (uint32_t v : h) { if (v >= 8) ok = false; else seen |= 1u << v; }
-    d.release();
-    c->xcc_ok = ok && seen == 0xFFu ? 1 : 0;
-    return c->xcc_ok == 1;
+
+// Slot strides of the non-persistent arena: the largest packed shape of a
+// record cap (reads <= NW_W/2, either column form), so the launches of every
+// lane of a call -- whose read lengths differ -- share one layout.
+static void np_strides(uint32_t xcap, uint64_t *tb_dw, uint64_t *ck_dw) {
+    const NwShape a = nw16_shape(NW_W / 2, xcap, NW16_K), b = nw16_shape(NW_W / 2, xcap, NW16_K5);
+    *tb_dw = std::max(nw16_tb_words(a), nw16_tb_words(b));
+    *ck_dw = std::max(nw16_ck_words(a), nw16_ck_words(b));
 }
 
 // Blocks per CU the XCD partitions of a context's slot bitmap hold: the
@@ -964,10 +999,7 @@ static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, 
         // launches of a lane at once (align_one), possibly of different
         // forms, on one arena and bitmap.  Strides of the larger form;
         // partitions for the larger residency without LDS (LDS only lowers it).
-        const NwShape so = nw16_shape(ymax, xcap, pl->k == NW16_K ? NW16_K5 : NW16_K);
-        pl->tb_dw = std::max(pl->tb_dw, nw16_tb_words(so));
-        if (pl->two) pl->ck_dw = std::max(pl->ck_dw, nw16_ck_words(so));
-        pl->bnd_dw = std::max<uint64_t>(pl->bnd_dw, 3ull * so.xcap);
+        np_strides(xcap, &pl->tb_dw, &pl->ck_dw);
         part_cu = nw16_np_part_cu(c);
         if (part_cu < per_cu) pl->np = false;   // (cannot happen: the bound is without LDS)
     }
@@ -1026,6 +1058,37 @@ static int nw_launch_done(imsame_ctx *c, int qi, uint32_t n, double *ms) {
     return 0;
 }
 
+// The shared arena of non-persistent packed launches (np_strides, slot
+// partitions of nw16_np_part_cu), allocated before a call's lanes start:
+// growing it while launches run would free memory in use, and hipFree waits
+// for the whole device.  Skipped (launches stay persistent) where the
+// probe failed or the free memory less 8 GB cannot hold it.
+static int np_prepare(imsame_ctx *o, uint32_t xcap) {
+    if (!nw_xcc_check(o) || nw16_np_part_cu(o) < 1) return 0;
+    const uint32_t words = (uint32_t)((((uint64_t)o->ncu / 8) * nw16_np_part_cu(o) * 4 + 31) / 32);
+    const uint64_t ns = (uint64_t)8 * 32 * words, nbits = (uint64_t)8 * words * 4;
+    uint64_t tb_dw = 0, ck_dw = 0;
+    np_strides(xcap < 2 ? 2 : xcap, &tb_dw, &ck_dw);
+    const uint64_t need_tb = ns * tb_dw * 4, need_ck = ns * ck_dw * 4;
+    if (o->np_tb.cap >= need_tb && o->np_ck.cap >= need_ck && o->slotbits.cap >= nbits) return 0;
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) return 0;
+    const uint64_t held = o->np_tb.cap + o->np_ck.cap;
+    if (fr + held < need_tb + need_ck + (8ull << 30)) return 0;
+    hipStream_t s = o->stream;
+    if (o->np_tb.ensure(need_tb) || o->np_ck.ensure(need_ck)) { o->np_tb.release(); o->np_ck.release(); return 0; }
+    if (o->slotbits.cap < nbits) {               // all free: waves clear their bits as they leave
+        if (o->slotbits.ensure(nbits)) return IMSAME_E_OOM;
+        HIPCHK(hipMemsetAsync(o->slotbits.p, 0, o->slotbits.cap, s));
+    }
+    if (poison_on()) {
+        if (int rc = o->np_tb.poison(s)) return rc;
+        if (int rc = o->np_ck.poison(s)) return rc;
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    return 0;
+}
+
 static int launch_nw(imsame_ctx *c, NwPlan &pl, const uint32_t *cread, const uint32_t *csid, uint32_t n,
                      imsame_read_result *outp, int64_t ig, int64_t eg, const imsame_params *p, uint32_t ymax,
                      uint32_t xmax, uint32_t *work, const uint8_t *dbp, const uint64_t *dbs, const uint8_t *qp,
@@ -1037,14 +1100,12 @@ static int launch_nw(imsame_ctx *c, NwPlan &pl, const uint32_t *cread, const uin
     const uint64_t tb_dw = pl.tb_dw;
     // fewer resident waves if the arena cannot be had (the queue still drains)
     const uint64_t per_slot = tb_dw * 4, bnd_slot = pl.bnd_dw * 4, ck_slot = pl.ck_dw * 4;
+    imsame_ctx *ao = c->np_owner ? c->np_owner : c;     // the shared arena (np_prepare)
     if (pl.np) {                                 // every slot of the 8 partitions, and their bitmap
         const uint64_t ns = (uint64_t)pl.max_blocks * 4, nbits = (uint64_t)8 * pl.slot_words * 4;
-        if (c->tb.ensure(ns * per_slot) || c->bnd.ensure(ns * bnd_slot + 64) || (ck_slot && c->ck.ensure(ns * ck_slot))) {
-            pl.np = false;                       // persistent, with what can be had
-            pl.blocks = std::min(pl.blocks, pl.max_blocks);
-        } else if (c->slotbits.cap < nbits) {    // all free: waves clear their bits as they leave
-            if (c->slotbits.ensure(nbits)) return IMSAME_E_OOM;
-            HIPCHK(hipMemsetAsync(c->slotbits.p, 0, c->slotbits.cap, s));
+        if (ao->np_tb.cap < ns * per_slot || ao->np_ck.cap < ns * ck_slot || ao->slotbits.cap < nbits) {
+            pl.np = false;                       // not prepared for this shape: persistent on this lane's
+            pl.blocks = (unsigned)std::min<uint64_t>((uint64_t)c->ncu * 8, pl.blocks);
         }
     }
     if (!pl.np) {
@@ -1058,8 +1119,8 @@ static int launch_nw(imsame_ctx *c, NwPlan &pl, const uint32_t *cread, const uin
             pl.blocks = (pl.blocks + 1) / 2;
         }
     }
-    if (poison_on()) {                           // slots hold nothing from earlier launches
-        const DBuf *scr[] = {&c->tb, &c->ck, &c->bnd};
+    if (poison_on() && !pl.np) {                 // slots hold nothing from earlier launches (the shared
+        const DBuf *scr[] = {&c->tb, &c->ck, &c->bnd};          // arena: at np_prepare)
         for (const DBuf *b : scr)
             if (int rc = b->poison(s)) return rc;
     }
@@ -1069,7 +1130,7 @@ static int launch_nw(imsame_ctx *c, NwPlan &pl, const uint32_t *cread, const uin
     P.cand_read = cread; P.cand_sid = csid; P.n_cand = n;
     P.igap = (int32_t)ig; P.egap = (int32_t)eg;
     P.G = pl.G; P.GPW = pl.GPW; P.xcap = pl.xcap; P.xstride = pl.xstride; P.steps = pl.steps;
-    P.tb = c->tb.as<uint32_t>(); P.tb_wave_dw = tb_dw;
+    P.tb = pl.np ? ao->np_tb.as<uint32_t>() : c->tb.as<uint32_t>(); P.tb_wave_dw = tb_dw;
     P.bnd = c->bnd.as<int32_t>(); P.bnd_wave = pl.bnd_dw;
     P.minlen = c->minlen.as<uint32_t>(); P.n_minlen = ymax + 1;
     P.minident = c->minident.as<uint32_t>(); P.n_minident = xmax + ymax + 2;
@@ -1079,10 +1140,11 @@ static int launch_nw(imsame_ctx *c, NwPlan &pl, const uint32_t *cread, const uin
     P.paths = c->paths.as<uint32_t>(); P.paths_cap = paths_cap;
     P.paths_used = (uint32_t *)(ctr + C_PATHS); P.want_paths = p->want_paths;
     P.flags = (uint32_t *)(ctr + C_FLAGS);
-    P.ck = (pl.two || pl.lng) ? c->ck.as<uint32_t>() : nullptr; P.ck_wave_dw = pl.ck_dw;
+    P.ck = !(pl.two || pl.lng) ? nullptr : pl.np ? ao->np_ck.as<uint32_t>() : c->ck.as<uint32_t>();
+    P.ck_wave_dw = pl.ck_dw;
     P.band_w = pl.band_w; P.redo = (uint32_t *)(ctr + C_REDO); P.win = (uint32_t *)(ctr + C_WIN);
     P.prof = getenv("IMSAME_NW_PROF") ? (unsigned long long *)(ctr + C_PROF) : nullptr;
-    P.slot_bits = pl.np ? c->slotbits.as<uint32_t>() : nullptr; P.slot_words = pl.slot_words;
+    P.slot_bits = pl.np ? ao->slotbits.as<uint32_t>() : nullptr; P.slot_words = pl.slot_words;
     HIPCHK(hipMemsetAsync(work, 0, 4, s));
     HIPCHK(hipEventRecord(e0, s));               // the launch's time includes its ordering
     if (crow && pl.two && n >= 64) {
@@ -1643,6 +1705,10 @@ static int align_impl(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint6
     const uint64_t n = read_to - read_from;
     uint64_t ymax = 0;
     ymax = range_ymax(c, read_from, read_to);
+    if (!c->is_sub && ymax <= (uint64_t)NW_W / 2 && n) {   // the lanes' shared NW arena, before they start
+        const int rp = np_prepare(c, (uint32_t)std::min<uint64_t>(c->max_rec, p->max_read_size));
+        if (rp) return rp;
+    }
     // LANES: the range is cut into `nl` parts that run concurrently on nl
     // streams (this context and c->subs, which share the index and the
     // query), so one part's latency-bound phases -- seed scans, the last
