@@ -86,10 +86,6 @@ __host__ __device__ constexpr int nw16_nrec(int K) { return K > 8 ? 3 : 2; }
 #define NW16_WIN_MAX 448          // longest window (steps) a wave writes in its first sweep
 #define NW16_WIN_BOTTOM 40        // rows above the last one for an unpredicted candidate
 #define NW16_BAND2 4              // the second sweep's retry band, in bands
-// Two-pass mode: the last-column values of the first sweep go to per-(group,
-// half) rows after the traceback records of the slot, 2 x GPW x steps dwords;
-// GPW x xstride <= 16384 (nw16_shape) and GPW x G <= 64 bound it for any shape
-#define NW16_VL_DW (2 * (16384 + 64))
 
 // does the launch fit the int16 path?  (all gap terms non-positive)
 __host__ static inline bool nw16_fits(int64_t ig, int64_t eg, uint64_t xcap, uint64_t ymax) {
@@ -330,18 +326,6 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
         int bestR[2] = {INT_MIN, INT_MIN}, bestRj[2] = {0, 0};
         const uint32_t limp = pk2(xl[0] - 2, xl[1] - 2);
         uint8_t *tb3 = (uint8_t *)tbw;
-        // TWO: the first sweep keeps no running best of the last column (5 VALU
-        // per step); the lane that owns half h's last column stores its value
-        // each step (vlc[h], row t - gl at index t) and the best cell is
-        // reduced from those rows after the sweep
-        // (stores: wave-uniform base + t in SGPRs, per-lane byte offsets vo0/vo1 -- no VALU per step)
-        uint8_t *vlb = tb3 + (uint32_t)(64 * NREC * 4) * (uint32_t)P.steps;
-        const uint32_t vo0 = (uint32_t)(2 * gg) * (uint32_t)P.steps * 4u, vo1 = vo0 + (uint32_t)P.steps * 4u;
-        const uint32_t *vlc0 = (const uint32_t *)(vlb + vo0), *vlc1 = (const uint32_t *)(vlb + vo1);
-#ifndef IMSAME_WAVE_EMU
-        const __amdgpu_buffer_rsrc_t vlr =
-            __builtin_amdgcn_make_buffer_rsrc(vlb, 0, 2 * GPW * P.steps * 4, 0x00020000);   // raw, bounds = the rows
-#endif
 
         auto step = [&](const bool PRE, const bool CAREFUL, const bool TB, const int t, uint32_t (&cur)[K],
                         const uint32_t (&own)[K], uint32_t &in0, const uint32_t in1) {
@@ -402,22 +386,9 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
             if (!LAST)
 #pragma unroll
                 for (int s = 1; s < K; ++s) vl = wv_bfi(lastm[s], cur[s], vl);
-            if (TWO) {
-#ifndef IMSAME_WAVE_EMU
-                if (ownC[0]) __builtin_amdgcn_raw_buffer_store_b32(vl, vlr, (int)vo0, t * 4, 0);
-                if (ownC[1]) __builtin_amdgcn_raw_buffer_store_b32(vl, vlr, (int)vo1, t * 4, 0);
-#else
-                if (ownC[0]) *(uint32_t *)(vlb + vo0 + (uint32_t)t * 4u) = vl;
-                if (ownC[1]) *(uint32_t *)(vlb + vo1 + (uint32_t)t * 4u) = vl;
-#endif
-            } else {
-                uint32_t km = pk_neg_mask(pk_sub(vl, bestC));         // keep where vl < best (">=" takes)
-                if (CAREFUL) km |= pk_neg_mask(pk_sub(limp, ipk)) | pk_neg_mask(pk_sub(ipk, pk1(1)));
-                bestC = wv_bfi(km, bestC, vl);
-                bestCi = wv_bfi(km, bestCi, ipk);
-                ipk = pk_add(ipk, 0x10001u);
-            }
+            uint32_t km = pk_neg_mask(pk_sub(vl, bestC));             // keep where vl < best (">=" takes)
             if (CAREFUL) {
+                km |= pk_neg_mask(pk_sub(limp, ipk)) | pk_neg_mask(pk_sub(ipk, pk1(1)));
                 if (i >= 1 && (i == xl[0] - 1 || i == xl[1] - 1)) {
                     for (int h = 0; h < 2; ++h) {
                         if (!lact[h] || i != xl[h] - 1) continue;
@@ -429,6 +400,9 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
                     }
                 }
             }
+            bestC = wv_bfi(km, bestC, vl);
+            bestCi = wv_bfi(km, bestCi, ipk);
+            ipk = pk_add(ipk, 0x10001u);
             in0 = pre ? in1 : sN;
             outT = cur[K - 1]; outMS = mfS; outL = l0;
         };
@@ -498,34 +472,11 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
         mark(1);
 
         // best cell per half: row-major order, ">=" -> last visited wins
-        int lcv[2] = {INT_MIN, INT_MIN}, lci[2] = {0, 0};
-        if (TWO) {
-            // last column, rows 1 .. xl-2: lane gl of the group takes rows
-            // 1 + gl, 1 + gl + G, ... in ascending order; the group reduction
-            // below takes the largest value, ties to the later row; lane 0
-            // carries the empty case (no such row: -BIG at row 0, as the
-            // one-pass running best starts)
-            for (int h = 0; h < 2; ++h) {
-                if (!valid[0] || yl[h] < 2) continue;             // no owner (ownC false in every lane)
-                const int o = (yl[h] - 1) / K;
-                const uint32_t *vr = (h ? vlc1 : vlc0) + o;
-                if (gl == 0) { lcv[h] = -NW16_BIG; lci[h] = 0; }
-                for (int i = 1 + gl; i <= xl[h] - 2; i += G) {
-                    const int val = pk_half(vr[i], h);
-                    if (val >= lcv[h]) { lcv[h] = val; lci[h] = i; }
-                }
-            }
-        } else {
-            for (int h = 0; h < 2; ++h) {
-                lcv[h] = ownC[h] ? pk_half(bestC, h) : INT_MIN;
-                lci[h] = pk_half(bestCi, h);
-            }
-        }
         for (int h = 0; h < 2; ++h) {
             red[lane * 8 + 4 * h + 0] = bestR[h];
             red[lane * 8 + 4 * h + 1] = bestRj[h];
-            red[lane * 8 + 4 * h + 2] = lcv[h];
-            red[lane * 8 + 4 * h + 3] = lci[h];
+            red[lane * 8 + 4 * h + 2] = ownC[h] ? pk_half(bestC, h) : INT_MIN;
+            red[lane * 8 + 4 * h + 3] = pk_half(bestCi, h);
         }
         wv_lds_sync();
         int bscore[2], bx[2], by[2];
@@ -695,9 +646,7 @@ __host__ static inline NwShape nw16_shape(uint32_t ymax, uint32_t xcap, int K = 
     return s;
 }
 // traceback dwords per wave slot (NREC per lane per step)
-__host__ static inline uint64_t nw16_tb_words(const NwShape &s) {
-    return (uint64_t)s.steps * 64 * nw16_nrec(s.k) + NW16_VL_DW;      // + the last-column rows (two-pass)
-}
+__host__ static inline uint64_t nw16_tb_words(const NwShape &s) { return (uint64_t)s.steps * 64 * nw16_nrec(s.k); }
 // checkpoint dwords per wave slot (two-pass mode): one per NW16_CK steps + the start
 __host__ static inline uint64_t nw16_ck_words(const NwShape &s) {
     return (uint64_t)((s.steps + NW16_CK - 1) / NW16_CK + 1) * nw16_nst(s.k) * 64;
@@ -767,7 +716,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? NW1
 void nw16_kernel(NwLaunch P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
-    // one call site, so nw16_wave is inlined (two made the compiler outline it)
+    // One call site, so nw16_wave is inlined: with two (persistent and
+    // non-persistent) the compiler outlined it as a function, 3 % slower at
+    // C2 (profiles/r3v_*: 127.1 vs 123.3 ms per step on one box).
     uint32_t slot;
     if (P.slot_bits) {                          // non-persistent: one task, a slot of this XCD
         slot = nw_slot_claim(P, lane);
