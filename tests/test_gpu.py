@@ -355,6 +355,26 @@ def test_headline_mode_parity():
     assert d["accepted"] > 850_000
 
 
+@pytest.mark.timeout(300)
+def test_poison_flag_active():
+    """IMSAME_DEBUG_POISON=1: in a subprocess, so the flag is
+    read at library load -- every reused device buffer is filled with poison
+    on its call's stream and every kernel is followed by a named stream
+    synchronize.  The "[poison]" lines show it was live; the rows stay
+    oracle-exact (no kernel reads memory it did not write)."""
+    import json
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, IMSAME_DEBUG_POISON="1")
+    p = subprocess.run([sys.executable, "-u", "-m", "tests.poison_run"], cwd=repo, env=env,
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=280)
+    assert p.returncode == 0, p.stderr[-3000:].decode(errors="replace")
+    err = p.stderr.decode(errors="replace")
+    assert err.count("[poison] nw16_kernel") > 0 and err.count("[poison] seed kernel") > 0
+    d = json.loads(p.stdout.decode().strip().splitlines()[-1])
+    assert d["oracle_rc"] == 0 and d["mismatched_fields"] == [] and d["accepted"] > 5000, d
+
+
 @pytest.fixture
 def oracle_memo(oracle):
     """The oracle with its test-speed memo of rejected (read, record) pairs
