@@ -1353,6 +1353,11 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     st.ms_setup = now_ms() - t_start;
 
     const uint32_t short_y = std::min<uint32_t>(ycap, NW_W / 2);
+    const char *l64_env = getenv("IMSAME_SEED_L64");
+    // (C2 1/8 shard: 18.5 vs 19.2 ms per step, round 2's ~2k reads scan in a
+    // third of the time; 32768 also takes round 1b's 17k: 18.9; C2 unchanged;
+    // profiles/r3l64/)
+    const uint64_t seed_l64_below = l64_env ? strtoull(l64_env, nullptr, 10) : 8192;
     const char *r1b_env = getenv("IMSAME_ROUND1B");
     const bool r1b_on = !(r1b_env && !atoi(r1b_env)) && ycap <= short_y && !crow && !poison_on();
     uint32_t nact = n;
@@ -1396,10 +1401,15 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         // round 1 instead of 16, whose extra windows a true read never needs;
         // +1.9 %, profiles/r2am_*)
         auto seed_launch = [&](const SeedLaunch &SL, uint32_t na, hipStream_t ss, hipEvent_t e0, hipEvent_t e1) -> int {
-            const int L = l_env ? atoi(l_env) : seed_lanes((uint32_t)std::min<uint64_t>((uint64_t)na * c->nlanes, 0xFFFFFFFFu));
+            int L = l_env ? atoi(l_env) : seed_lanes((uint32_t)std::min<uint64_t>((uint64_t)na * c->nlanes, 0xFFFFFFFFu));
+            // a whole wave per read where few reads scan (the later rounds: each
+            // read's remaining windows 64 at a time), IMSAME_SEED_L64 = the read
+            // count (over all lanes) below which (0: never)
+            if (!l_env && (uint64_t)na * c->nlanes < seed_l64_below) L = 64;
             const size_t slds = 256 * SEED_LDS_PER_LANE;
             HIPCHK(hipEventRecord(e0, ss));
-            if (L >= 16)     seed_group_kernel<16><<<nblk((uint64_t)na * 16, 256), 256, slds, ss>>>(SL);
+            if (L >= 64)     seed_group_kernel<64><<<nblk((uint64_t)na * 64, 256), 256, slds, ss>>>(SL);
+            else if (L >= 16) seed_group_kernel<16><<<nblk((uint64_t)na * 16, 256), 256, slds, ss>>>(SL);
             else if (L >= 4) seed_group_kernel<4><<<nblk((uint64_t)na * 4, 256), 256, slds, ss>>>(SL);
             else if (L >= 2) seed_group_kernel<2><<<nblk((uint64_t)na * 2, 256), 256, slds, ss>>>(SL);
             else             seed_kernel<<<nblk(na, 256), 256, 0, ss>>>(SL);

@@ -301,7 +301,8 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
                     run_wave([&](int lane) {
                         uint64_t h = 0;
                         const uint32_t gidx = (uint32_t)((w0 + lane) / L);
-                        if (L == 16) seed_group<16>(SL, gidx, lane % 16, lane, lds.data() + lane * SPEC_MAX, h);
+                        if (L == 64) seed_group<64>(SL, gidx, lane, lane, lds.data() + lane * SPEC_MAX, h);
+                        else if (L == 16) seed_group<16>(SL, gidx, lane % 16, lane, lds.data() + lane * SPEC_MAX, h);
                         else         seed_group<4>(SL, gidx, lane % 4, lane, lds.data() + lane * SPEC_MAX, h);
                         wh += h;
                     });

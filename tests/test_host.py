@@ -413,7 +413,7 @@ def test_emulated_pipeline_matches_oracle(emu, oracle, name, flags, monkeypatch)
 
 @pytest.mark.parametrize("budget,lanes,spec,weak", [("1", "1", "8", "4"), ("3", "1", "1", "1"), ("0", "4", "8", "8"),
                                                     ("3", "4", "2", "4"), ("1", "16", "8", "2"), ("0", "16", "1", "8"),
-                                                    ("0", "1", "1", "8")])
+                                                    ("0", "1", "1", "8"), ("1", "64", "8", "4"), ("3", "64", "2", "1")])
 def test_emulated_pipeline_seed_budget(emu, oracle, budget, lanes, spec, weak, monkeypatch):
     """Reads that pause on the per-round hit budget resume at the same hit,
     the grouped scan (L lanes per read, seed_kernel.hip:seed_group) merges
