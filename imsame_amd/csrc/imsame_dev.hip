@@ -1400,15 +1400,20 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         // times the call's lanes (C2, 8 lanes of 125k: 4 lanes per read in
         // round 1 instead of 16, whose extra windows a true read never needs;
         // +1.9 %, profiles/r2am_*)
-        auto seed_launch = [&](const SeedLaunch &SL, uint32_t na, hipStream_t ss, hipEvent_t e0, hipEvent_t e1) -> int {
+        auto pick_L = [&](uint32_t na) {
             int L = l_env ? atoi(l_env) : seed_lanes((uint32_t)std::min<uint64_t>((uint64_t)na * c->nlanes, 0xFFFFFFFFu));
             // a whole wave per read where few reads scan (the later rounds: each
             // read's remaining windows 64 at a time), IMSAME_SEED_L64 = the read
-            // count (over all lanes) below which (0: never)
+            // count (over all lanes) below which (0: never); those groups may
+            // emit up to SPEC_BIG candidates per read
             if (!l_env && (uint64_t)na * c->nlanes < seed_l64_below) L = 64;
+            return L;
+        };
+        auto seed_launch = [&](const SeedLaunch &SL, uint32_t na, hipStream_t ss, hipEvent_t e0, hipEvent_t e1) -> int {
+            const int L = pick_L(na);
             const size_t slds = 256 * SEED_LDS_PER_LANE;
             HIPCHK(hipEventRecord(e0, ss));
-            if (L >= 64)     seed_group_kernel<64><<<nblk((uint64_t)na * 64, 256), 256, slds, ss>>>(SL);
+            if (L >= 64)      seed_group_kernel<64, SPEC_BIG><<<nblk((uint64_t)na * 64, 256), 256, 256 * SPEC_BIG * 8, ss>>>(SL);
             else if (L >= 16) seed_group_kernel<16><<<nblk((uint64_t)na * 16, 256), 256, slds, ss>>>(SL);
             else if (L >= 4) seed_group_kernel<4><<<nblk((uint64_t)na * 4, 256), 256, slds, ss>>>(SL);
             else if (L >= 2) seed_group_kernel<2><<<nblk((uint64_t)na * 2, 256), 256, slds, ss>>>(SL);
@@ -1453,6 +1458,8 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
             HIPCHK(hipGetLastError());
             return 0;
         };
+        if (st.rounds >= 2 && !spec_env && pick_L(nact) >= 64)   // whole-wave groups: up to SPEC_BIG
+            S.spec = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(SPEC_BIG, ccap / nact));
         if ((rc = seed_launch(S, nact, s, c->ev0, c->ev1))) return rc;
         uint64_t hc[3];
         HIPCHK(hipMemcpyAsync(hc, ctr + C_NCAND, 24, hipMemcpyDeviceToHost, s));

@@ -63,6 +63,10 @@ __device__ __forceinline__ void seed_outcome(const SeedLaunch &S, uint32_t ne, b
 }
 #endif
 #define SPEC_MAX 8
+// ... in rounds scanned by whole-wave groups (few reads: seed_group<64, SPEC_BIG>),
+// so a random read with more than SPEC_MAX live e-value passes needs no
+// extra round of one read (its NW alone is ~0.6 ms of a 2000-row record)
+#define SPEC_BIG 32
 // speculation width from a weak first candidate on (spec_after_first); 1 = off
 #ifndef SPEC_WEAK
 #define SPEC_WEAK 1
@@ -360,14 +364,16 @@ __device__ __forceinline__ uint32_t kmer_code_at(const uint8_t *__restrict__ q, 
 
 // emit[] lives in registers, identical in every lane of the group (each lane
 // runs the same merge); statically indexed so it never spills to scratch.
-__device__ __forceinline__ bool emit_has(const uint32_t (&em)[SPEC_MAX], uint32_t ne, uint32_t sid) {
+template <int SM>
+__device__ __forceinline__ bool emit_has(const uint32_t (&em)[SM], uint32_t ne, uint32_t sid) {
     bool f = false;
 #pragma unroll
-    for (int m = 0; m < SPEC_MAX; ++m) f |= (uint32_t)m < ne && em[m] == sid;
+    for (int m = 0; m < SM; ++m) f |= (uint32_t)m < ne && em[m] == sid;
     return f;
 }
 
-template <int L>
+// SM: the most candidates a read may emit (its list in LDS, emit[] in registers)
+template <int L, int SM = SPEC_MAX>
 __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane, uint2 *lst, uint64_t &hits) {
     const bool gvalid = gidx < S.n_active;
     const int gbase = lane - wl;                                  // first lane of the group
@@ -390,9 +396,9 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
         mraw = ylen < S.n_minraw ? S.minraw[ylen] : ~0ull;
         ys = (int64_t)rs; ye = (r == S.n_q - 1) ? (int64_t)S.q_len : (int64_t)re - 1;
     }
-    uint32_t emit[SPEC_MAX];
+    uint32_t emit[SM];
 #pragma unroll
-    for (int m = 0; m < SPEC_MAX; ++m) emit[m] = 0xFFFFFFFFu;
+    for (int m = 0; m < SM; ++m) emit[m] = 0xFFFFFFFFu;
     uint32_t ne = 0, perr = 0, used = 0;
     uint32_t e0p = 0, e0r = 0;             // first candidate's window (read-relative) and bucket rank
     bool done = !gvalid || p >= up_to || read_irrelevant(S, ylen), paused = false,
@@ -444,7 +450,7 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
             if (stop) continue;
             const uint64_t pk = p + (uint64_t)wk;
             if (pk >= up_to) { exhausted = true; stop = true; continue; }
-            const uint2 *lk = lst + (wk - wl) * SPEC_MAX;           // lane wk's list
+            const uint2 *lk = lst + (wk - wl) * SM;                 // lane wk's list
             for (uint32_t m = 0; m < cnt && !stop; ++m) {
                 const uint2 it = lk[m];
                 if (emit_has(emit, ne, it.x)) continue;            // emitted by an earlier window
@@ -454,7 +460,7 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
                     if (nm == 0 && S.spec_weak > spec && (it.y & 0x40000000u)) spec = S.spec_weak;   // spec_after_first
                 }
 #pragma unroll
-                for (int q2 = 0; q2 < SPEC_MAX; ++q2) emit[q2] = ((uint32_t)q2 == ne) ? it.x : emit[q2];
+                for (int q2 = 0; q2 < SM; ++q2) emit[q2] = ((uint32_t)q2 == ne) ? it.x : emit[q2];
                 ++ne;
                 if (ne == spec) {                                  // resume after this hit
                     if (wl == 0) { S.cur_p[k] = pk; S.cur_h[k] = (it.y & LST_RANK) + 1; }
@@ -498,7 +504,7 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
     const uint32_t o = wv_atomic_add(shortc ? S.ncand : S.ncand2, ne);
     uint32_t *cr = shortc ? S.cread : S.cread2, *cs = shortc ? S.csid : S.csid2;
 #pragma unroll
-    for (int m = 0; m < SPEC_MAX; ++m)
+    for (int m = 0; m < SM; ++m)
         if ((uint32_t)m < ne) { cr[o + m] = (uint32_t)r; cs[o + m] = emit[m]; }
     if (shortc && S.crow) {
         // the first candidate's hit again: its entry gives the record position
@@ -616,14 +622,14 @@ __global__ void accept_window_kernel(const SeedLaunch S, const imsame_read_resul
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k < n) accept_window_one(S, res, k, wout);
 }
-template <int L>
+template <int L, int SM = SPEC_MAX>
 __global__ __launch_bounds__(256) void seed_group_kernel(SeedLaunch S) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x & 63, wl = lane % L;
-    uint2 *lst = (uint2 *)smem + threadIdx.x * SPEC_MAX;
+    uint2 *lst = (uint2 *)smem + threadIdx.x * SM;
     const uint32_t gidx = (blockIdx.x * blockDim.x + threadIdx.x) / L;
     uint64_t hits = 0;
-    seed_group<L>(S, gidx, wl, lane, lst, hits);
+    seed_group<L, SM>(S, gidx, wl, lane, lst, hits);
     if (hits) atomicAdd(S.nhits, (unsigned long long)hits);
 }
 

@@ -282,6 +282,11 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
         S.minident = mi.data(); S.n_minident = xcap + ymax + 2;
         S.max_rs = p->max_read_size; S.short_ylen = short_y; S.max_rec = max_rec;
         S.spec = (st.rounds == 1) ? 1u : (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(spec_later, ccap / nact));
+        {   // imsame_dev.hip:align_one -- whole-wave groups may emit up to SPEC_BIG
+            const char *le = getenv("IMSAME_SEED_L");
+            if (st.rounds >= 2 && !spec_env && (le ? atoi(le) : seed_lanes(nact)) >= 64)
+                S.spec = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(SPEC_BIG, ccap / nact));
+        }
         S.spec_weak = spec_weak;
         S.budget = seed_budget(budget1, (uint32_t)st.rounds);
         S.next = nxt.data(); S.nnext = &nc[2];
@@ -295,13 +300,13 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
             if (L <= 1) {
                 for (uint32_t i = 0; i < na; ++i) { uint64_t h = 0; seed_one(SL, i, h); nhits += h; }
             } else {                   // seed_group_kernel: one 64-lane wave at a time
-                std::vector<uint2> lds(64 * SPEC_MAX);
+                std::vector<uint2> lds(64 * SPEC_BIG);
                 std::atomic<unsigned long long> wh{0};
                 for (uint64_t w0 = 0; w0 < (uint64_t)na * L; w0 += 64)
                     run_wave([&](int lane) {
                         uint64_t h = 0;
                         const uint32_t gidx = (uint32_t)((w0 + lane) / L);
-                        if (L == 64) seed_group<64>(SL, gidx, lane, lane, lds.data() + lane * SPEC_MAX, h);
+                        if (L == 64) seed_group<64, SPEC_BIG>(SL, gidx, lane, lane, lds.data() + lane * SPEC_BIG, h);
                         else if (L == 16) seed_group<16>(SL, gidx, lane % 16, lane, lds.data() + lane * SPEC_MAX, h);
                         else         seed_group<4>(SL, gidx, lane % 4, lane, lds.data() + lane * SPEC_MAX, h);
                         wh += h;

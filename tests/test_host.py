@@ -221,16 +221,20 @@ def test_emulated_predicted_traceback_window(emu, oracle, seed_l, monkeypatch):
         assert np.array_equal(got0[f], exp[f]), f
 
 
-@pytest.mark.parametrize("r1b", ["1", "0"])
-def test_emulated_round1b(emu, oracle, r1b, monkeypatch):
+@pytest.mark.parametrize("r1b,seed_l", [("1", ""), ("0", ""), ("1", "64"), ("0", "64")])
+def test_emulated_round1b(emu, oracle, r1b, seed_l, monkeypatch):
     """Round 1b (imsame_dev.hip:align_one): reads that round 1 paused without
     a candidate (random reads against a 20 Mbp database spend the 32-hit
     budget) scan on at once with weak-first speculation, before round 1's
     NW results, on the device's second stream; both NW launches update the
     same per-read state.  Every field equals the oracle with and without it,
-    and the 1b scan took reads over."""
+    and the 1b scan took reads over.  seed_l 64: whole-wave scan groups,
+    up to SPEC_BIG candidates per read in the later rounds."""
     from tests import synth
     monkeypatch.setenv("IMSAME_ROUND1B", r1b)
+    if seed_l:          # whole-wave groups, which emit up to SPEC_BIG per read after round 1
+        monkeypatch.setenv("IMSAME_SEED_L", seed_l)
+        monkeypatch.delenv("IMSAME_SPEC", raising=False)
     cnt = emu.lib.emu_r1b_count
     cnt.restype = C.c_uint32
     cnt()
