@@ -424,9 +424,14 @@ static int hw_queues() {
     return q;
 }
 
-// Most lanes a call runs (imsame_dev_align): one per hardware queue, <= 8.
+// Most lanes a call runs (imsame_dev_align): a lane has two streams (its
+// rounds and round 1b's scan + NW launch, align_one), each wants a hardware
+// queue of its own -- a stream that shares one waits behind the other's
+// kernels (C2 with 8 lanes on 8 queues: lane 0's round-1b launch ran 75 ms
+// late, profiles/r3_c2_timeline.txt) -- so queues / 2, <= 8 (C2, 8 queues:
+// 4 lanes, 119.3-119.9 vs 121.0-121.6 ms with 8, profiles/r3q16/).
 #define LANES_MAX 8
-static int lanes_for_queues() { return std::max(1, std::min(LANES_MAX, hw_queues())); }
+static int lanes_for_queues() { return std::max(1, std::min(LANES_MAX, hw_queues() / 2)); }
 
 extern "C" int imsame_dev_count(void) {
     int n = 0;

@@ -3,7 +3,7 @@
 bench.py's C2 step -- ONE query of 1M x 150 bp reads vs the 50 Mbp reference
 (BASELINE.json configs[1], bench.py's seeds), page-locked query uploaded
 asynchronously, -n_threads 16, GPU_MAX_HW_QUEUES=8 set before HIP starts so
-the call runs its 8 lanes on 8 hardware queues -- then read-for-read parity
+the call runs 4 lanes, two streams each, on 8 hardware queues -- then read-for-read parity
 with the oracle on the start, middle (a chunk head) and end windows.
 
     python -m tests.headline_run        -> one JSON line on stdout
