@@ -1742,9 +1742,9 @@ static int align_impl(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint6
     // LANE_READS reads for its first NW launch to fill the chip's wave slots
     // on its own (~0.9 candidates per read, 8 per wave: 40k reads -> 4.5k
     // waves against 4 per SIMD x 1024 SIMDs), and a hardware queue of its own
-    // (lanes_for_queues).  C2 with 8 queues: 1M reads -> 8 lanes (+1.4 % over
-    // 4, profiles/r2ab_*), its 1/8 shard (125k) -> 3 (1-3 % faster than 2,
-    // r2w_*).  IMSAME_LANES overrides (tests, A/B runs).
+    // (lanes_for_queues).  C2 with 8 queues: 1M reads -> 4 lanes (1-2 % faster
+    // than 8, profiles/r3q16/, r3ln/), its 1/8 shard (125k) -> 3 (1-3 % faster
+    // than 2, r2w_*).  IMSAME_LANES overrides (tests, A/B runs).
     const char *le = getenv("IMSAME_LANES");
     const char *lre = getenv("IMSAME_LANE_READS");
     const uint64_t lane_reads = std::max<uint64_t>(1, lre ? strtoull(lre, nullptr, 10) : LANE_READS);
