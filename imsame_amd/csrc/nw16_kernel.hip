@@ -104,6 +104,15 @@ __host__ static inline bool nw16_fits(int64_t ig, int64_t eg, uint64_t xcap, uin
 WV_DEVICE uint32_t pk1(int v) { return (uint32_t)(uint16_t)v * 0x10001u; }
 WV_DEVICE uint32_t pk2(int lo, int hi) { return (uint32_t)(uint16_t)lo | ((uint32_t)(uint16_t)hi << 16); }
 WV_DEVICE int pk_half(uint32_t v, int h) { return (int)(int16_t)(h ? (v >> 16) : (v & 0xFFFFu)); }
+// DP values are held BIASED by 2^15 (each half's top bit flipped, an xor):
+// every value of a launch lies in [-NW16_BIG - R, NW16_BIG] (nw16_fits: R <=
+// 8191, sentinels and drift included), so a biased half stays in [8193,
+// 49152].  Unsigned maxes order them, differences (and their signs) are the
+// unbiased ones, and adding a gap constant is a plain 32-bit subtract of its
+// magnitude -- no borrow can cross from one half into the other -- which
+// issues in half the cycles of v_pk_add_i16 (§4.1, profiles/r06_valu_rate.txt).
+#define NW16_H 0x80008000u
+WV_DEVICE int pk_score(uint32_t v, int h) { return (int)(h ? (v >> 16) : (v & 0xFFFFu)) - 32768; }
 WV_DEVICE uint32_t base_code(uint8_t b) { return (b >> 1) & 3u; }          // A0 C1 T2 G3: distinct
 
 // score table for v_perm: selector byte d = xcode ^ ycode picks the low byte
@@ -272,7 +281,7 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
         const int j0 = gl * K;
         const bool leadc0 = gl == 0;
         const int xcl = max(xlp - 1, 0);
-        const uint32_t NBIG = pk1(-NW16_BIG), EG = pk1(eg), IGE = pk1(ig + eg);
+        const uint32_t NBIG = pk1(-NW16_BIG) ^ NW16_H, EGN = pk1(-eg), IGEN = pk1(-(ig + eg));   // biased; gap magnitudes
         uint32_t yreg[K], lastm[K];
         bool ownC[2], lact[2];
         for (int h = 0; h < 2; ++h) {
@@ -298,7 +307,7 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
             const uint32_t ya = base_code(Yp[0][min(j0 - 1, yl[0] - 1)]), yb = base_code(Yp[1][min(j0 - 1, yl[1] - 1)]);
             yprev = ya | ((ya | 4u) << 8) | (yb << 16) | ((yb | 4u) << 24);
         }
-        const uint32_t t0prev = wv_perm(NW16_TBL_HI, NW16_TBL_LO, xsel0 ^ yprev);
+        const uint32_t t0prev = wv_perm(NW16_TBL_HI, NW16_TBL_LO, xsel0 ^ yprev) ^ NW16_H;
         // The column state keeps mc's score in a frame shifted by ig + eg: dI[s]
         // = T[i-2][j-1] + ig + eg is the previous row's d0 + ig + eg of this
         // slot (the left take computes it anyway), so the column max compares
@@ -307,22 +316,22 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
         uint32_t A[K], B[K], dI[K], mcS[K], u0[K];
 #pragma unroll
         for (int s = 0; s < K; ++s) {
-            A[s] = wv_perm(NW16_TBL_HI, NW16_TBL_LO, xsel0 ^ yreg[s]);
+            A[s] = wv_perm(NW16_TBL_HI, NW16_TBL_LO, xsel0 ^ yreg[s]) ^ NW16_H;
             B[s] = A[s];
         }
 #pragma unroll
         for (int s = 0; s < K; ++s) {
             // mc[j-1] = (T[0][j-1], row 0); row 0 stands in for rows -1 and -2
-            dI[s] = pk_add((s == 0) ? t0prev : A[s - 1], IGE);
+            dI[s] = ((s == 0) ? t0prev : A[s - 1]) - IGEN;
             mcS[s] = dI[s];
             u0[s] = dI[s];                                        // its up term at row 2
-            if (j0 + s == 1) mcS[s] = pk1(NW16_BIG);             // mc[0] is never updated (:476)
+            if (j0 + s == 1) mcS[s] = pk1(NW16_BIG) ^ NW16_H;            // mc[0] is never updated (:476)
         }
         uint32_t I1 = t0prev, I2 = t0prev;
         uint32_t outT = A[K - 1], outMS = 0, outL = 0;
         const int tend = xmax - 1 + G;
         xrow = valid[0] ? X8[min(max(1 - gl, 0), xcl)] : 0u;
-        uint32_t bestC = pk1(-NW16_BIG), bestCi = 0, ipk = pk1(1 - gl);
+        uint32_t bestC = pk1(-NW16_BIG) ^ NW16_H, bestCi = 0, ipk = pk1(1 - gl);
         int bestR[2] = {INT_MIN, INT_MIN}, bestRj[2] = {0, 0};
         const uint32_t limp = pk2(xl[0] - 2, xl[1] - 2);
         uint8_t *tb3 = (uint8_t *)tbw;
@@ -343,9 +352,9 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
                 const uint32_t tl = (s == 0) ? sN : cur[s - 1];      // T[i][j-1]
                 const uint32_t sc = wv_perm(NW16_TBL_HI, NW16_TBL_LO, xsel ^ yreg[s]);
                 const uint32_t up = row1 ? NBIG : u0[s];
-                const uint32_t lu = pk_max(l0, up);
-                uint32_t v = pk_add(pk_max(d0, lu), sc);
-                if (s == 0) v = leadc0 ? sc : v;                      // column 0 (:426)
+                const uint32_t lu = pk_maxu(l0, up);
+                uint32_t v = pk_add(pk_maxu(d0, lu), sc);
+                if (s == 0) v = leadc0 ? (sc ^ NW16_H) : v;                      // column 0 (:426)
                 cur[s] = pre ? own[s] : v;
                 // move bits: signs of (d0 - lu) [not diagonal] and (l0 - up) [up > left] (:457-472)
                 // (sign-replicating selectors 8-11: bytes 0xFF / 0x00, no shift before packing)
@@ -353,13 +362,13 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
                 // column max of column j-1 over rows <= i-2, strict > (:476-480), in the
                 // +ig+eg frame: dI[s] = T[i-2][j-1] + ig + eg; the max is the select
                 const uint32_t mU = pk_neg_mask(pk_sub(mcS[s], dI[s]));
-                const uint32_t u0n = pk_add(wv_bfi(mU, dI[s], u0[s]), EG);
+                const uint32_t u0n = wv_bfi(mU, dI[s], u0[s]) - EGN;
                 u0[s] = row1 ? u0[s] : u0n;
                 mcS[s] = wv_bfi(mU, dI[s], mcS[s]);
                 // row state for column j+1: tested on row i, taken from row i-1 (:434-438)
                 const uint32_t mnL = pk_neg_mask(pk_sub(tl, mfS));   // 0xFFFF: mf kept (not L)
-                dI[s] = pk_add(d0, IGE);                              // this row's; the next row's u2 + ig + eg
-                l0 = wv_bfi(mnL, pk_add(l0, EG), dI[s]);
+                dI[s] = d0 - IGEN;                              // this row's; the next row's u2 + ig + eg
+                l0 = wv_bfi(mnL, l0 - EGN, dI[s]);
                 mfS = wv_bfi(mnL, mfS, d0);
                 if (s == 0) { mfS = leadc0 ? NBIG : mfS; l0 = leadc0 ? NBIG : l0; }   // j = 1: mf = T[i][0]
                 if (!TB) {
@@ -394,7 +403,7 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
                         if (!lact[h] || i != xl[h] - 1) continue;
 #pragma unroll
                         for (int s = 0; s < K; ++s) {
-                            const int j = j0 + s, val = pk_half(cur[s], h);
+                            const int j = j0 + s, val = pk_score(cur[s], h);
                             if (j >= 1 && j < yl[h] && val >= bestR[h]) { bestR[h] = val; bestRj[h] = j; }
                         }
                     }
@@ -475,7 +484,7 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
         for (int h = 0; h < 2; ++h) {
             red[lane * 8 + 4 * h + 0] = bestR[h];
             red[lane * 8 + 4 * h + 1] = bestRj[h];
-            red[lane * 8 + 4 * h + 2] = ownC[h] ? pk_half(bestC, h) : INT_MIN;
+            red[lane * 8 + 4 * h + 2] = ownC[h] ? pk_score(bestC, h) : INT_MIN;
             red[lane * 8 + 4 * h + 3] = pk_half(bestCi, h);
         }
         wv_lds_sync();
@@ -544,18 +553,18 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
                 const uint32_t tl = (s == 0) ? sN : cur[s - 1];
                 const uint32_t sc = wv_perm(NW16_TBL_HI, NW16_TBL_LO, xsel ^ yreg[s]);
                 const uint32_t up = MASK ? wv_bfi(r1, NBIG, u0[s]) : u0[s];
-                const uint32_t lu = pk_max(l0, up);
-                uint32_t v = pk_add(pk_max(d0, lu), sc);
-                if (s == 0) v = leadc0 ? sc : v;
+                const uint32_t lu = pk_maxu(l0, up);
+                uint32_t v = pk_add(pk_maxu(d0, lu), sc);
+                if (s == 0) v = leadc0 ? (sc ^ NW16_H) : v;
                 cur[s] = MASK ? wv_bfi(pm, own[s], v) : v;
                 const uint32_t P2 = wv_perm(pk_sub(l0, up), pk_sub(d0, lu), 0x0B0A0908u);
                 const uint32_t mU = pk_neg_mask(pk_sub(mcS[s], dI[s]));
-                const uint32_t u0n = pk_add(wv_bfi(mU, dI[s], u0[s]), EG);
+                const uint32_t u0n = wv_bfi(mU, dI[s], u0[s]) - EGN;
                 u0[s] = MASK ? wv_bfi(r1, u0[s], u0n) : u0n;
                 mcS[s] = wv_bfi(mU, dI[s], mcS[s]);
                 const uint32_t mnL = pk_neg_mask(pk_sub(tl, mfS));
-                dI[s] = pk_add(d0, IGE);
-                l0 = wv_bfi(mnL, pk_add(l0, EG), dI[s]);
+                dI[s] = d0 - IGEN;
+                l0 = wv_bfi(mnL, l0 - EGN, dI[s]);
                 mfS = wv_bfi(mnL, mfS, d0);
                 if (s == 0) { mfS = leadc0 ? NBIG : mfS; l0 = leadc0 ? NBIG : l0; }
                 if (s < 8) {

@@ -58,6 +58,10 @@ WV_DEVICE uint32_t pk_u(wv_s2 a) { return __builtin_bit_cast(uint32_t, a); }
 WV_DEVICE uint32_t pk_add(uint32_t a, uint32_t b) { return pk_u(pk_v(a) + pk_v(b)); }          // v_pk_add_u16
 WV_DEVICE uint32_t pk_sub(uint32_t a, uint32_t b) { return pk_u(pk_v(a) - pk_v(b)); }          // v_pk_sub_u16
 WV_DEVICE uint32_t pk_max(uint32_t a, uint32_t b) { return pk_u(__builtin_elementwise_max(pk_v(a), pk_v(b))); }
+typedef unsigned short wv_u2 __attribute__((ext_vector_type(2)));
+WV_DEVICE uint32_t pk_maxu(uint32_t a, uint32_t b) {                                             // v_pk_max_u16
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(wv_u2, a), __builtin_bit_cast(wv_u2, b)));
+}
 // 0xFFFF in each half that is negative.  Opaque on purpose: seen as a sign
 // splat, LLVM turns the bfi/and_or users into per-half v_cmp + v_cndmask.
 WV_DEVICE uint32_t pk_neg_mask(uint32_t a) {
@@ -187,6 +191,10 @@ inline uint32_t pk_map(uint32_t a, uint32_t b, int (*f)(int, int)) {
 inline uint32_t pk_add(uint32_t a, uint32_t b) { return pk_map(a, b, [](int x, int y) { return x + y; }); }
 inline uint32_t pk_sub(uint32_t a, uint32_t b) { return pk_map(a, b, [](int x, int y) { return x - y; }); }
 inline uint32_t pk_max(uint32_t a, uint32_t b) { return pk_map(a, b, [](int x, int y) { return x > y ? x : y; }); }
+inline uint32_t pk_maxu(uint32_t a, uint32_t b) {
+    const uint32_t lo = std::max(a & 0xFFFFu, b & 0xFFFFu), hi = std::max(a >> 16, b >> 16);
+    return lo | (hi << 16);
+}
 inline uint32_t pk_neg_mask(uint32_t a) { return pk_map(a, 0, [](int x, int) { return x < 0 ? -1 : 0; }); }
 inline uint32_t wv_shift_in(uint32_t w, bool c) { return (w << 1) | (c ? 1u : 0u); }
 inline uint32_t wv_and_or(uint32_t m, uint32_t c, uint32_t w) { return (m & c) | w; }
