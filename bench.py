@@ -113,6 +113,9 @@ def parse():
                          "(auto: on for c2 at N=1)")
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo: rehearsal on one card)")
+    ap.add_argument("--dist", action="store_true",
+                    help="initialise torch.distributed (--dist-backend) even at one rank, so the collectives of an "
+                         "N-rank run (RCCL all-reduce of the clock and counters) execute next to the library's streams")
     ap.add_argument("--device", type=int, default=None,
                     help="HIP device of this rank (default LOCAL_RANK; a fixed value rehearses N ranks on one card)")
     ap.add_argument("--shard", default=None, metavar="R/N",
@@ -161,23 +164,86 @@ def host_cpu():
     return {"model": model, "nproc": nproc, "affinity": aff, "cgroup_quota_cpus": quota, "usable": usable}
 
 
+def visible_gpus():
+    """GPUs this process may use, counted WITHOUT initialising HIP (the rank
+    launcher forks children afterwards): torch.cuda.device_count() does not
+    start the runtime on this image (it reads the KFD topology), and it
+    honours HIP/ROCR/CUDA_VISIBLE_DEVICES."""
+    import torch
+    return torch.cuda.device_count()
+
+
+def launch_ranks(a):
+    """`--gpus N` without a launcher: start N rank processes of this script,
+    one per GPU -- the fan-out IMSAME does with pthread_create over read
+    ranges (IMSAME.c:414-467), one process per GPU here -- with RANK,
+    LOCAL_RANK, WORLD_SIZE, MASTER_ADDR/PORT set as torch.distributed.run
+    sets them.  The parent never touches the GPU (children are fresh
+    processes, not forks of a HIP process).  Rank 0 prints the line (the
+    children share this stdout); a failing rank stops the others and its exit
+    status becomes ours."""
+    import signal
+    import socket
+    import subprocess
+    if a.device is None:
+        n = visible_gpus()
+        if a.gpus > n:
+            sys.exit(f"bench.py: --gpus {a.gpus} but {n} GPU(s) visible (--device D rehearses N ranks on one card)")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus),
+                   LOCAL_WORLD_SIZE=str(a.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   IMSAME_BENCH_LAUNCHED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                r = p.poll()
+                if r is None:
+                    continue
+                live.remove(p)
+                if r != 0 and rc == 0:
+                    rc = r if r > 0 else 128 - r
+                    for q in live:                       # the collectives would wait for the dead rank
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
+
+
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {a.gpus}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     gpu = local if a.device is None else a.device
-    if world > 1:
+    backend = None
+    if world > 1 or a.dist:
         import torch
         import torch.distributed as dist
-        if a.dist_backend == "nccl":
+        backend = a.dist_backend
+        if backend == "nccl":
             torch.cuda.set_device(gpu)
             dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
         else:
             dist.init_process_group("gloo")
     import imsame_amd
-    from imsame_amd.dist import shard_range
+    from imsame_amd.dist import shard_range, hip_runtimes
     from tests import synth
 
     # synthetic inputs: the reference is replicated; strong scaling = ONE query
@@ -337,12 +403,19 @@ def main():
                        "reads": a.reads, "reads_per_gpu": hi - lo, "read_len": a.read_len, "ref_bp": a.ref_bp,
                        "record_bp": a.record_bp, "n_threads_semantic": a.n_threads,
                        "parallelism": f"dp{world} (read shards, replicated index)"
+                       + (f"; collectives: {'RCCL' if backend == 'nccl' else backend} over {world} rank(s)"
+                          if backend else "")
                        + ("" if world == 1 or a.dist_backend == "nccl" else
                           f"; REHEARSAL: {a.dist_backend} collectives, device {gpu} shared by all ranks")},
             "roofline": roofline,
             "parity": parity,
             "cpu_baseline": cpu,
             "e2e": e2e,
+            "ranks": {"world": world, "backend": ("rccl" if backend == "nccl" else backend),
+                      "launcher": "bench.py" if os.environ.get("IMSAME_BENCH_LAUNCHED") else
+                                  ("torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ or world > 1
+                                   else None),
+                      "hip_runtime": hip_runtimes()},
             "detail": {"accepted_reads": accepted_all, "index_build_s": round(t_index, 3),
                        "rounds": last["rounds"], "nw_per_read": round(last["n_nw"] / max(hi - lo, 1), 4),
                        "hits_per_read": round(last["n_hits"] / max(hi - lo, 1), 2),

@@ -22,6 +22,16 @@ import numpy as np
 from . import abi
 from .abi import Params, Stats, RESULT_DTYPE, PARITY_FIELDS  # noqa: F401
 
+# Lanes: the library runs one alignment lane per two hardware queues, read
+# from GPU_MAX_HW_QUEUES as the HIP runtime saw it (imsame_dev.hip:hw_queues;
+# the library itself never sets it).  HIP's default is 4 (2 lanes, where 8
+# queues give 4 lanes and 1-2 % more at C2), so a Python host that has not
+# chosen asks for 8 here -- effective only when nothing in this process has
+# started HIP yet (the CLI and bench.py set it at start-up for the same
+# reason).  Results never depend on it.
+if not os.environ.get("GPU_MAX_HW_QUEUES"):
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DEV = os.environ.get("IMSAME_LIB_DEV") or os.path.join(HERE, "lib", "libimsame_dev.so")
 LIB_HOST = os.path.join(HERE, "lib", "libimsame_host.so")

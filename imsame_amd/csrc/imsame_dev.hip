@@ -997,17 +997,28 @@ static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, 
     // the queue is empty).  The partitions must hold the kernel's full
     // residency, so per_cu is the true occupancy here.
     pl->np = pl->pk && rounds && nw_xcc_check(c) && nw16_np_part_cu(c) > 0;
-    if (!pl->np) per_cu = std::min(per_cu, 8);
     int part_cu = per_cu;                   // np: blocks per CU the XCD partitions hold
     if (pl->np) {
         // One slot layout for both column forms: round 1b runs two packed
         // launches of a lane at once (align_one), possibly of different
         // forms, on one arena and bitmap.  Strides of the larger form;
         // partitions for the larger residency without LDS (LDS only lowers it).
-        np_strides(xcap, &pl->tb_dw, &pl->ck_dw);
         part_cu = nw16_np_part_cu(c);
-        if (part_cu < per_cu) pl->np = false;   // (cannot happen: the bound is without LDS)
+        uint64_t tb_dw = 0, ck_dw = 0;
+        np_strides(xcap, &tb_dw, &ck_dw);
+        const uint32_t words = (uint32_t)((((uint64_t)c->ncu / 8) * part_cu * wpb + 31) / 32);
+        const uint64_t ns = (uint64_t)8 * 32 * words;
+        // the arena np_prepare actually holds (it skips the allocation when
+        // free HBM is short, e.g. after a long-read call grew c->tb): a plan
+        // is non-persistent only if its slots exist, so two launches planned
+        // np (round 1b) never fall back to one persistent arena together
+        const imsame_ctx *ao = c->np_owner ? c->np_owner : c;
+        if (part_cu < per_cu || ao->np_tb.cap < ns * tb_dw * 4 || ao->np_ck.cap < ns * ck_dw * 4 ||
+            ao->slotbits.cap < (uint64_t)8 * words * 4)
+            pl->np = false;
+        else { pl->tb_dw = tb_dw; pl->ck_dw = ck_dw; }
     }
+    if (!pl->np) { per_cu = std::min(per_cu, 8); part_cu = per_cu; }
     const uint32_t cpw = pl->pk ? 2 * pl->GPW : pl->GPW;            // candidates per wave pull
     const uint64_t waves_needed = (ncand + cpw - 1) / cpw;
     pl->slot_words = (uint32_t)((((uint64_t)c->ncu / 8) * part_cu * wpb + 31) / 32);
@@ -1364,7 +1375,10 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     // profiles/r3l64/)
     const uint64_t seed_l64_below = l64_env ? strtoull(l64_env, nullptr, 10) : 8192;
     const char *r1b_env = getenv("IMSAME_ROUND1B");
-    const bool r1b_on = !(r1b_env && !atoi(r1b_env)) && ycap <= short_y && !crow && !poison_on();
+    // (on under IMSAME_DEBUG_POISON too: the poisoned suite must run the
+    // concurrent path -- two streams on the shared arena, slot bitmap,
+    // C_PATHS / C_FLAGS counters; POISON_SYNC waits for one stream only)
+    const bool r1b_on = !(r1b_env && !atoi(r1b_env)) && ycap <= short_y && !crow;
     uint32_t nact = n;
     uint32_t *act = c->act0.as<uint32_t>(), *nxt = c->act1.as<uint32_t>();
     while (nact) {
@@ -1457,7 +1471,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
                            c->cur_p.as<uint64_t>(), next,
                            (uint32_t *)(ctr + nnext_slot), (unsigned long long *)(ctr + C_CELLS),
                            (unsigned long long *)(ctr + C_NACC), (unsigned long long *)(ctr + C_ERR),
-                           c->db_start.as<uint64_t>()};
+                           c->db_start.as<uint64_t>(), ctr + C_FLAGS};
             update_kernel<<<nblk(nc, 256), 256, 0, ss>>>(U);
             POISON_SYNC(ss, "update_kernel", c);
             HIPCHK(hipGetLastError());
@@ -1526,7 +1540,10 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
             bool a_done = n1 == 0;
             if (nb) {
                 if ((rc = plan_nw(c, short_y, xcap, nb, p, c->q_len_mult, &plb))) return rc;
-                const bool same = plb.np && plb.slot_words == pla.slot_words && plb.tb_dw == pla.tb_dw &&
+                // N1a's launch_nw may have fallen back to a persistent launch on
+                // this lane's own arena: then N1b must wait for it (pla.np is
+                // what it ran with)
+                const bool same = pla.np && plb.np && plb.slot_words == pla.slot_words && plb.tb_dw == pla.tb_dw &&
                                   plb.ck_dw == pla.ck_dw && plb.bnd_dw == pla.bnd_dw && plb.max_blocks == pla.max_blocks;
                 if (!same && !a_done) {                               // not N1a's arena layout: after it
                     if ((rc = nw_launch_done(c, 0, n1, &msa))) return rc;
@@ -1755,7 +1772,7 @@ static int align_impl(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint6
     while (nl > 1 && n < (uint64_t)nl * lane_min) --nl;
     if (c->is_sub || c->use_wcap || ymax > (uint64_t)NW_W / 2) nl = 1;
     if (nl == 1) {
-        imsame_stats s1;
+        imsame_stats s1{};
         int rc = align_one(c, read_from, read_to, n_threads_semantic, p, res, paths, paths_cap, paths_used, &s1);
         s1.ms_nw_busy = union_ms(c->nw_iv);
         span_ms(c->nw_iv, &s1.ms_nw_first, &s1.ms_nw_last);
@@ -2167,6 +2184,10 @@ extern "C" int imsame_dev_revcomp(imsame_ctx *c, const uint8_t *in, uint64_t n, 
     HIPCHK(hipMemcpyAsync(&nr, gpos + n, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     if (nr == 0) return IMSAME_OK;
+    // output offsets and sizes are u32: a record's output is at most its input
+    // bytes + one '\n' (headers copied, bodies lose their newlines), so the
+    // whole output is < n + nr; refuse what could wrap instead of wrapping
+    if ((uint64_t)n + nr >= 0xFFFFFFF0ull) return IMSAME_E_ARG;
     if (c->rc_c.ensure((uint64_t)nr * 4 * 5 + 64)) return IMSAME_E_OOM;
     if ((rc = c->rc_c.poison(s)) || (rc = c->rc_out.poison(s))) return rc;
     uint32_t *off = c->rc_c.as<uint32_t>(), *hend = off + nr, *bend = hend + nr, *szr = bend + nr, *oo = szr + nr;

@@ -731,10 +731,10 @@ void nw16_kernel(NwLaunch P) {
     uint32_t slot;
     if (P.slot_bits) {                          // non-persistent: one task, a slot of this XCD
         slot = nw_slot_claim(P, lane);
-        if (slot == ~0u) {                      // never (partitions hold the residency); the queue
-            if (lane == 0) wv_atomic_or(P.flags, 4u);     // is drained by the other waves
-            return;
-        }
+        if (slot == ~0u) {                      // never (partitions hold the residency).  This wave's
+            if (lane == 0) wv_atomic_or(P.flags, 4u);     // task is NOT run by anyone: the flag makes the
+            return;                             // update_kernel behind the launch consume nothing and
+        }                                       // the host fail the call (align_one)
     } else {
         slot = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + wib);   // wave-uniform
     }

@@ -565,6 +565,7 @@ struct UpdLaunch {
     unsigned long long *cells; unsigned long long *nacc;
     unsigned long long *err;
     const uint64_t *db_start;
+    const uint64_t *flags = nullptr;       // NW launch flags (C_FLAGS): bit 2 = a wave ran no task
 };
 
 // Per read (run by its first candidate): the first accepted candidate in
@@ -643,6 +644,9 @@ __global__ __launch_bounds__(256) void seed_kernel(SeedLaunch S) {
 __global__ void update_kernel(UpdLaunch U) {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t cells = 0, acc = 0;
+    // a non-persistent NW wave that found no arena slot left its candidates'
+    // rows unwritten: consume none of them (the host fails the call)
+    if (U.flags && (__hip_atomic_load(U.flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 4u)) return;
     if (c < U.n) update_one(U, c, cells, acc);
     if (cells) atomicAdd(U.cells, (unsigned long long)cells);
     if (acc) atomicAdd(U.nacc, (unsigned long long)acc);

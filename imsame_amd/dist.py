@@ -9,6 +9,26 @@ backend, gloo on CPU in the tests).
 import numpy as np
 
 
+def hip_runtimes():
+    """Distinct HIP runtime files mapped into this process (/proc/self/maps).
+    A multi-rank process must hold exactly one: torch's wheel ships
+    libamdhip64 (SONAME libamdhip64.so.7, ROCm 7.0) and is imported first, so
+    libimsame_dev.so's libamdhip64.so.7 dependency resolves to that same
+    object by SONAME.  Loading the library first would map /opt/rocm's 7.2
+    copy, and torch -- which asks for the FILE name libamdhip64.so -- would
+    then map its own next to it: two runtimes in one process."""
+    import os
+    seen = set()
+    try:
+        for line in open("/proc/self/maps"):
+            f = line.split()
+            if len(f) >= 6 and os.path.basename(f[5]).startswith("libamdhip64"):
+                seen.add(os.path.realpath(f[5]))
+    except OSError:
+        pass
+    return sorted(seen)
+
+
 def shard_range(n_reads, rank, world):
     """Contiguous [from, to) of rank `rank` out of `world`."""
     return (n_reads * rank) // world, (n_reads * (rank + 1)) // world

@@ -846,3 +846,81 @@ def test_lanes_equal_one_lane(dev, monkeypatch):
         t2, _ = render(X, Y, r2, p2[r2["path_off"]:r2["path_off"] + r2["path_len"]])
         t1, _ = render(X, Y, r1, p1[r1["path_off"]:r1["path_off"] + r1["path_len"]])
         assert t2 == t1, k
+
+
+def test_short_call_after_long_call_arena(oracle):
+    """A long-read call grows the context's persistent traceback arena to most
+    of HBM, so the shared non-persistent arena of a following short-read call
+    cannot be allocated (np_prepare skips it).  Every launch of that call must
+    then be PLANNED persistent (plan_nw checks the arena the context holds),
+    and round 1b -- two concurrent launches -- must not run on one persistent
+    arena (both fell back to it and shared its slots).  Rows equal
+    the oracle's."""
+    with Device(0) as d:
+        ref_l, rst_l = synth.make_reference_arr(12_001 * 20, 12_001, seed=48)
+        ql, qls = synth.make_long_reads_arr(ref_l, 4, 10_000, seed=49)
+        d.index(ref_l, rst_l)
+        d.set_query(ql, qls)
+        _, _, stl = d.align(n_threads=2, params=d.params(max_read_size=12_001))
+        assert stl.n_nw > 0
+        ref, rst = synth.make_reference_arr(2_000_000, 2_000, seed=42)
+        q, qs = synth.make_reads_arr(ref, 12_000, 150, seed=43)
+        d.index(ref, rst)
+        d.set_query(q, qs)
+        res, _, st = d.align(n_threads=16)
+        rc, exp, _ = oracle.align(ref, rst, q, qs, None, 16)
+        assert rc == 0
+        assert not _cmp(res, exp), _cmp(res, exp)
+        assert st.launch_np == 0, hex(st.launch_np)      # no shared arena: every launch persistent
+
+
+def test_bench_launches_ranks_itself():
+    """`bench.py --gpus 2` with no launcher starts its two ranks itself (the
+    driver's form of the N-GPU run), here as a gloo rehearsal on one card: the
+    line says n_gpus 2, and the shards' accepted reads sum to a one-rank run's."""
+    import json
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    base = [sys.executable, "-u", "bench.py", "--steps", "1", "--warmup", "0", "--cpu-sample", "0", "--e2e", "off",
+            "--reads", "100000"]
+    lines = {}
+    for n in (2, 1):
+        extra = ["--gpus", str(n)] + (["--dist-backend", "gloo", "--device", "0"] if n > 1 else [])
+        p = subprocess.run(base + extra, cwd=repo, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                           timeout=900)
+        assert p.returncode == 0, p.stderr[-3000:].decode(errors="replace")
+        lines[n] = json.loads([x for x in p.stdout.decode().splitlines() if x.startswith("{")][-1])
+    two, one = lines[2], lines[1]
+    print(json.dumps({"two": {k: two[k] for k in ("value", "n_gpus", "ranks")}, "one_value": one["value"]}))
+    assert two["n_gpus"] == 2 and two["ranks"]["world"] == 2 and two["ranks"]["launcher"] == "bench.py"
+    assert two["ranks"]["backend"] == "gloo" and len(two["ranks"]["hip_runtime"]) == 1
+    assert two["detail"]["accepted_reads"] == one["detail"]["accepted_reads"] > 80_000
+    assert two["config"]["reads_per_gpu"] == 50_000
+
+
+def test_rccl_world1_next_to_library():
+    """A world-size-1 RCCL process group with GPU-tensor all-reduces and the
+    database-shard merge (imsame_amd.dist) in the same process as the
+    library's streams: one HIP runtime mapped, the merge equals the rows,
+    and an alignment after the collectives gives the same rows again."""
+    import json
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-u", "-m", "tests.rccl_run"], cwd=repo, stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:].decode(errors="replace")
+    d = json.loads(p.stdout.decode().strip().splitlines()[-1])
+    print(d)
+    assert d["backend"] == "nccl" and len(d["hip_runtime"]) == 1, d
+    assert d["merge_equal"] and d["rerun_equal"], d
+    assert d["all_reduce"] == [d["accepted"], d["reads"]] and d["all_reduce_max"] == [1.5], d
+    # the bench's own one-rank RCCL form (--dist): its line names the backend
+    p = subprocess.run([sys.executable, "-u", "bench.py", "--gpus", "1", "--dist", "--steps", "1", "--warmup", "0",
+                        "--cpu-sample", "0", "--e2e", "off", "--reads", "50000"], cwd=repo, stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:].decode(errors="replace")
+    line = json.loads([x for x in p.stdout.decode().splitlines() if x.startswith("{")][-1])
+    print(line["ranks"])
+    assert line["ranks"]["backend"] == "rccl" and line["ranks"]["world"] == 1
+    assert len(line["ranks"]["hip_runtime"]) == 1 and line["detail"]["accepted_reads"] > 40_000
