@@ -237,6 +237,13 @@ def main():
         import torch
         import torch.distributed as dist
         backend = a.dist_backend
+        if world == 1 and "RANK" not in os.environ:          # --dist at one rank, no launcher
+            import socket
+            s_ = socket.socket()
+            s_.bind(("127.0.0.1", 0))
+            os.environ.update(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
+                              MASTER_PORT=str(s_.getsockname()[1]))
+            s_.close()
         if backend == "nccl":
             torch.cuda.set_device(gpu)
             dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))

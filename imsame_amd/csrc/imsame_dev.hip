@@ -1081,6 +1081,9 @@ static int nw_launch_done(imsame_ctx *c, int qi, uint32_t n, double *ms) {
 // probe failed or the free memory less 8 GB cannot hold it.
 static int np_prepare(imsame_ctx *o, uint32_t xcap) {
     if (!nw_xcc_check(o) || nw16_np_part_cu(o) < 1) return 0;
+    // test hook: behave as if free HBM could not hold the arena (the state a
+    // long-read call that grew the persistent arena leaves behind)
+    if (const char *sk = getenv("IMSAME_DEBUG_NP_SKIP")) if (atoi(sk)) return 0;
     const uint32_t words = (uint32_t)((((uint64_t)o->ncu / 8) * nw16_np_part_cu(o) * 4 + 31) / 32);
     const uint64_t ns = (uint64_t)8 * 32 * words, nbits = (uint64_t)8 * words * 4;
     uint64_t tb_dw = 0, ck_dw = 0;
@@ -2148,6 +2151,12 @@ extern "C" int imsame_dev_nw_pairs(imsame_ctx *c, const uint8_t *xs, const uint6
     uint64_t hc[C_NSLOTS];
     HIPCHK(hipMemcpyAsync(hc, ctr, C_NSLOTS * 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    if (getenv("IMSAME_NW_PROF") && pl.pk) {  // diagnostics (scripts/micro/nw16_loop.py): raw phase wave-cycles
+        fprintf(stderr, "[nwprof-raw] blocks %u G %d GPW %d k %d steps %d cand %llu setup %llu sweep1 %llu reduce %llu "
+                "sweep2 %llu walk %llu ms %.4f\n", pl.blocks, pl.G, pl.GPW, pl.k, pl.steps, (unsigned long long)npairs,
+                (unsigned long long)hc[C_PROF], (unsigned long long)hc[C_PROF + 1], (unsigned long long)hc[C_PROF + 2],
+                (unsigned long long)hc[C_PROF + 3], (unsigned long long)hc[C_PROF + 4], ms);
+    }
     int ret = IMSAME_OK;
     if (p->want_paths) {
         if (paths_used) *paths_used = (uint32_t)hc[C_PATHS];

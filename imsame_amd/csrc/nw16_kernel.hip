@@ -76,9 +76,18 @@
 #define NW16_K   10               // columns per lane (the full-chip launches)
 #define NW16_K5  5                // columns per lane of the latency-bound launches (nw16_k)
 #define NW16_BIG 16384
-#define NW16_CK  24               // checkpoint interval of the first sweep (steps, even: the rotation period)
-// dwords of wave state per lane in a checkpoint; traceback dwords per lane per step
-__host__ __device__ constexpr int nw16_nst(int K) { return 5 * K + 5; }
+// Checkpoint interval of the first sweep (steps; even: the rotation period;
+// <= 32: nw16_fits bounds the rows a second sweep runs past the first by
+// NW16_CK + G <= 64).  32 (round 3: 24) with the checkpoint 4K+5 dwords (dI is
+// recomputed on restore): 0.46 -> 0.28 B/cell of checkpoint writes at C2 for
+// ~4 more second-sweep rows per half on average.
+#ifndef NW16_CK
+#define NW16_CK  32
+#endif
+static_assert(NW16_CK % 2 == 0 && NW16_CK <= 32, "NW16_CK: even, <= 32 (nw16_fits)");
+// dwords of wave state per lane in a checkpoint (A, B, mcS, u0 per column; I1,
+// I2, outT, outMS, outL); dI is a function of A and I2 there (save())
+__host__ __device__ constexpr int nw16_nst(int K) { return 4 * K + 5; }
 __host__ __device__ constexpr int nw16_nrec(int K) { return K > 8 ? 3 : 2; }
 #define NW16_NOROW INT32_MIN      // cand_row: no prediction
 #define NW16_WIN_UP 32            // window rows above the predicted first row
@@ -95,7 +104,7 @@ __host__ static inline bool nw16_fits(int64_t ig, int64_t eg, uint64_t xcap, uin
     if (aig > 8191 || aeg > 8191) return false;
     // |T| <= 4*ycols; l0 >= -T - |ig| - |eg|*ycols; u0 drifts at most over
     // xcap + 64 rows (lockstep garbage rows included -- a second sweep runs at
-    // most NW16_CK + G <= 24 + 32 rows past the first one, G <= 32 at K = 5)
+    // most NW16_CK + G <= 32 + 32 rows past the first one, G <= 32 at K = 5)
     // and takes u2 + ig + 2eg.  ycols at K = 10 bounds ycols at K = 5.
     const uint64_t R = 4 * ycols + aig + aeg * (xcap + 64 + ycols + 2) + 16;
     return R <= 8191;
@@ -417,17 +426,20 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
         };
         // Checkpoint m = the state before step 1 + m*NW16_CK, where the roles
         // are (cur, own) = (A, B), (in0, in1) = (I2, I1); register r of lane l
-        // at ckw[(m*NST + r)*64] (coalesced).
+        // at ckw[(m*NST + r)*64] (coalesced).  dI is not stored: the step
+        // before a checkpoint ran with (own, in1) = (A, I2) and set dI[s] =
+        // d0 - IGEN with d0 = (s ? A[s-1] : I2), neither of which it changed
+        // (it wrote B and I1), so the restore recomputes it.
         constexpr bool TB1 = !TWO;                // the first sweep writes traceback only in one-pass mode
         auto save = [&](const int m) {
             uint32_t *p = ckw + (uint32_t)m * (NST * 64u);
 #pragma unroll
             for (int s = 0; s < K; ++s) {
-                p[s * 64] = A[s]; p[(K + s) * 64] = B[s]; p[(2 * K + s) * 64] = dI[s];
-                p[(3 * K + s) * 64] = mcS[s]; p[(4 * K + s) * 64] = u0[s];
+                p[s * 64] = A[s]; p[(K + s) * 64] = B[s];
+                p[(2 * K + s) * 64] = mcS[s]; p[(3 * K + s) * 64] = u0[s];
             }
-            p[5 * K * 64] = I1; p[(5 * K + 1) * 64] = I2;
-            p[(5 * K + 2) * 64] = outT; p[(5 * K + 3) * 64] = outMS; p[(5 * K + 4) * 64] = outL;
+            p[4 * K * 64] = I1; p[(4 * K + 1) * 64] = I2;
+            p[(4 * K + 2) * 64] = outT; p[(4 * K + 3) * 64] = outMS; p[(4 * K + 4) * 64] = outL;
         };
         int nextck = 1 + NW16_CK, mck = 1;
         auto ck = [&](const int t) { if (TWO && t == nextck) { save(mck); ++mck; nextck += NW16_CK; } };
@@ -600,11 +612,13 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
                 auto ld = [&](const int r) { return wv_bfi(0x0000FFFFu, pa[r * 64], pb[r * 64]); };
 #pragma unroll
                 for (int s = 0; s < K; ++s) {
-                    A[s] = ld(s); B[s] = ld(K + s); dI[s] = ld(2 * K + s);
-                    mcS[s] = ld(3 * K + s); u0[s] = ld(4 * K + s);
+                    A[s] = ld(s); B[s] = ld(K + s);
+                    mcS[s] = ld(2 * K + s); u0[s] = ld(3 * K + s);
                 }
-                I1 = ld(5 * K); I2 = ld(5 * K + 1);
-                outT = ld(5 * K + 2); outMS = ld(5 * K + 3); outL = ld(5 * K + 4);
+                I1 = ld(4 * K); I2 = ld(4 * K + 1);
+                outT = ld(4 * K + 2); outMS = ld(4 * K + 3); outL = ld(4 * K + 4);
+#pragma unroll
+                for (int s = 0; s < K; ++s) dI[s] = (s ? A[s - 1] : I2) - IGEN;    // (save())
                 xrow = (X8[min(max(t0h[0] - gl, 0), xcl)] & 3u) | (X8[min(max(t0h[1] - gl, 0), xcl)] & 0xCu);
             }
             // rows <= 1 need the masked step: while tau <= G - min(t0h) (wave-uniform bound)

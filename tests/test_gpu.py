@@ -848,30 +848,29 @@ def test_lanes_equal_one_lane(dev, monkeypatch):
         assert t2 == t1, k
 
 
-def test_short_call_after_long_call_arena(oracle):
-    """A long-read call grows the context's persistent traceback arena to most
-    of HBM, so the shared non-persistent arena of a following short-read call
-    cannot be allocated (np_prepare skips it).  Every launch of that call must
-    then be PLANNED persistent (plan_nw checks the arena the context holds),
-    and round 1b -- two concurrent launches -- must not run on one persistent
-    arena (both fell back to it and shared its slots).  Rows equal
-    the oracle's."""
-    with Device(0) as d:
-        ref_l, rst_l = synth.make_reference_arr(12_001 * 20, 12_001, seed=48)
-        ql, qls = synth.make_long_reads_arr(ref_l, 4, 10_000, seed=49)
-        d.index(ref_l, rst_l)
-        d.set_query(ql, qls)
-        _, _, stl = d.align(n_threads=2, params=d.params(max_read_size=12_001))
-        assert stl.n_nw > 0
-        ref, rst = synth.make_reference_arr(2_000_000, 2_000, seed=42)
-        q, qs = synth.make_reads_arr(ref, 12_000, 150, seed=43)
-        d.index(ref, rst)
-        d.set_query(q, qs)
-        res, _, st = d.align(n_threads=16)
-        rc, exp, _ = oracle.align(ref, rst, q, qs, None, 16)
-        assert rc == 0
-        assert not _cmp(res, exp), _cmp(res, exp)
-        assert st.launch_np == 0, hex(st.launch_np)      # no shared arena: every launch persistent
+def test_short_call_without_shared_arena(oracle, monkeypatch):
+    """When the shared non-persistent NW arena cannot be allocated (free HBM
+    short of it: e.g. after a long-read call grew the context's persistent
+    traceback arena to most of HBM; IMSAME_DEBUG_NP_SKIP simulates it), every
+    launch must be PLANNED persistent (plan_nw checks the arena the context
+    holds), and round 1b's two concurrent launches must not both fall back to
+    the one persistent arena (they shared its slots).  Rows equal
+    the oracle's; the same call with the arena runs non-persistent launches."""
+    ref, rst = synth.make_reference_arr(2_000_000, 2_000, seed=42)
+    q, qs = synth.make_reads_arr(ref, 12_000, 150, seed=43)
+    rc, exp, _ = oracle.align(ref, rst, q, qs, None, 16)
+    assert rc == 0
+    for skip in ("1", "0"):
+        monkeypatch.setenv("IMSAME_DEBUG_NP_SKIP", skip)
+        with Device(0) as d:
+            d.index(ref, rst)
+            d.set_query(q, qs)
+            res, _, st = d.align(n_threads=16)
+        assert not _cmp(res, exp), (skip, _cmp(res, exp))
+        if skip == "1":
+            assert st.launch_np == 0, hex(st.launch_np)   # no shared arena: every launch persistent
+        else:
+            assert st.launch_np != 0                      # (the box has the XCD probe: np launches)
 
 
 def test_bench_launches_ranks_itself():
