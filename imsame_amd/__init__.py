@@ -34,7 +34,7 @@ if not os.environ.get("GPU_MAX_HW_QUEUES"):
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DEV = os.environ.get("IMSAME_LIB_DEV") or os.path.join(HERE, "lib", "libimsame_dev.so")
-LIB_HOST = os.path.join(HERE, "lib", "libimsame_host.so")
+LIB_HOST = os.environ.get("IMSAME_LIB_HOST") or os.path.join(HERE, "lib", "libimsame_host.so")
 CLI = os.path.join(HERE, "bin", "imsame")
 FLAG_NW32 = 1          # imsame_params.flags: force the int32 NW kernel (include/imsame_dev.h)
 FLAG_NW16 = 2          # ... or the packed int16 kernel for every launch it fits, however small

@@ -124,7 +124,9 @@ __device__ __forceinline__ void nw_sweep(const NwLaunch &P, const NwCand &cd, ui
     }
     // row 0 (:404-413): T[0][j] = s(X0,Yj); mc[j] = (T[0][j], row 0)
     const int x0 = cvalid ? (int)cd.X[0] : 0;
-    const int yprev = (cvalid && j0 > 0) ? (int)cd.Y[j0 - 1] : 0;
+    // (a lane wholly past the read's end computes garbage columns only: it must
+    // not read past the read -- found by the ASan build of the emulator)
+    const int yprev = (cvalid && j0 > 0 && j0 <= ylen) ? (int)cd.Y[j0 - 1] : 0;
     const int t0prev = (x0 == yprev) ? 4 : -4;
     // Three rotating row buffers (cur / own = row i-1 / own2 = row i-2), all
     // starting as row 0.  A lane repeats row 0 until its first row and runs

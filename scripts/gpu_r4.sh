@@ -70,10 +70,11 @@ run_step() {   # $1 = step, $2 = output suffix
          done ;;
     # nw16 first-sweep loop ceiling (scripts/micro/nw16_loop.py); MICRO_VALU / MICRO_WPS from the env
     micro) timeout -k 10 600 python -u scripts/micro/nw16_loop.py --valu ${MICRO_VALU:-351} \
-             --waves-per-simd ${MICRO_WPS:-4} --out $O/micro_${TAG}$X.json > $O/micro_${TAG}$X.log 2>&1
+             ${MICRO_WPS:+--waves-per-simd $MICRO_WPS} --out $O/micro_${TAG}$X.json > $O/micro_${TAG}$X.log 2>&1
            ok_or_stop $? micro$X ;;
-    benchab) timeout -k 10 600 python -u bench.py $BQ --steps 10 --warmup 2 > $O/benchab_${TAG}$X.json \
-           2> $O/benchab_${TAG}$X.err; ok_or_stop $? benchab$X ;;
+    benchab) local Y=$X k=1; while [ -e $O/benchab_${TAG}$Y.json ]; do k=$((k+1)); Y=${X}_$k; done
+           timeout -k 10 600 python -u bench.py $BQ --steps 10 --warmup 2 > $O/benchab_${TAG}$Y.json \
+           2> $O/benchab_${TAG}$Y.err; ok_or_stop $? benchab$Y ;;
     *) echo "unknown step $s" >> $O/steps_${TAG}.txt ;;
   esac
 }

@@ -54,10 +54,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--valu", type=float, required=True, help="VALU instructions per fast-loop iteration (2 steps)")
     ap.add_argument("--pairs", type=int, default=65536)
-    ap.add_argument("--xlen", type=int, default=3000)
+    ap.add_argument("--xlen", type=int, default=2000)      # C2's records (LDS: 4 blocks of 4 waves per CU)
     ap.add_argument("--ylen", type=int, default=150)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--waves-per-simd", type=int, default=4)
+    ap.add_argument("--waves-per-simd", type=float, default=None,
+                    help="resident waves per SIMD (default: the launch's blocks x 4 waves / 1024 SIMDs)")
     ap.add_argument("--out", default=None)
     ap.add_argument("--child", action="store_true")
     a = ap.parse_args()
@@ -79,14 +80,18 @@ def main():
     iters = (a.xlen + G - 1) / 2.0
     tot = sum(r[k] for k in ("setup", "sweep1", "reduce", "sweep2", "walk"))
     cyc_iter = r["sweep1"] / (tasks * iters)
+    if a.waves_per_simd is None:                           # persistent launch: blocks x 4 waves over 1024 SIMDs
+        a.waves_per_simd = min(r["blocks"] * 4, tasks) / 1024.0
     rate = a.waves_per_simd * a.valu / cyc_iter           # wave-instructions per SIMD cycle
+    tot_cyc = sum(r[k] for k in ("setup", "sweep1", "reduce", "sweep2", "walk"))
+    ghz = tot_cyc / (r["blocks"] * 4) / (r["ms"] * 1e-3) / 1e9     # s_memtime ticks per second
     out = {"kernel": "nw16_kernel<10,LAST,TWO>", "what": "first-sweep fast loop, chip full, kernel alone",
            "pairs": int(r["cand"]), "xlen": a.xlen, "ylen": a.ylen, "G": G, "GPW": GPW, "tasks": tasks,
            "valu_per_iteration": a.valu, "waves_per_simd": a.waves_per_simd,
            "cycles_per_iteration_per_wave": round(cyc_iter, 1),
            "cycles_per_valu_per_simd": round(cyc_iter / (a.waves_per_simd * a.valu), 3),
            "simd_valu_rate": round(rate, 4), "mix_ceiling_frac": round(rate / 0.5, 4),
-           "sweep1_share": round(r["sweep1"] / tot, 4), "kernel_ms": r["ms"],
+           "sweep1_share": round(r["sweep1"] / tot, 4), "kernel_ms": r["ms"], "memtime_ghz": round(ghz, 3),
            "cells_per_s": round(a.pairs * a.xlen * a.ylen / (r["ms"] / 1e3), 1),
            "raw": runs}
     s = json.dumps(out, indent=1)

@@ -14,7 +14,7 @@ from imsame_amd.abi import Params, Stats, RESULT_DTYPE
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 EMU_DIR = os.path.join(HERE, "emu")
-LIB = os.path.join(EMU_DIR, "build", "libwave_emu.so")
+LIB = os.environ.get("IMSAME_EMU_LIB") or os.path.join(EMU_DIR, "build", "libwave_emu.so")   # (scripts/sanitize.sh)
 
 
 class Emu:

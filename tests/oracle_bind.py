@@ -12,8 +12,9 @@ from imsame_amd.abi import Params, ReadResult, RESULT_DTYPE
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(REPO, "oracle")
-LIB = os.path.join(ORACLE_DIR, "build", "liboracle.so")
-BIN = os.path.join(ORACLE_DIR, "build", "imsame_oracle")
+# IMSAME_ORACLE_LIB / _BIN: other builds of the same source (scripts/sanitize.sh)
+LIB = os.environ.get("IMSAME_ORACLE_LIB") or os.path.join(ORACLE_DIR, "build", "liboracle.so")
+BIN = os.environ.get("IMSAME_ORACLE_BIN") or os.path.join(ORACLE_DIR, "build", "imsame_oracle")
 
 
 class NwOut(C.Structure):
@@ -42,7 +43,7 @@ class Oracle:
     @classmethod
     def load(cls, build=False):
         if cls._inst is None:
-            if build or not os.path.exists(LIB):
+            if (build and not os.environ.get("IMSAME_ORACLE_LIB")) or not os.path.exists(LIB):
                 build_oracle()
             cls._inst = cls(C.CDLL(LIB))
         return cls._inst
