@@ -75,6 +75,9 @@ run_step() {   # $1 = step, $2 = output suffix
     benchab) local Y=$X k=1; while [ -e $O/benchab_${TAG}$Y.json ]; do k=$((k+1)); Y=${X}_$k; done
            timeout -k 10 600 python -u bench.py $BQ --steps 10 --warmup 2 > $O/benchab_${TAG}$Y.json \
            2> $O/benchab_${TAG}$Y.err; ok_or_stop $? benchab$Y ;;
+    # single-file write rates of this box's TMPDIR (scripts/micro/write_rate.c; host only)
+    wrate) gcc -O2 -pthread -o /tmp/write_rate scripts/micro/write_rate.c && \
+           timeout -k 10 300 /tmp/write_rate ${TMPDIR:-/tmp} 3 > $O/wrate_${TAG}$X.txt 2>&1; ok_or_stop $? wrate$X ;;
     *) echo "unknown step $s" >> $O/steps_${TAG}.txt ;;
   esac
 }
