@@ -1322,7 +1322,11 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     const uint32_t spec_weak = (uint32_t)std::max(1, std::min(SPEC_MAX, sw_env ? atoi(sw_env) : SPEC_WEAK));
     // candidate lists: 2 per read (up to SPEC_MAX for small calls -- long
     // reads, few per call, fill launches by speculating)
-    const uint64_t ccap = std::max<uint64_t>((uint64_t)n * (spec_weak > 1 ? spec_weak + 1 : 2),
+    // (IMSAME_CCAP_MULT: candidates per read the lists hold, default 2 -- round
+    // 1b's speculation width is bounded by the room left after round 1)
+    const char *cm_env = getenv("IMSAME_CCAP_MULT");
+    const uint64_t cmult = cm_env ? (uint64_t)std::max(2, std::min(SPEC_BIG, atoi(cm_env))) : 2u;
+    const uint64_t ccap = std::max<uint64_t>((uint64_t)n * std::max<uint64_t>(spec_weak > 1 ? spec_weak + 1 : 2, cmult),
                                              std::min<uint64_t>((uint64_t)n * SPEC_MAX, 1u << 20));
     if (c->res.ensure((uint64_t)n * 64) || c->cur_p.ensure((uint64_t)n * 8) || c->cur_h.ensure((uint64_t)n * 4) ||
         c->memo.ensure((uint64_t)n * 4 * MEMO) || c->nmemo.ensure(n) || c->rstat.ensure(n) ||
@@ -1381,7 +1385,9 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     // (on under IMSAME_DEBUG_POISON too: the poisoned suite must run the
     // concurrent path -- two streams on the shared arena, slot bitmap,
     // C_PATHS / C_FLAGS counters; POISON_SYNC waits for one stream only)
-    const bool r1b_on = !(r1b_env && !atoi(r1b_env)) && ycap <= short_y && !crow;
+    // (with predicted traceback windows, round 1's launch is ordered by row;
+    // round 1b's candidates carry no prediction and keep their order)
+    const bool r1b_on = !(r1b_env && !atoi(r1b_env)) && ycap <= short_y;
     uint32_t nact = n;
     uint32_t *act = c->act0.as<uint32_t>(), *nxt = c->act1.as<uint32_t>();
     while (nact) {
@@ -1516,7 +1522,9 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
             SeedLaunch Sb = S;
             Sb.active = nxt; Sb.n_active = npz;
             Sb.spec = 1;
-            Sb.spec_weak = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(SPEC_MAX, (ccap - n1) / npz));
+            // up to SPEC_MAX per read, SPEC_BIG where whole-wave groups scan (their lists hold it)
+            Sb.spec_weak = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(pick_L(npz) >= 64 ? SPEC_BIG : SPEC_MAX,
+                                                                              (ccap - n1) / npz));
             Sb.budget = seed_budget(budget1, 2, grow);
             Sb.next = act2; Sb.nnext = (uint32_t *)(ctr + C_NNEXT2);
             Sb.cread = c->cread.as<uint32_t>() + n1; Sb.csid = c->csid.as<uint32_t>() + n1;
@@ -1528,7 +1536,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
             if (n1) {
                 rc = launch_nw(c, pla, c->cread.as<uint32_t>(), c->csid.as<uint32_t>(), n1, c->cout.as<imsame_read_result>(),
                                p->igap, p->egap, p, ymax, xcap, (uint32_t *)(ctr + C_WORK), c->db.as<uint8_t>(),
-                               c->db_start.as<uint64_t>(), qd, qsd, pcap, &msa, nullptr, 0, false);
+                               c->db_start.as<uint64_t>(), qd, qsd, pcap, &msa, crow, 0, false);
                 if (rc) return rc;
                 if ((rc = upd_launch(c->cread.as<uint32_t>(), c->csid.as<uint32_t>(), n1, c->cout.as<imsame_read_result>(),
                                      act2, C_NNEXT2, s))) return rc;

@@ -237,7 +237,9 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
     // imsame_dev.hip:align_one -- speculation from a weak first candidate, candidate capacity
     const char *sw_env = getenv("IMSAME_SPEC_WEAK");
     const uint32_t spec_weak = (uint32_t)std::max(1, std::min(SPEC_MAX, sw_env ? atoi(sw_env) : SPEC_WEAK));
-    const size_t ccap = std::max<size_t>((size_t)n * (spec_weak > 1 ? spec_weak + 1 : 2),
+    const char *cm_env = getenv("IMSAME_CCAP_MULT");
+    const size_t cmult = cm_env ? (size_t)std::max(2, std::min(SPEC_BIG, atoi(cm_env))) : 2u;
+    const size_t ccap = std::max<size_t>((size_t)n * std::max<size_t>(spec_weak > 1 ? spec_weak + 1 : 2, cmult),
                                          std::min<size_t>((size_t)n * SPEC_MAX, 1u << 20));
     std::vector<uint32_t> cur_h(n), memo((size_t)n * MEMO), act(n), nxt(n), act2(n), cr(ccap), cs(ccap), cr2(ccap), cs2(ccap);
     std::vector<uint32_t> cbase(n), ccnt(n), perr(n);
@@ -260,7 +262,7 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
     unsigned long long err = ~0ull, nhits = 0, cells = 0, nacc = 0;
     const uint32_t short_y = std::min<uint32_t>(ycap, NW_W / 2);
     const char *r1b_env = getenv("IMSAME_ROUND1B");
-    const bool r1b_on = !(r1b_env && !atoi(r1b_env)) && ycap <= short_y && !crowp;
+    const bool r1b_on = !(r1b_env && !atoi(r1b_env)) && ycap <= short_y;
     uint32_t nact = n;
     imsame_stats st;
     memset(&st, 0, sizeof st);
@@ -334,14 +336,16 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
             SeedLaunch Sb = S;
             Sb.active = nxt.data(); Sb.n_active = npz;
             Sb.spec = 1;
-            Sb.spec_weak = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(SPEC_MAX, (ccap - n1) / npz));
+            const int Lb = l_env ? atoi(l_env) : seed_lanes(npz);
+            Sb.spec_weak = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(Lb >= 64 ? SPEC_BIG : SPEC_MAX,
+                                                                              (ccap - n1) / npz));
             Sb.budget = seed_budget(budget1, 2);
             Sb.next = act2.data(); Sb.nnext = &nb[2];
             Sb.cread = cr.data() + n1; Sb.csid = cs.data() + n1; Sb.ncand = &nb[0]; Sb.crow = nullptr;
             Sb.ncand2 = &nb[1];
             run_seed(Sb, npz);
             if (nb[1]) return IMSAME_E_STATE;
-            if (n1) nw_upd(cr.data(), cs.data(), n1, o1.data(), short_y, nullptr, act2.data(), &nb[2]);
+            if (n1) nw_upd(cr.data(), cs.data(), n1, o1.data(), short_y, crowp, act2.data(), &nb[2]);
             if (nb[0]) nw_upd(cr.data() + n1, cs.data() + n1, nb[0], o1.data() + n1, short_y, nullptr, act2.data(), &nb[2]);
             g_r1b += npz;
             if (getenv("IMSAME_DEBUG_ROUNDS"))

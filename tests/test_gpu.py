@@ -923,3 +923,35 @@ def test_rccl_world1_next_to_library():
     print(line["ranks"])
     assert line["ranks"]["backend"] == "rccl" and line["ranks"]["world"] == 1
     assert len(line["ranks"]["hip_runtime"]) == 1 and line["detail"]["accepted_reads"] > 40_000
+
+
+def test_c3_shard_of_10m_query(dev, oracle_memo):
+    """BASELINE configs[2] as an 8-GPU rank holds it: reads [0, 1.25M) of a
+    10M-read query, uploaded alone with imsame_dev_set_query_range, aligned
+    with the chunk heads of -n_threads 16 over the WHOLE 10M query (rpt =
+    625,000: a head inside the shard, none at its end) -- not those of a
+    1.25M-read query of its own.  Oracle parity on three windows of the
+    shard: its start, the chunk head at read 625,000, its end.  (50 Mbp
+    database: the semantics under test is the cut; the reads past the shard
+    are filler the device never receives.)"""
+    ref, rst = synth.make_reference_arr(50_000_000, 2_000, seed=42)
+    n_all, n_sh = 10_000_000, 1_250_000
+    q_sh, qs_sh = synth.make_reads_arr(ref, n_sh, 150, seed=44)
+    assert len(q_sh) == 150 * n_sh
+    q = np.empty(150 * n_all, dtype=np.uint8)
+    q[:len(q_sh)] = q_sh
+    q[len(q_sh):] = np.frombuffer(b"ACGT", dtype=np.uint8)[np.arange(len(q) - len(q_sh)) % 4]
+    qs = np.arange(n_all, dtype=np.uint64) * np.uint64(150)
+    dev.index(ref, rst)
+    dev.set_query(q, qs, 0, n_sh)
+    res, _, _ = dev.align(0, n_sh, n_threads=16)
+    assert (res["status"] == 1).mean() > 0.85
+    head = n_all // 16
+    wins = [(0, 1_500), (head - 750, head + 750), (n_sh - 1_500, n_sh)]
+    rc, exp, _ = oracle_memo.align_windows(ref, rst, q, qs, wins, None, 16)
+    assert rc == 0
+    for (a, b), e in zip(wins, exp):
+        assert not _cmp(res[a:b], e), ((a, b), _cmp(res[a:b], e))
+    # the same reads as a 1.25M-read query of their own have other chunk heads
+    # (rpt 78,125): read 78,125 starts a chunk there, not in the 10M query
+    assert n_sh // 16 != head
