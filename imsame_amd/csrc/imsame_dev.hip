@@ -1344,12 +1344,13 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
             if ((rc = b->poison(s))) return rc;
     }
     // predicted rows for the packed kernel's first-sweep traceback windows:
-    // OFF by default (IMSAME_NW_WINDOW=1 turns them on).  Measured at C2 they
-    // cut the NW wave-cycles by 2 % but the whole step by -1..-3 %: the window
-    // steps issue +73 VALU per step and spill (profiles/r2s_ab_*.json), and
-    // the second sweep they replace is only 13 % of the cycles.
+    // ON by default (IMSAME_NW_WINDOW=0 turns them off).  Round 2 measured them
+    // 1-3 % slower (the window steps spilled at 4 waves per SIMD, and round 1b
+    // was off with them, profiles/r2s_ab_*.json); at 3 waves per SIMD (no
+    // spills) and with round 1b they take C2's NW busy time from 113.4 to
+    // 107.4 ms and the step from 119.9 to 113.9 ms (profiles/r4d/).
     const char *win_env = getenv("IMSAME_NW_WINDOW");
-    int32_t *crow = (win_env && atoi(win_env)) ? c->crow.as<int32_t>() : nullptr;
+    int32_t *crow = (win_env && !atoi(win_env)) ? nullptr : c->crow.as<int32_t>();
     // speculation: round 1 emits one candidate per read (most reads accept
     // it); later rounds emit up to SPEC_MAX, bounded by the candidate buffers
     const char *spec_env = getenv("IMSAME_SPEC");

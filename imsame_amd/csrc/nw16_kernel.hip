@@ -728,8 +728,12 @@ __global__ void xcc_probe_kernel(uint32_t *out) {
     if (threadIdx.x == 0) out[blockIdx.x] = nw_xcc_id();
 }
 
+// 3 waves per SIMD (168 VGPRs): at 4 (128) the compiler spills in the sweep
+// loops; the first-sweep loop issues 3.81 vs 3.95 cycles per VALU per SIMD
+// (scripts/micro/nw16_loop.py, profiles/r4c/) and C2 runs 1.5 % faster
+// (profiles/r4c/benchab_*)
 #ifndef NW16_WAVES_PER_EU
-#define NW16_WAVES_PER_EU 4
+#define NW16_WAVES_PER_EU 3
 #endif
 #ifndef NW16_K5_WAVES_PER_EU
 #define NW16_K5_WAVES_PER_EU 5

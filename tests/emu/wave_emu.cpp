@@ -245,7 +245,7 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
     std::vector<uint32_t> cbase(n), ccnt(n), perr(n);
     std::vector<int32_t> crow(ccap);
     const char *win_env = getenv("IMSAME_NW_WINDOW");
-    int32_t *crowp = (win_env && atoi(win_env)) ? crow.data() : nullptr;     // imsame_dev.hip: off by default
+    int32_t *crowp = (win_env && !atoi(win_env)) ? nullptr : crow.data();     // imsame_dev.hip: on by default
     const char *spec_env = getenv("IMSAME_SPEC");
     const uint32_t spec_later = spec_env ? (uint32_t)std::max(1, std::min(SPEC_MAX, atoi(spec_env))) : (uint32_t)SPEC_MAX;
     const char *bud_env = getenv("IMSAME_SEED_BUDGET");

@@ -207,8 +207,7 @@ def test_nw16_two_pass_equals_one_pass(dev, oracle):
 
     # band sizes, and the first sweep's predicted traceback windows off ("nowin")
     for band in (None, "40", "0", "nowin"):
-        if band != "nowin":
-            os.environ["IMSAME_NW_WINDOW"] = "1"      # opt-in (imsame_dev.hip: off by default)
+        os.environ["IMSAME_NW_WINDOW"] = "0" if band == "nowin" else "1"      # (imsame_dev.hip: on by default)
         if band not in (None, "nowin"):
             os.environ["IMSAME_NW_BAND"] = band
         try:

@@ -199,7 +199,7 @@ def test_emulated_predicted_traceback_window(emu, oracle, seed_l, monkeypatch):
     (IMSAME_NW_WINDOW=0), and both kinds of half occur."""
     from tests import synth
     monkeypatch.setenv("IMSAME_SEED_L", seed_l)
-    monkeypatch.setenv("IMSAME_NW_WINDOW", "1")       # opt-in (imsame_dev.hip: off by default)
+    monkeypatch.setenv("IMSAME_NW_WINDOW", "1")       # (imsame_dev.hip: on by default)
     win = emu.lib.emu_win_count
     win.restype = C.c_uint32
     ref, rst = synth.make_reference_arr(240_000, 700, seed=61)
