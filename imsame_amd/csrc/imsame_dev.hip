@@ -297,6 +297,7 @@ struct imsame_ctx {
     std::vector<hipEvent_t> q_part_ev;
     std::vector<uint64_t> q_part_end;
     bool q_len_mult = false;         // every read length is a multiple of NW16_K
+    uint32_t q_len_uni = 0;          // the one read length of the uploaded range (0: lengths differ)
     // per-read state
     DBuf res, cur_p, cur_h, memo, nmemo, rstat, act0, act1, act2, cbase, ccnt, perr;
     // candidates
@@ -573,7 +574,7 @@ static int lane_sub(imsame_ctx *c, int k, imsame_ctx **out) {
     l->have_index = c->have_index;
     l->n_q = c->n_q; l->q_len = c->q_len; l->q_lo = c->q_lo; l->q_hi = c->q_hi; l->q_base = c->q_base;
     l->q_lo_first = c->q_lo_first; l->hq = c->hq; l->hqb = c->hqb; l->have_query = c->have_query;
-    l->q_len_mult = c->q_len_mult;
+    l->q_len_mult = c->q_len_mult; l->q_len_uni = c->q_len_uni;
     l->q_part_ev = c->q_part_ev; l->q_part_end = c->q_part_end;
     l->ev_db_len = 0; l->use_wcap = l->use_wstart = false;
     l->np_owner = c;
@@ -727,36 +728,41 @@ extern "C" int imsame_dev_set_query_range_async(imsame_ctx *c, const uint8_t *q_
     h[0] = qs(read_from);
     // reads k-1 (k = 1 .. m) in chunks of whole blocks, one host thread each
     // (1M reads: ~1 ms on one core, on the critical path of every upload)
-    auto pass = [&](uint64_t k0, uint64_t k1, bool *okp, bool *multp) {
+    auto pass = [&](uint64_t k0, uint64_t k1, bool *okp, bool *multp, uint64_t *lminp) {
         uint64_t prev = k0 == 1 ? h[0] : qs(read_from + k0 - 1);
         bool ok = true, mult = true;
+        uint64_t lmin = ~0ull;
         for (uint64_t k = k0; k < k1; ++k) {
             const uint64_t v = read_from + k < n_q ? q_start[read_from + k] : q_len;
             const uint64_t len = v - prev;
             ok &= v >= prev;
             mult &= len % NW16_K == 0;
+            lmin = std::min(lmin, len);
             uint32_t &b = bm[(k - 1) / QB_READS];
             b = std::max<uint32_t>(b, (uint32_t)std::min<uint64_t>(len, 0xFFFFFFFFu));
             h[k] = v;
             prev = v;
         }
-        *okp = ok; *multp = mult;
+        *okp = ok; *multp = mult; *lminp = lmin;
     };
     const uint64_t nblk_r = (m + QB_READS - 1) / QB_READS;
     const int nt = (int)std::min<uint64_t>(8, (nblk_r + 15) / 16);      // >= 16 blocks per thread
     bool okv[8] = {true, true, true, true, true, true, true, true}, mv[8] = {true, true, true, true, true, true, true, true};
+    uint64_t lminv[8] = {~0ull, ~0ull, ~0ull, ~0ull, ~0ull, ~0ull, ~0ull, ~0ull};
     if (nt <= 1) {
-        pass(1, m + 1, &okv[0], &mv[0]);
+        pass(1, m + 1, &okv[0], &mv[0], &lminv[0]);
     } else {
         std::vector<std::thread> th;
         for (int t = 0; t < nt; ++t) {
             const uint64_t k0 = 1 + (nblk_r * t / nt) * QB_READS, k1 = std::min<uint64_t>(1 + (nblk_r * (t + 1) / nt) * QB_READS, m + 1);
-            th.emplace_back(pass, k0, k1, &okv[t], &mv[t]);
+            th.emplace_back(pass, k0, k1, &okv[t], &mv[t], &lminv[t]);
         }
         for (auto &x : th) x.join();
     }
     bool ok = h[0] <= q_len, mult = true;
-    for (int t = 0; t < 8; ++t) { ok = ok && okv[t]; mult = mult && mv[t]; }
+    uint64_t lmin = ~0ull, lmax = 0;
+    for (int t = 0; t < 8; ++t) { ok = ok && okv[t]; mult = mult && mv[t]; lmin = std::min(lmin, lminv[t]); }
+    for (uint32_t b : c->h_q_bmax) lmax = std::max<uint64_t>(lmax, b);
     const uint64_t prev = h[m];
     if (!ok || prev > q_len) return IMSAME_E_ARG;                   // starts ascend within the query
     c->n_q = n_q; c->q_len = q_len; c->q_lo = read_from; c->q_hi = read_to;
@@ -770,6 +776,7 @@ extern "C" int imsame_dev_set_query_range_async(imsame_ctx *c, const uint8_t *q_
     c->q_base = b0 > QPAD ? b0 - QPAD : 0;
     const uint64_t nb = b1 - c->q_base, ns = read_to - read_from + 1;
     c->q_len_mult = mult;
+    c->q_len_uni = (m > 0 && lmin == lmax && lmax < 0xFFFFFFFFu) ? (uint32_t)lmax : 0u;
     if (c->q.ensure(nb + 64) || c->q_start.ensure(ns * 8)) return IMSAME_E_OOM;
     while (c->q_part_ev.size() < Q_PARTS) {
         hipEvent_t e;
@@ -899,9 +906,10 @@ static int nw16_band_rows() {
 // record cap (reads <= NW_W/2, either column form), so the launches of every
 // lane of a call -- whose read lengths differ -- share one layout.
 static void np_strides(uint32_t xcap, uint64_t *tb_dw, uint64_t *ck_dw) {
-    const NwShape a = nw16_shape(NW_W / 2, xcap, NW16_K), b = nw16_shape(NW_W / 2, xcap, NW16_K5);
-    *tb_dw = std::max(nw16_tb_words(a), nw16_tb_words(b));
-    *ck_dw = std::max(nw16_ck_words(a), nw16_ck_words(b));
+    const NwShape a = nw16_shape(NW_W / 2, xcap, NW16_K), b = nw16_shape(NW_W / 2, xcap, NW16_K5),
+                  d = nw16_shape(NW16_K19_YLEN, xcap, NW16_K19);
+    *tb_dw = std::max(std::max(nw16_tb_words(a), nw16_tb_words(b)), nw16_tb_words(d));
+    *ck_dw = std::max(std::max(nw16_ck_words(a), nw16_ck_words(b)), nw16_ck_words(d));
 }
 
 // Blocks per CU the XCD partitions of a context's slot bitmap hold: the
@@ -921,6 +929,8 @@ static int nw16_np_part_cu(imsame_ctx *c) {
     q((const void *)nw16_kernel<NW16_K, false, false>); q((const void *)nw16_kernel<NW16_K, true, false>);
     q((const void *)nw16_kernel<NW16_K5, false, true>); q((const void *)nw16_kernel<NW16_K5, true, true>);
     q((const void *)nw16_kernel<NW16_K5, false, false>); q((const void *)nw16_kernel<NW16_K5, true, false>);
+    q((const void *)nw16_kernel<NW16_K19, true, true, NW16_K19_OFF>);
+    q((const void *)nw16_kernel<NW16_K19, true, false, NW16_K19_OFF>);
     c->np_part_cu = ok ? m : 0;
     return c->np_part_cu;
 }
@@ -949,8 +959,9 @@ static int nw16_k(imsame_ctx *c, uint32_t ncand, bool rounds) {
 
 // pk: the packed-pair int16 kernel (nw16_kernel.hip) when the launch fits it
 // ylen_mult: every read of the launch has a length that is a multiple of NW16_K
+// ylen_uni: the one length of every read of the launch (0: lengths differ)
 static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, const imsame_params *p,
-                   bool ylen_mult, NwPlan *pl, bool rounds = true) {
+                   bool ylen_mult, NwPlan *pl, bool rounds = true, uint32_t ylen_uni = 0) {
     const int wpb = 4;
     // Small launches (the last rounds; every round of a small shard) are
     // latency-bound: one packed task is 8 candidates x all rows with 10
@@ -971,6 +982,10 @@ static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, 
         pl->band_w = nb ? std::max(1, std::min(NWL_BAND, atoi(nb))) : NWL_BAND_DEF;
     }
     pl->k = pl->pk ? nw16_k(c, ncand, rounds) : 0;
+    if (pl->pk && pl->k == NW16_K && nw16_k19_ok(ylen_uni, ymax, xcap, p)) {
+        pl->k = NW16_K19;
+        pl->last4 = true;                   // 150 = 8 x 19 - OFF: last column in slot K-1
+    }
     const NwShape sh = pl->pk ? nw16_shape(ymax, xcap, pl->k) : pl->lng ? nwl_shape(ymax, xcap) : nw_shape(ymax, xcap);
     pl->G = sh.G; pl->GPW = sh.GPW; pl->nstr = sh.nstr; pl->xcap = sh.xcap; pl->xstride = sh.xstride;
     pl->steps = sh.steps;
@@ -980,8 +995,12 @@ static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, 
     pl->lds = (size_t)wpb * (pl->pk ? nw16_wave_lds(pl->GPW, pl->xstride)
                              : pl->lng ? nwl_wave_lds(pl->xstride) : nw_wave_lds(pl->GPW, pl->xstride));
     int per_cu = 0;
-    const bool k5 = pl->k == NW16_K5;
+    const bool k5 = pl->k == NW16_K5, k19 = pl->k == NW16_K19;
     hipError_t oe = pl->lng ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nwl_kernel, wpb * 64, pl->lds)
+                  : k19 ? (pl->two ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                                         &per_cu, nw16_kernel<NW16_K19, true, true, NW16_K19_OFF>, wpb * 64, pl->lds)
+                                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                                         &per_cu, nw16_kernel<NW16_K19, true, false, NW16_K19_OFF>, wpb * 64, pl->lds))
                   : pl->two ? (k5 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw16_kernel<NW16_K5, false, true>, wpb * 64, pl->lds)
                                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw16_kernel<NW16_K, false, true>, wpb * 64, pl->lds))
                   : pl->pk ? (k5 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw16_kernel<NW16_K5, false, false>, wpb * 64, pl->lds)
@@ -1184,6 +1203,8 @@ static int launch_nw(imsame_ctx *c, NwPlan &pl, const uint32_t *cread, const uin
     }
     const bool k5 = pl.k == NW16_K5;
     if (pl.lng)                        nwl_kernel<<<pl.blocks, 256, pl.lds, s>>>(P);
+    else if (pl.k == NW16_K19 && pl.two) nw16_kernel<NW16_K19, true, true, NW16_K19_OFF><<<pl.blocks, 256, pl.lds, s>>>(P);
+    else if (pl.k == NW16_K19)         nw16_kernel<NW16_K19, true, false, NW16_K19_OFF><<<pl.blocks, 256, pl.lds, s>>>(P);
     else if (pl.two && pl.last4 && k5) nw16_kernel<NW16_K5, true, true><<<pl.blocks, 256, pl.lds, s>>>(P);
     else if (pl.two && k5)             nw16_kernel<NW16_K5, false, true><<<pl.blocks, 256, pl.lds, s>>>(P);
     else if (pl.pk && pl.last4 && k5)  nw16_kernel<NW16_K5, true, false><<<pl.blocks, 256, pl.lds, s>>>(P);
@@ -1257,7 +1278,7 @@ static int rewalk_lost(imsame_ctx *c, const imsame_params *p, uint64_t read_from
         HIPCHK(hipMemcpyAsync(c->cread.p, rd[cl].data(), (uint64_t)m * 4, hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(c->csid.p, sid[cl].data(), (uint64_t)m * 4, hipMemcpyHostToDevice, s));
         NwPlan pl;
-        if ((rc = plan_nw(c, cl ? ycap : short_y, xcap, m, p, c->q_len_mult, &pl))) return rc;
+        if ((rc = plan_nw(c, cl ? ycap : short_y, xcap, m, p, c->q_len_mult, &pl, true, c->q_len_uni))) return rc;
         double ms = 0;
         rc = launch_nw(c, pl, c->cread.as<uint32_t>(), c->csid.as<uint32_t>(), m, c->cout.as<imsame_read_result>(),
                        p->igap, p->egap, p, ymax, xcap, (uint32_t *)(ctr + C_WORK), c->db.as<uint8_t>(),
@@ -1470,6 +1491,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
                 if (pl.pk) st.launch_pk |= 1ull << st.nw_launches;
                 if (pl.pk && pl.k == NW16_K5) st.launch_k5 |= 1ull << st.nw_launches;
                 if (pl.np) st.launch_np |= 1ull << st.nw_launches;
+                if (pl.pk && pl.k == NW16_K19) st.launch_k19 |= 1ull << st.nw_launches;
             }
             st.ms_nw += ms; st.nw_launches++; st.n_nw += nc;
         };
@@ -1509,7 +1531,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         // IMSAME_ROUND1B=0 turns it off.
         NwPlan pla = {};
         bool r1b = st.rounds == 1 && r1b_on && hc[2] > 0 && n2 == 0 && ccap > n1;
-        if (r1b && n1 && (rc = plan_nw(c, short_y, xcap, n1, p, c->q_len_mult, &pla))) return rc;
+        if (r1b && n1 && (rc = plan_nw(c, short_y, xcap, n1, p, c->q_len_mult, &pla, true, c->q_len_uni))) return rc;
         if (r1b && n1 && !pla.np) r1b = false;
         if (r1b) {
             if (!c->stream_b) {
@@ -1551,7 +1573,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
             NwPlan plb = {};
             bool a_done = n1 == 0;
             if (nb) {
-                if ((rc = plan_nw(c, short_y, xcap, nb, p, c->q_len_mult, &plb))) return rc;
+                if ((rc = plan_nw(c, short_y, xcap, nb, p, c->q_len_mult, &plb, true, c->q_len_uni))) return rc;
                 // N1a's launch_nw may have fallen back to a persistent launch on
                 // this lane's own arena: then N1b must wait for it (pla.np is
                 // what it ran with)
@@ -1599,7 +1621,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         for (int k = 0; k < 2; ++k) {
             if (!cls[k].n) continue;
             NwPlan pl;
-            if ((rc = plan_nw(c, cls[k].ylim, xcap, cls[k].n, p, c->q_len_mult, &pl))) return rc;
+            if ((rc = plan_nw(c, cls[k].ylim, xcap, cls[k].n, p, c->q_len_mult, &pl, true, c->q_len_uni))) return rc;
             double ms = 0;
             rc = launch_nw(c, pl, cls[k].cr, cls[k].cs, cls[k].n, cls[k].o, p->igap, p->egap, p, ymax, xcap,
                            (uint32_t *)(ctr + cls[k].work), c->db.as<uint8_t>(), c->db_start.as<uint64_t>(), qd, qsd,
@@ -2147,9 +2169,12 @@ extern "C" int imsame_dev_nw_pairs(imsame_ctx *c, const uint8_t *xs, const uint6
     uint64_t *ctr = c->ctr.as<uint64_t>();
     HIPCHK(hipMemsetAsync(ctr, 0, C_NSLOTS * 8, s));
     NwPlan pl;
-    bool ymult = true;
-    for (uint64_t k = 0; k < npairs; ++k) ymult = ymult && (y_start[k + 1] - y_start[k]) % NW16_K == 0;
-    if ((rc = plan_nw(c, ymax, xmax, (uint32_t)npairs, p, ymult, &pl, false))) return rc;
+    bool ymult = true, yuni = true;
+    for (uint64_t k = 0; k < npairs; ++k) {
+        ymult = ymult && (y_start[k + 1] - y_start[k]) % NW16_K == 0;
+        yuni = yuni && y_start[k + 1] - y_start[k] == ymax;
+    }
+    if ((rc = plan_nw(c, ymax, xmax, (uint32_t)npairs, p, ymult, &pl, false, yuni ? ymax : 0))) return rc;
     double ms = 0;
     rc = launch_nw(c, pl, dc.as<uint32_t>(), dc.as<uint32_t>(), (uint32_t)npairs, dout.as<imsame_read_result>(),
                    p->igap, p->egap, p, ymax, xmax, (uint32_t *)(ctr + C_WORK), dx.as<uint8_t>(), dxs.as<uint64_t>(),

@@ -88,7 +88,18 @@ static_assert(NW16_CK % 2 == 0 && NW16_CK <= 32, "NW16_CK: even, <= 32 (nw16_fit
 // dwords of wave state per lane in a checkpoint (A, B, mcS, u0 per column; I1,
 // I2, outT, outMS, outL); dI is a function of A and I2 there (save())
 __host__ __device__ constexpr int nw16_nst(int K) { return 4 * K + 5; }
-__host__ __device__ constexpr int nw16_nrec(int K) { return K > 8 ? 3 : 2; }
+// K <= 10: WM, WU (+ WX for cells 8-9); K > 10 (the 19-column form): WM_b, WU_b
+// for each block b of 8 cells (cells 8b .. 8b+7 at bits q = s - 8b)
+__host__ __device__ constexpr int nw16_nrec(int K) { return K <= 8 ? 2 : K <= 10 ? 3 : 2 * ((K + 7) / 8); }
+// The 19-column form (nw16_k19): 8 lanes per candidate pair, 8 groups per
+// wave -- all 64 lanes busy at 150 bp, where K = 10 leaves 4 of 64 idle -- and
+// the per-step work (DPP, row code, best cell) spread over 19 columns instead
+// of 10.  Lane gl owns columns [gl*K - OFF, gl*K - OFF + K): the OFF leading
+// columns of lane 0 are padding (never read), so a read of length G*K - OFF
+// ends in slot K-1 of its last lane (the LAST form) -- 150 = 8*19 - 2.
+#define NW16_K19 19
+#define NW16_K19_OFF 2
+#define NW16_K19_YLEN (8 * NW16_K19 - NW16_K19_OFF)
 #define NW16_NOROW INT32_MIN      // cand_row: no prediction
 #define NW16_WIN_UP 32            // window rows above the predicted first row
 #define NW16_WIN_DOWN 24          // ... and below the predicted last row
@@ -97,15 +108,16 @@ __host__ __device__ constexpr int nw16_nrec(int K) { return K > 8 ? 3 : 2; }
 #define NW16_BAND2 4              // the second sweep's retry band, in bands
 
 // does the launch fit the int16 path?  (all gap terms non-positive)
-__host__ static inline bool nw16_fits(int64_t ig, int64_t eg, uint64_t xcap, uint64_t ymax) {
+__host__ static inline bool nw16_fits(int64_t ig, int64_t eg, uint64_t xcap, uint64_t ymax, int K = NW16_K) {
     if (ig > 0 || eg > 0 || ymax > (uint64_t)NW_W / 2 || ymax == 0) return false;
-    const uint64_t G = (ymax + NW16_K - 1) / NW16_K, ycols = G * NW16_K;
+    const uint64_t G = (ymax + K - 1) / K, ycols = G * K;
     const uint64_t aig = (uint64_t)(-ig), aeg = (uint64_t)(-eg);
     if (aig > 8191 || aeg > 8191) return false;
     // |T| <= 4*ycols; l0 >= -T - |ig| - |eg|*ycols; u0 drifts at most over
     // xcap + 64 rows (lockstep garbage rows included -- a second sweep runs at
     // most NW16_CK + G <= 32 + 32 rows past the first one, G <= 32 at K = 5)
-    // and takes u2 + ig + 2eg.  ycols at K = 10 bounds ycols at K = 5.
+    // and takes u2 + ig + 2eg.  ycols at K = 10 bounds ycols at K = 5 (K = 19
+    // asks with its own ycols; its padding columns never feed a real one).
     const uint64_t R = 4 * ycols + aig + aeg * (xcap + 64 + ycols + 2) + 16;
     return R <= 8191;
 }
@@ -132,16 +144,20 @@ WV_DEVICE uint32_t base_code(uint8_t b) { return (b >> 1) & 3u; }          // A0
 // traceback of half h of group g (layout above) -> nw_kernel.hip's nibble
 // t0: step of the sweep that wrote record 0 (0: one pass, steps indexed by t;
 // two passes: the half's restart step, cells before it were not written)
-template <int K>
+template <int K, int OFF = 0>
 struct TbAcc16 {
     const uint32_t *tb; const uint8_t *X; const uint8_t *Y; int g, G, h, t0;
     int t1 = INT_MAX;                      // steps [t0, t1) were written
-    __device__ bool has(int i, int j) const { const int t = i + j / K; return t >= t0 && t < t1; }
+    __device__ bool has(int i, int j) const { const int t = i + (j + OFF) / K; return t >= t0 && t < t1; }
     __device__ uint32_t nib(int i, int j) const {
-        const int l = j / K, s = j - l * K;
+        const int l = (j + OFF) / K, s = (j + OFF) - l * K;
         const uint32_t *w = tb + ((uint32_t)(i + l - t0) * 64u + (uint32_t)(g * G + l)) * (uint32_t)nw16_nrec(K);
         uint32_t nd, up, U, nL;
-        if (s < 8) {
+        if (K > 10) {
+            const uint32_t wm = w[2 * (s >> 3)], wu = w[2 * (s >> 3) + 1], q = (uint32_t)(s & 7);
+            nd = (wm >> (8 * h + q)) & 1u; up = (wm >> (16 + 8 * h + q)) & 1u;
+            U = (wu >> (16 * h + q)) & 1u; nL = (wu >> (16 * h + 8 + q)) & 1u;
+        } else if (s < 8) {
             const uint32_t wm = w[0], wu = w[1];
             nd = (wm >> (8 * h + s)) & 1u; up = (wm >> (16 + 8 * h + s)) & 1u;
             U = (wu >> (16 * h + s)) & 1u; nL = (wu >> (16 * h + 8 + s)) & 1u;
@@ -155,15 +171,45 @@ struct TbAcc16 {
     __device__ bool match(int i, int j) const { return ((X[i] >> (2 * h)) & 3u) == base_code(Y[j]); }
 };
 
+// one lane's traceback words of one step (layout above), built cell by cell
+// (s is a compile-time slot after unrolling: the words stay in registers)
+template <int K>
+struct TbWords {
+    uint32_t w[nw16_nrec(K)];
+    WV_DEVICE void add(const int s, const uint32_t P2, const uint32_t mU, const uint32_t mnL) {
+        if (K > 10) {
+            const int b = s >> 3, q = s & 7;
+            w[2 * b] = wv_and_or(P2, 0x01010101u << q, w[2 * b]);
+            w[2 * b + 1] = wv_and_or(mU, 0x00010001u << q, w[2 * b + 1]);
+            w[2 * b + 1] = wv_and_or(mnL, 0x01000100u << q, w[2 * b + 1]);
+        } else if (s < 8) {
+            w[0] = wv_and_or(P2, 0x01010101u << s, w[0]);
+            w[1] = wv_and_or(mU, 0x00010001u << s, w[1]);
+            w[1] = wv_and_or(mnL, 0x01000100u << s, w[1]);
+        } else {
+            constexpr int X = nw16_nrec(K) - 1;       // WX (K = 10; the branch is dead for K <= 8)
+            const int q = s - 8;
+            w[X] = wv_and_or(P2, 0x01010101u << q, w[X]);
+            w[X] = wv_and_or(mU, 0x00040004u << q, w[X]);
+            w[X] = wv_and_or(mnL, 0x00100010u << q, w[X]);
+        }
+    }
+    WV_DEVICE void store(uint32_t *rec) const {
+#pragma unroll
+        for (int r = 0; r < nw16_nrec(K); ++r) rec[r] = w[r];
+    }
+};
+
 __host__ __device__ static inline size_t nw16_wave_lds(int GPW, int xstride) {
     return (size_t)GPW * xstride + 64 * 8 * 4;
 }
 
-// LAST: every read length of the launch is a multiple of K, so each
-// candidate's last column is slot K-1 of its owner lane (no select).
+// LAST: every read length of the launch is a multiple of K (or, with OFF > 0,
+// equals G*K - OFF), so each candidate's last column is slot K-1 of its owner
+// lane (no select).  OFF: padding columns ahead of column 0 (nw16_k19).
 // TWO: score-only sweep + checkpoints, then the traceback band (header).
-template <int K, bool LAST, bool TWO>
-__device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const uint32_t slot) {
+template <int K, bool LAST, bool TWO, int OFF = 0>
+__device__ __forceinline__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const uint32_t slot) {
     constexpr int NST = nw16_nst(K), NREC = nw16_nrec(K);
     constexpr uint32_t RECB = 64u * 4u * NREC;     // traceback bytes per step
     const int G = P.G, GPW = P.GPW;
@@ -287,7 +333,7 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
         const int tb0 = TWO ? tw0 : 0;             // step of traceback record 0
 
         // ------------------------------------------------------------ sweep
-        const int j0 = gl * K;
+        const int j0 = gl * K - OFF;
         const bool leadc0 = gl == 0;
         const int xcl = max(xlp - 1, 0);
         const uint32_t NBIG = pk1(-NW16_BIG) ^ NW16_H, EGN = pk1(-eg), IGEN = pk1(-(ig + eg));   // biased; gap magnitudes
@@ -300,8 +346,8 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
 #pragma unroll
         for (int s = 0; s < K; ++s) {
             const int j = j0 + s;
-            const uint32_t ya = (valid[0] && j < yl[0]) ? base_code(Yp[0][j]) : 0u;
-            const uint32_t yb = (valid[0] && j < yl[1]) ? base_code(Yp[1][j]) : 0u;
+            const uint32_t ya = (valid[0] && j >= 0 && j < yl[0]) ? base_code(Yp[0][j]) : 0u;
+            const uint32_t yb = (valid[0] && j >= 0 && j < yl[1]) ? base_code(Yp[1][j]) : 0u;
             yreg[s] = ya | ((ya | 4u) << 8) | (yb << 16) | ((yb | 4u) << 24);
             lastm[s] = ((ownC[0] && yl[0] - 1 - j0 == s) ? 0x0000FFFFu : 0u) |
                        ((ownC[1] && yl[1] - 1 - j0 == s) ? 0xFFFF0000u : 0u);
@@ -354,7 +400,8 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
             xrow = CAREFUL ? X8[min(max(i + 1, 0), xcl)] : X8[i + 1];          // next row, read ahead
             const bool pre = PRE && i < 1;
             const bool row1 = CAREFUL && i <= 1;                     // up invalid, mc frozen (:449, :476)
-            uint32_t mfS = mS, l0 = mL0, wm = 0, wu = 0, wx = 0;
+            uint32_t mfS = mS, l0 = mL0;
+            TbWords<K> tw = {};
 #pragma unroll
             for (int s = 0; s < K; ++s) {
                 const uint32_t d0 = (s == 0) ? in1 : own[s - 1];     // T[i-1][j-1]
@@ -363,7 +410,7 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
                 const uint32_t up = row1 ? NBIG : u0[s];
                 const uint32_t lu = pk_maxu(l0, up);
                 uint32_t v = pk_add(pk_maxu(d0, lu), sc);
-                if (s == 0) v = leadc0 ? (sc ^ NW16_H) : v;                      // column 0 (:426)
+                if (s == OFF) v = leadc0 ? (sc ^ NW16_H) : v;                    // column 0 (:426)
                 cur[s] = pre ? own[s] : v;
                 // move bits: signs of (d0 - lu) [not diagonal] and (l0 - up) [up > left] (:457-472)
                 // (sign-replicating selectors 8-11: bytes 0xFF / 0x00, no shift before packing)
@@ -379,26 +426,12 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
                 dI[s] = d0 - IGEN;                              // this row's; the next row's u2 + ig + eg
                 l0 = wv_bfi(mnL, l0 - EGN, dI[s]);
                 mfS = wv_bfi(mnL, mfS, d0);
-                if (s == 0) { mfS = leadc0 ? NBIG : mfS; l0 = leadc0 ? NBIG : l0; }   // j = 1: mf = T[i][0]
-                if (!TB) {
-                } else if (s < 8) {
-                    wm = wv_and_or(P2, 0x01010101u << s, wm);
-                    wu = wv_and_or(mU, 0x00010001u << s, wu);
-                    wu = wv_and_or(mnL, 0x01000100u << s, wu);
-                } else {
-                    const int q = s - 8;
-                    wx = wv_and_or(P2, 0x01010101u << q, wx);
-                    wx = wv_and_or(mU, 0x00040004u << q, wx);
-                    wx = wv_and_or(mnL, 0x00100010u << q, wx);
-                }
+                if (s == OFF) { mfS = leadc0 ? NBIG : mfS; l0 = leadc0 ? NBIG : l0; }   // j = 1: mf = T[i][0]
+                if (TB) tw.add(s, P2, mU, mnL);
             }
             // rows outside [1, xlen) are never read; 32-bit byte offset from the
             // wave-uniform slot base (global_store saddr form)
-            if (TB) {
-                uint32_t *rec = (uint32_t *)(tb3 + ((uint32_t)(t - tb0) * RECB + (uint32_t)lane * (4u * NREC)));
-                rec[0] = wm; rec[1] = wu;
-                if (NREC > 2) rec[2] = wx;
-            }
+            if (TB) tw.store((uint32_t *)(tb3 + ((uint32_t)(t - tb0) * RECB + (uint32_t)lane * (4u * NREC))));
             // last column (rows 1 .. xlen-2) and last row (:481-484)
             uint32_t vl = cur[LAST ? K - 1 : 0];
             if (!LAST)
@@ -516,7 +549,7 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
         mark(2);
         if (!TWO) {
             for (int h = 0; h < 2; ++h) {
-                const TbAcc16<K> acc16 = {tbw, X8, Yp[h], gg, G, h, 0};
+                const TbAcc16<K, OFF> acc16 = {tbw, X8, Yp[h], gg, G, h, 0};
                 nw_finish(P, acc16, xl[h], yl[h], valid[h], gg, gl, G, bscore[h], bx[h], by[h], cidx[h], sid[h]);
             }
             wv_lds_sync();
@@ -535,7 +568,7 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
             for (int h = 0; h < 2; ++h) cov[h] = todo[h] && bx[h] + G <= tw1;
             if (wv_any(cov[0] || cov[1])) {
                 for (int h = 0; h < 2; ++h) {
-                    TbAcc16<K> acc16 = {tbw, X8, Yp[h], gg, G, h, tw0};
+                    TbAcc16<K, OFF> acc16 = {tbw, X8, Yp[h], gg, G, h, tw0};
                     acc16.t1 = tw1;
                     const bool lost = nw_finish(P, acc16, xl[h], yl[h], cov[h], gg, gl, G, bscore[h], bx[h], by[h],
                                                 cidx[h], sid[h]);
@@ -558,7 +591,8 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
             // per-half forms of pass 1's `pre` (i < 1: row 0 repeats) and `row1` (i <= 1)
             const uint32_t pm = !MASK ? 0u : (iA < 1 ? 0x0000FFFFu : 0u) | (iB < 1 ? 0xFFFF0000u : 0u);
             const uint32_t r1 = !MASK ? 0u : (iA <= 1 ? 0x0000FFFFu : 0u) | (iB <= 1 ? 0xFFFF0000u : 0u);
-            uint32_t mfS = mS, l0 = mL0, wm = 0, wu = 0, wx = 0;
+            uint32_t mfS = mS, l0 = mL0;
+            TbWords<K> tw = {};
 #pragma unroll
             for (int s = 0; s < K; ++s) {
                 const uint32_t d0 = (s == 0) ? in1 : own[s - 1];
@@ -567,7 +601,7 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
                 const uint32_t up = MASK ? wv_bfi(r1, NBIG, u0[s]) : u0[s];
                 const uint32_t lu = pk_maxu(l0, up);
                 uint32_t v = pk_add(pk_maxu(d0, lu), sc);
-                if (s == 0) v = leadc0 ? (sc ^ NW16_H) : v;
+                if (s == OFF) v = leadc0 ? (sc ^ NW16_H) : v;
                 cur[s] = MASK ? wv_bfi(pm, own[s], v) : v;
                 const uint32_t P2 = wv_perm(pk_sub(l0, up), pk_sub(d0, lu), 0x0B0A0908u);
                 const uint32_t mU = pk_neg_mask(pk_sub(mcS[s], dI[s]));
@@ -578,21 +612,10 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
                 dI[s] = d0 - IGEN;
                 l0 = wv_bfi(mnL, l0 - EGN, dI[s]);
                 mfS = wv_bfi(mnL, mfS, d0);
-                if (s == 0) { mfS = leadc0 ? NBIG : mfS; l0 = leadc0 ? NBIG : l0; }
-                if (s < 8) {
-                    wm = wv_and_or(P2, 0x01010101u << s, wm);
-                    wu = wv_and_or(mU, 0x00010001u << s, wu);
-                    wu = wv_and_or(mnL, 0x01000100u << s, wu);
-                } else {
-                    const int q = s - 8;
-                    wx = wv_and_or(P2, 0x01010101u << q, wx);
-                    wx = wv_and_or(mU, 0x00040004u << q, wx);
-                    wx = wv_and_or(mnL, 0x00100010u << q, wx);
-                }
+                if (s == OFF) { mfS = leadc0 ? NBIG : mfS; l0 = leadc0 ? NBIG : l0; }
+                tw.add(s, P2, mU, mnL);
             }
-            uint32_t *rec = (uint32_t *)(tb3 + ((uint32_t)tau * RECB + (uint32_t)lane * (4u * NREC)));
-            rec[0] = wm; rec[1] = wu;
-            if (NREC > 2) rec[2] = wx;
+            tw.store((uint32_t *)(tb3 + ((uint32_t)tau * RECB + (uint32_t)lane * (4u * NREC))));
             in0 = MASK ? wv_bfi(pm, in1, sN) : sN;
             outT = cur[K - 1]; outMS = mfS; outL = l0;
         };
@@ -639,7 +662,7 @@ __device__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const
             wv_mem_sync();                        // band traceback written by all lanes, read by the walkers
             mark(3);
             for (int h = 0; h < 2; ++h) {
-                const TbAcc16<K> acc16 = {tbw, X8, Yp[h], gg, G, h, t0h[h]};
+                const TbAcc16<K, OFF> acc16 = {tbw, X8, Yp[h], gg, G, h, t0h[h]};
                 todo[h] = nw_finish(P, acc16, xl[h], yl[h], todo[h], gg, gl, G, bscore[h], bx[h], by[h], cidx[h],
                                     sid[h]);
             }
@@ -667,6 +690,17 @@ __host__ static inline NwShape nw16_shape(uint32_t ymax, uint32_t xcap, int K = 
     while (s.GPW > 1 && (size_t)s.GPW * s.xstride > 16384) s.GPW--;
     s.steps = s.xcap + s.G;
     return s;
+}
+// The 19-column form where every read of a launch has length NW16_K19_YLEN
+// (150) and the shape fills the wave (imsame_dev.hip:plan_nw); on by default,
+// IMSAME_NW_K19=0 (or IMSAME_NW_K=10 / 5) keeps the 10-column form.
+__host__ static inline bool nw16_k19_ok(uint32_t ylen_uni, uint32_t ymax, uint32_t xcap, const imsame_params *p) {
+    const char *e = getenv("IMSAME_NW_K19"), *k = getenv("IMSAME_NW_K");
+    if ((e && !atoi(e)) || (k && atoi(k) != NW16_K19)) return false;
+    if (ylen_uni != NW16_K19_YLEN || ymax != NW16_K19_YLEN) return false;
+    if (!nw16_fits(p->igap, p->egap, xcap, ymax, NW16_K19)) return false;
+    const NwShape s = nw16_shape(ymax, xcap, NW16_K19);
+    return s.G * s.GPW == 64;
 }
 // traceback dwords per wave slot (NREC per lane per step)
 __host__ static inline uint64_t nw16_tb_words(const NwShape &s) { return (uint64_t)s.steps * 64 * nw16_nrec(s.k); }
@@ -738,8 +772,15 @@ __global__ void xcc_probe_kernel(uint32_t *out) {
 #ifndef NW16_K5_WAVES_PER_EU
 #define NW16_K5_WAVES_PER_EU 5
 #endif
-template <int K, bool LAST, bool TWO>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 8 ? NW16_WAVES_PER_EU : NW16_K5_WAVES_PER_EU)))
+// the 19-column form holds 6 x 19 per-column registers: 2 waves per SIMD (256
+// VGPRs), which the first-sweep loop's ILP keeps issuing (a 2-wave SIMD ran
+// the 10-column loop at 4.0 cycles per VALU, profiles/r4b/micro_*)
+#ifndef NW16_K19_WAVES_PER_EU
+#define NW16_K19_WAVES_PER_EU 2
+#endif
+template <int K, bool LAST, bool TWO, int OFF = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 10 ? NW16_K19_WAVES_PER_EU
+                                                                     : K > 8 ? NW16_WAVES_PER_EU : NW16_K5_WAVES_PER_EU)))
 void nw16_kernel(NwLaunch P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
@@ -756,7 +797,7 @@ void nw16_kernel(NwLaunch P) {
     } else {
         slot = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + wib);   // wave-uniform
     }
-    nw16_wave<K, LAST, TWO>(P, smem + wib * nw16_wave_lds(P.GPW, P.xstride), lane, slot);
+    nw16_wave<K, LAST, TWO, OFF>(P, smem + wib * nw16_wave_lds(P.GPW, P.xstride), lane, slot);
     if (P.slot_bits) nw_slot_release(P, lane, slot);
 }
 #endif

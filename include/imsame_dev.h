@@ -138,6 +138,9 @@ typedef struct imsame_stats {
                                (latency-bound launches), else 10           */
     uint64_t launch_np;     /* bit k: NW launch k was non-persistent (one wave
                                per task, arena slots per XCD)             */
+    uint64_t launch_k19;    /* bit k: packed NW launch k ran the 19-column
+                               form (8 lanes per pair, reads of one length
+                               150: every lane of the wave busy)          */
 } imsame_stats;
 
 typedef struct imsame_ctx imsame_ctx;

@@ -54,6 +54,10 @@ extern "C" uint32_t emu_r1b_count(void) { const uint32_t r = g_r1b; g_r1b = 0; r
 static uint32_t g_win;
 extern "C" uint32_t emu_win_count(void) { const uint32_t r = g_win; g_win = 0; return r; }
 
+// packed launches that ran the 19-column form (nw16_k19_ok), since the last emu_k19_count()
+static uint32_t g_k19;
+extern "C" uint32_t emu_k19_count(void) { const uint32_t r = g_k19; g_k19 = 0; return r; }
+
 static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, const uint64_t *qs,
                   const uint32_t *cread, const uint32_t *csid, uint32_t n, const imsame_params *p, uint32_t ymax,
                   uint32_t xmax, const std::vector<uint32_t> &ml, const std::vector<uint32_t> &mi,
@@ -68,7 +72,10 @@ static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, cons
     // columns per lane of the packed kernel: imsame_dev.hip:nw16_k picks by the
     // chip's fill; here IMSAME_NW_K=5 selects the latency-bound form
     const char *ke = getenv("IMSAME_NW_K");
-    const int K = (ke && atoi(ke) == NW16_K5) ? NW16_K5 : NW16_K;
+    uint32_t yuni = n ? (uint32_t)(qs[cread[0] + 1] - qs[cread[0]]) : 0;    // one read length? (nw16_k19_ok)
+    for (uint32_t k = 0; k < n; ++k) if (qs[cread[k] + 1] - qs[cread[k]] != yuni) yuni = 0;
+    const int K = (ke && atoi(ke) == NW16_K5) ? NW16_K5
+                : (pk && nw16_k19_ok(yuni, ymax, xmax, p)) ? NW16_K19 : NW16_K;
     const NwShape sh = pk ? nw16_shape(ymax, xmax, K) : lng ? nwl_shape(ymax, xmax) : nw_shape(ymax, xmax);
     std::vector<uint32_t> tb((pk ? nw16_tb_words(sh) : lng ? nwl_tb_words(sh, ymax) : nw_tb_words(sh)) + 64, 0xABABABABu);
     std::vector<uint32_t> ck(two ? nw16_ck_words(sh) : lng ? nwl_ck_words(sh) : 1, 0xCDCDCDCDu);
@@ -122,6 +129,11 @@ static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, cons
     bool ymult = true;        // every read length a multiple of NW16_K (imsame_dev.hip: q_len_mult)
     for (uint32_t k = 0; k < n; ++k) ymult = ymult && (qs[cread[k] + 1] - qs[cread[k]]) % NW16_K == 0;
     if (lng)              run_wave([&](int lane) { nwl_wave(P, lds.data(), lane, 0); });
+    else if (pk && K == NW16_K19) {
+        ++g_k19;
+        if (two) run_wave([&](int lane) { nw16_wave<NW16_K19, true, true, NW16_K19_OFF>(P, lds.data(), lane, 0); });
+        else     run_wave([&](int lane) { nw16_wave<NW16_K19, true, false, NW16_K19_OFF>(P, lds.data(), lane, 0); });
+    }
     else if (pk && K == NW16_K5) {
         if (two && ymult)     run_wave([&](int lane) { nw16_wave<NW16_K5, true, true>(P, lds.data(), lane, 0); });
         else if (two)         run_wave([&](int lane) { nw16_wave<NW16_K5, false, true>(P, lds.data(), lane, 0); });

@@ -954,3 +954,31 @@ def test_c3_shard_of_10m_query(dev, oracle_memo):
     # the same reads as a 1.25M-read query of their own have other chunk heads
     # (rpt 78,125): read 78,125 starts a chunk there, not in the 10M query
     assert n_sh // 16 != head
+
+
+def test_k19_form_equals_k10_and_oracle(dev, oracle, monkeypatch):
+    """The packed kernel's 19-column form (reads of one length, 150: 8 lanes
+    per pair, every lane of the wave busy) against the 10-column form on the
+    same C2-shaped call -- identical rows and paths -- and the oracle; the
+    default runs it (stats.launch_k19), IMSAME_NW_K19=0 does not."""
+    ref, rst = synth.make_reference_arr(4_000_000, 2_000, seed=71)
+    q, qs = synth.make_reads_arr(ref, 40_000, 150, seed=72, ins=0.002, dele=0.002)
+    dev.index(ref, rst)
+    dev.set_query(q, qs)
+    r19, p19, s19 = dev.align(n_threads=16, want_paths=True)
+    monkeypatch.setenv("IMSAME_NW_K19", "0")
+    r10, p10, s10 = dev.align(n_threads=16, want_paths=True)
+    monkeypatch.delenv("IMSAME_NW_K19")
+    assert s19.launch_k19 != 0 and s10.launch_k19 == 0, (hex(s19.launch_k19), hex(s10.launch_k19))
+    assert not _cmp(r19, r10), _cmp(r19, r10)
+    acc = np.flatnonzero(r19["status"] == 1)
+    assert len(acc) > 30_000
+    for k in acc[::11]:
+        a, b = r19[k], r10[k]
+        assert p19[a["path_off"]:a["path_off"] + a["path_len"]].tolist() == \
+            p10[b["path_off"]:b["path_off"] + b["path_len"]].tolist(), k
+    wins = _windows(len(qs))
+    rc, exp, _ = oracle.align_windows(ref, rst, q, qs, wins, None, 16)
+    assert rc == 0
+    for (a, b), e in zip(wins, exp):
+        assert not _cmp(r19[a:b], e), ((a, b), _cmp(r19[a:b], e))

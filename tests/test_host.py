@@ -187,6 +187,60 @@ def test_emulated_two_pass_band(emu, oracle, band, cols, monkeypatch):
         assert n_redo == 0
 
 
+@pytest.mark.parametrize("band", ["200", "40", "0"])
+def test_emulated_k19_form(emu, oracle, band, monkeypatch):
+    """nw16_kernel.hip's 19-column form (emulated): launches whose reads all
+    have 150 bases run 8 lanes per pair (two padding columns ahead of column
+    0 in lane 0, the last column in slot 18), 8 groups per wave, 6 traceback
+    dwords per lane per step.  Two passes with bands that hold the path, that
+    do not (redo) and none, and one pass: every field equals the oracle and
+    every path the 10-column form's; 19 pairs leave idle groups in the last
+    wave."""
+    rng = np.random.default_rng(int(band) + 19)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    X, Y = [], []
+    for k in range(19):
+        xl = int(rng.integers(150, 700))
+        x = acgt[rng.integers(0, 4, xl)]
+        if k % 3 != 2:
+            o = int(rng.integers(0, max(1, xl - 150)))
+            y = x[o:o + 150].copy()
+            if len(y) < 150:
+                y = np.concatenate([y, acgt[rng.integers(0, 4, 150 - len(y))]])
+            mut = rng.random(150) < 0.04
+            y[mut] = acgt[rng.integers(0, 4, int(mut.sum()))]
+            if rng.random() < 0.5:                  # an indel run: up / left jumps
+                c = int(rng.integers(10, 140))
+                y = np.concatenate([y[:c], acgt[rng.integers(0, 4, 3)], y[c:]])[:150]
+        else:
+            y = acgt[rng.integers(0, 4, 150)]
+        X.append(x.tobytes()); Y.append(y.tobytes())
+    monkeypatch.setenv("IMSAME_NW_BAND", band)
+    k19 = emu.lib.emu_k19_count
+    k19.restype = C.c_uint32
+    k19()
+    out = {}
+    for form, env in (("k19", None), ("k10", "10")):
+        if env:
+            monkeypatch.setenv("IMSAME_NW_K", env)
+        for one in (False, True):
+            p = oracle.params(want_paths=1, flags=imsame_amd.FLAG_NW16_ONEPASS if one else 0)
+            rc, res, paths, fl = emu.nw_pairs(X, Y, p, paths_cap=8192)
+            assert rc == 0 and fl == 0
+            out[form, one] = (res, paths)
+        assert (k19() > 0) == (form == "k19")
+    for k in range(len(X)):
+        o = oracle.nw(X[k], Y[k], text=False)
+        for key, (res, paths) in out.items():
+            for f in ("score", "bx", "by", "length", "identities", "igaps", "egaps", "head_x", "head_y"):
+                assert int(res[k][f]) == int(o[f]), (key, f, k, band)
+        if o["length"] and out["k10", True][0][k]["status"] == 1:
+            ref = out["k10", True]
+            want = ref[1][ref[0][k]["path_off"]:ref[0][k]["path_off"] + ref[0][k]["path_len"]].tolist()
+            for key, (res, paths) in out.items():
+                assert paths[res[k]["path_off"]:res[k]["path_off"] + res[k]["path_len"]].tolist() == want, (key, k)
+
+
 @pytest.mark.parametrize("seed_l", ["1", "4"])
 def test_emulated_predicted_traceback_window(emu, oracle, seed_l, monkeypatch):
     """nw16_kernel.hip's predicted window (emulated pipeline): the strong seed
