@@ -43,11 +43,11 @@
 // that kernel's nibble.
 //
 // Two passes (TWO, the default): the full sweep writes no traceback -- it
-// keeps the DP values, the best cell and, every NW16_CK steps, a checkpoint of
-// the wave's whole register state (56 dwords per lane) -- and a second sweep
+// keeps the DP values, the best cell and, every nw16_ck(K) steps, a checkpoint of
+// the wave's register state (4K+5 dwords per lane) -- and a second sweep
 // restarts each half from the last checkpoint at least band_w rows above its
 // best cell, per half (its own rows: two LDS row reads and per-half row masks),
-// and writes the traceback of those ~band_w + NW16_CK + G steps only.  The
+// and writes the traceback of those ~band_w + nw16_ck(K) + G steps only.  The
 // walk reads only rows the second sweep wrote (TbAcc16::has); a path that
 // leaves them is LOST and the wave redoes the second sweep over 4 bands, then
 // from row 1 (same values: the state restored is the state the first sweep
@@ -76,15 +76,14 @@
 #define NW16_K   10               // columns per lane (the full-chip launches)
 #define NW16_K5  5                // columns per lane of the latency-bound launches (nw16_k)
 #define NW16_BIG 16384
-// Checkpoint interval of the first sweep (steps; even: the rotation period;
-// <= 32: nw16_fits bounds the rows a second sweep runs past the first by
-// NW16_CK + G <= 64).  32 (round 3: 24) with the checkpoint 4K+5 dwords (dI is
-// recomputed on restore): 0.46 -> 0.28 B/cell of checkpoint writes at C2 for
-// ~4 more second-sweep rows per half on average.
-#ifndef NW16_CK
-#define NW16_CK  32
-#endif
-static_assert(NW16_CK % 2 == 0 && NW16_CK <= 32, "NW16_CK: even, <= 32 (nw16_fits)");
+// Checkpoint interval of the first sweep, per column form (steps; even: the
+// rotation period).  nw16_fits bounds the rows a second sweep runs past the
+// first by CK + G <= 64: K = 5 has G <= 32 (CK 32), K = 10 G <= 16 and K = 19
+// G = 8 (CK 48).  The checkpoint is 4K+5 dwords (dI is recomputed on restore):
+// round 3 wrote 5K+5 every 24 steps (0.46 B/cell at C2), 4K+5 every 48 is
+// ~0.19 B/cell, for ~8 more second-sweep rows per half on average -- only
+// for the halves the first sweep's predicted window does not cover.
+__host__ __device__ constexpr int nw16_ck(int K) { return K <= 5 ? 32 : 48; }
 // dwords of wave state per lane in a checkpoint (A, B, mcS, u0 per column; I1,
 // I2, outT, outMS, outL); dI is a function of A and I2 there (save())
 __host__ __device__ constexpr int nw16_nst(int K) { return 4 * K + 5; }
@@ -115,7 +114,7 @@ __host__ static inline bool nw16_fits(int64_t ig, int64_t eg, uint64_t xcap, uin
     if (aig > 8191 || aeg > 8191) return false;
     // |T| <= 4*ycols; l0 >= -T - |ig| - |eg|*ycols; u0 drifts at most over
     // xcap + 64 rows (lockstep garbage rows included -- a second sweep runs at
-    // most NW16_CK + G <= 32 + 32 rows past the first one, G <= 32 at K = 5)
+    // most nw16_ck(K) + G <= 64 rows past the first one)
     // and takes u2 + ig + 2eg.  ycols at K = 10 bounds ycols at K = 5 (K = 19
     // asks with its own ycols; its padding columns never feed a real one).
     const uint64_t R = 4 * ycols + aig + aeg * (xcap + 64 + ycols + 2) + 16;
@@ -210,7 +209,7 @@ __host__ __device__ static inline size_t nw16_wave_lds(int GPW, int xstride) {
 // TWO: score-only sweep + checkpoints, then the traceback band (header).
 template <int K, bool LAST, bool TWO, int OFF = 0>
 __device__ __forceinline__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const uint32_t slot) {
-    constexpr int NST = nw16_nst(K), NREC = nw16_nrec(K);
+    constexpr int NST = nw16_nst(K), NREC = nw16_nrec(K), CK = nw16_ck(K);
     constexpr uint32_t RECB = 64u * 4u * NREC;     // traceback bytes per step
     const int G = P.G, GPW = P.GPW;
     const int g = lane / G, gl = lane - g * G;
@@ -457,7 +456,7 @@ __device__ __forceinline__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const
             in0 = pre ? in1 : sN;
             outT = cur[K - 1]; outMS = mfS; outL = l0;
         };
-        // Checkpoint m = the state before step 1 + m*NW16_CK, where the roles
+        // Checkpoint m = the state before step 1 + m*CK, where the roles
         // are (cur, own) = (A, B), (in0, in1) = (I2, I1); register r of lane l
         // at ckw[(m*NST + r)*64] (coalesced).  dI is not stored: the step
         // before a checkpoint ran with (own, in1) = (A, I2) and set dI[s] =
@@ -474,8 +473,8 @@ __device__ __forceinline__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const
             p[4 * K * 64] = I1; p[(4 * K + 1) * 64] = I2;
             p[(4 * K + 2) * 64] = outT; p[(4 * K + 3) * 64] = outMS; p[(4 * K + 4) * 64] = outL;
         };
-        int nextck = 1 + NW16_CK, mck = 1;
-        auto ck = [&](const int t) { if (TWO && t == nextck) { save(mck); ++mck; nextck += NW16_CK; } };
+        int nextck = 1 + CK, mck = 1;
+        auto ck = [&](const int t) { if (TWO && t == nextck) { save(mck); ++mck; nextck += CK; } };
         if (TWO) save(0);
         mark(0);
         // (cur, own) and (in0, in1) swap every step; every loop advances t by 2
@@ -625,13 +624,13 @@ __device__ __forceinline__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const
             int n2 = 0;
             for (int h = 0; h < 2; ++h) {
                 const int lo = bx[h] - (att == 0 ? P.band_w : NW16_BAND2 * P.band_w) - 1;
-                t0h[h] = (att < 2 && lo >= 0) ? 1 + NW16_CK * (lo / NW16_CK) : 1;
+                t0h[h] = (att < 2 && lo >= 0) ? 1 + CK * (lo / CK) : 1;
                 if (todo[h]) n2 = max(n2, bx[h] + G - t0h[h]);
             }
             for (int o = 32; o > 0; o >>= 1) n2 = max(n2, wv_shfl_xor(n2, o));
             {   // restore: half A from its checkpoint, half B from its own
-                const uint32_t *pa = ckw + (uint32_t)((t0h[0] - 1) / NW16_CK) * (NST * 64u);
-                const uint32_t *pb = ckw + (uint32_t)((t0h[1] - 1) / NW16_CK) * (NST * 64u);
+                const uint32_t *pa = ckw + (uint32_t)((t0h[0] - 1) / CK) * (NST * 64u);
+                const uint32_t *pb = ckw + (uint32_t)((t0h[1] - 1) / CK) * (NST * 64u);
                 auto ld = [&](const int r) { return wv_bfi(0x0000FFFFu, pa[r * 64], pb[r * 64]); };
 #pragma unroll
                 for (int s = 0; s < K; ++s) {
@@ -704,9 +703,9 @@ __host__ static inline bool nw16_k19_ok(uint32_t ylen_uni, uint32_t ymax, uint32
 }
 // traceback dwords per wave slot (NREC per lane per step)
 __host__ static inline uint64_t nw16_tb_words(const NwShape &s) { return (uint64_t)s.steps * 64 * nw16_nrec(s.k); }
-// checkpoint dwords per wave slot (two-pass mode): one per NW16_CK steps + the start
+// checkpoint dwords per wave slot (two-pass mode): one per nw16_ck(K) steps + the start
 __host__ static inline uint64_t nw16_ck_words(const NwShape &s) {
-    return (uint64_t)((s.steps + NW16_CK - 1) / NW16_CK + 1) * nw16_nst(s.k) * 64;
+    return (uint64_t)((s.steps + nw16_ck(s.k) - 1) / nw16_ck(s.k) + 1) * nw16_nst(s.k) * 64;
 }
 
 #ifndef IMSAME_WAVE_EMU

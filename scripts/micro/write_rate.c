@@ -105,8 +105,8 @@ int main(int argc, char **argv) {
     const uint64_t total = (uint64_t)(gb * 1e9);
     char path[512];
     snprintf(path, sizeof path, "%s/write_rate.tmp", dir);
-    char *buf = aligned_alloc(1 << 21, (64ull << 20) + (4 << 20));
-    for (uint64_t k = 0; k < (64ull << 20) + (4 << 20); ++k) buf[k] = "ACGT*- \n"[k & 7];
+    char *buf = aligned_alloc(1 << 21, (64ull << 20) + (16 << 20));
+    for (uint64_t k = 0; k < (64ull << 20) + (16 << 20); ++k) buf[k] = "ACGT*- \n"[k & 7];
     const int T[] = {1, 4, 16};
     for (int i = 0; i < 3; ++i)
         printf("buffered pwrite %2d threads: %6.2f GB/s\n", T[i], trial(path, T[i], 0, total, 8 << 20, buf));
