@@ -84,6 +84,39 @@ def nw_kernel_name(read_len, record_bp, igap=-5, egap=-2):
     return "nw16_kernel" if R <= 8191 else "nw_kernel"
 
 
+def nw16_form(read_len, record_bp):
+    """The packed kernel's column form at this shape (imsame_dev.hip:plan_nw,
+    nw16_kernel.hip): the 19-column form when every read has 150 bases and 8
+    groups fit the LDS, else 10 columns per lane."""
+    if read_len == 150 and 8 * ((record_bp + 15) // 16 * 16) <= 16384:
+        K, G, GPW = 19, 8, 8
+    else:
+        K = 10
+        G = -(-read_len // K)
+        GPW = max(1, min(64 // G, 16384 // ((max(record_bp, 2) + 15) // 16 * 16)))
+    nrec = 2 if K <= 8 else 3 if K <= 10 else 2 * ((K + 7) // 8)
+    return {"K": K, "G": G, "GPW": GPW, "nst": 4 * K + 5, "nrec": nrec, "ck": 32 if K <= 5 else 48}
+
+
+def nw16_min_bytes_per_cell(read_len, record_bp):
+    """HBM bytes per DP cell the TWO-PASS kernel cannot avoid:
+    every wave writes its register checkpoint (4K+5 dwords per lane) every CK
+    steps, the traceback of the band the walk reads (the first sweep's
+    predicted window: the read's rows + 32 above + 24 below + the skew G, NREC
+    dwords per lane per step), and reads the record and the read once.
+    Per DP cell of the wave's 2 x GPW candidates."""
+    f = nw16_form(read_len, record_bp)
+    steps = record_bp + f["G"]
+    cells_per_wave_step = 2 * f["GPW"] * read_len * record_bp / steps
+    ck = f["nst"] * 4 * 64 / f["ck"]
+    band = read_len + 32 + 24 + f["G"]
+    tb = f["nrec"] * 4 * 64 * band / steps
+    inp = (record_bp + read_len) / (record_bp * read_len)
+    bpc = (ck + tb) / cells_per_wave_step + inp
+    return {"bytes_per_cell": round(bpc, 4), "checkpoint": round(ck / cells_per_wave_step, 4),
+            "band_traceback": round(tb / cells_per_wave_step, 4), "inputs": round(inp, 5), "form": f}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -354,16 +387,23 @@ def main():
     # the average rocprofv3 --stats reports for that kernel name
     pk_ms = [m for s_ in stats for j, m in enumerate(s_["launch_ms"])
              if ((s_["launch_pk"] >> j) & 1) == (1 if kernel == "nw16_kernel" else 0)]
-    # HBM: the contract's algorithmic figure and the bytes the PMC counters saw
+    # HBM: the contract's algorithmic figure (2 B/cell), the
+    # two-pass kernel's own minimum (nw16_min_bytes_per_cell) and the bytes
+    # the PMC counters saw per cell
     measured = bpc * cells_per_s / 1e9 if bpc and cells_per_s else None
-    hbm = {"basis": "algorithmic bytes (SURVEY 8(d): xlen + ylen + 2 B/cell traceback floor per NW) / NW busy time",
+    tp = nw16_min_bytes_per_cell(a.read_len, a.record_bp) if kernel == "nw16_kernel" else None
+    hbm = {"basis": "CONTRACT figure: algorithmic bytes of SURVEY 8(d) (xlen + ylen + 2 B/cell traceback floor per "
+                    "NW) / NW busy time -- the kernel stores 4 bits per cell of a band, not 2 B per cell",
            "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(achieved / HBM_PEAK_GBS, 4),
+           "two_pass_min": tp,
+           "measured_bytes_per_cell": bpc,
+           "measured_over_two_pass_min": round(bpc / tp["bytes_per_cell"], 3) if bpc and tp else None,
            "measured_gbs": round(measured, 2) if measured else None,
            "measured_frac": round(measured / HBM_PEAK_GBS, 4) if measured else None,
            "measured_basis": "PMC bytes per DP cell (2 x FETCH_SIZE + WRITE_SIZE, %s) x this run's cells/s of NW "
                              "busy time" % os.path.relpath(a.traffic_json, REPO)}
-    valu = valu_roofline(a.valu_json, kernel, a.config, cells_per_s)
+    valu = valu_roofline(a.valu_json, kernel, a.config, cells_per_s, a.read_len, a.record_bp)
     common = {"traffic": traffic,
               "traffic_over_alg": round(traffic / per_launch, 4) if traffic and per_launch else None,
               "kernel": kernel, "launches": nw_launches,
@@ -452,7 +492,7 @@ def main():
 VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 2.0     # wave-instructions / s
 
 
-def valu_roofline(path, kernel, config, cells_per_s):
+def valu_roofline(path, kernel, config, cells_per_s, read_len=150, record_bp=2000):
     """The NW kernel's binding resource is VALU issue.  Lane-
     instructions per cell come from a PMC pass (SQ_INSTS_VALU x 64 / cells of
     the same launches, profiles/nw_valu.json); achieved issue = that x the
@@ -467,10 +507,25 @@ def valu_roofline(path, kernel, config, cells_per_s):
         return None
     ipc = vj["lane_instr_per_cell"]
     rate = ipc * cells_per_s / 64.0
-    return {"instr_per_cell": round(ipc, 3), "achieved": round(rate / 1e9, 2), "issue_peak": round(VALU_ISSUE_PEAK / 1e9, 2),
-            "unit": "G wave-instr/s", "frac": round(rate / VALU_ISSUE_PEAK, 4), "source": os.path.relpath(path, REPO),
-            "note": "peak = 2 cycles per wave instruction; v_pk_*_i16 / v_perm issue at ~4 (profiles/r06_valu_rate.txt),"
-                    " so this instruction mix saturates near 0.5"}
+    out = {"instr_per_cell": round(ipc, 3), "achieved": round(rate / 1e9, 2), "issue_peak": round(VALU_ISSUE_PEAK / 1e9, 2),
+           "unit": "G wave-instr/s", "frac": round(rate / VALU_ISSUE_PEAK, 4), "source": os.path.relpath(path, REPO),
+           "note": "peak = 2 cycles per wave instruction at 2.4 GHz; v_pk_*_i16 / v_perm issue at ~4 "
+                   "(profiles/r06_valu_rate.txt)"}
+    # the measured ceiling of this instruction mix: the first-sweep loop
+    # alone on a full chip (scripts/micro/nw16_loop.py), cycles per VALU per
+    # SIMD -> a fraction of the same 2-cycle peak
+    cp = os.path.join(REPO, "profiles", "nw16_loop_ceiling.json")
+    if os.path.exists(cp):
+        try:
+            cj = json.load(open(cp))
+            if cj.get("kernel") == kernel and cj.get("form") == nw16_form(read_len, record_bp)["K"]:
+                out.update({"mix_ceiling_frac": cj["mix_ceiling_frac"],
+                            "mix_ceiling_cycles_per_valu": cj["cycles_per_valu_per_simd"],
+                            "frac_of_mix_ceiling": round(out["frac"] / cj["mix_ceiling_frac"], 4),
+                            "mix_ceiling_source": os.path.relpath(cp, REPO)})
+        except Exception:
+            pass
+    return out
 
 
 def run_e2e(ref, rst, q, qs, a):

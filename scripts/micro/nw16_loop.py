@@ -2,10 +2,10 @@
 """Measured issue ceiling of nw16_kernel's first-sweep loop.
 
 Runs the packed NW kernel alone on the chip (imsame_dev_nw_pairs: one
-persistent launch, every resident wave slot busy -- 4 waves per SIMD) over
-150-bp reads against 3000-bp records, so ~99 % of each task's sweep steps are
-fast-loop steps, with IMSAME_NW_PROF=1: the kernel sums each wave's s_memtime
-cycles per phase (nw16_kernel.hip `mark`).  From the first-sweep cycles:
+persistent launch, every resident wave slot busy) over 150-bp reads against
+2000-bp records (C2's shape; the column form the library picks for it), with
+IMSAME_NW_PROF=1: the kernel sums each wave's s_memtime cycles (shader
+cycles) per phase (nw16_kernel.hip `mark`).  From the first-sweep cycles:
 
   cycles per 2-step iteration of one wave = sweep1 / (tasks x (xlen+G-1)/2)
   SIMD issue rate = waves/SIMD x VALU per iteration / cycles per iteration
@@ -16,7 +16,8 @@ peak (0.5 wave-instructions per SIMD cycle) is this loop's ceiling: what the
 whole kernel could reach if every step were a fast first-sweep step with the
 chip full and nothing else running.
 
-    python scripts/micro/nw16_loop.py --valu 351 [--pairs 65536] [--out FILE]
+    python scripts/micro/nw16_loop.py --valu 641 [--pairs 65536] [--out FILE]
+    (641: the 19-column form's loop; 351: the 10-column form's, IMSAME_NW_K19=0)
 """
 import argparse
 import json
@@ -85,7 +86,7 @@ def main():
     rate = a.waves_per_simd * a.valu / cyc_iter           # wave-instructions per SIMD cycle
     tot_cyc = sum(r[k] for k in ("setup", "sweep1", "reduce", "sweep2", "walk"))
     ghz = tot_cyc / (r["blocks"] * 4) / (r["ms"] * 1e-3) / 1e9     # s_memtime ticks per second
-    out = {"kernel": "nw16_kernel<10,LAST,TWO>", "what": "first-sweep fast loop, chip full, kernel alone",
+    out = {"kernel": "nw16_kernel", "form": int(r["k"]), "what": "first-sweep fast loop, chip full, kernel alone",
            "pairs": int(r["cand"]), "xlen": a.xlen, "ylen": a.ylen, "G": G, "GPW": GPW, "tasks": tasks,
            "valu_per_iteration": a.valu, "waves_per_simd": a.waves_per_simd,
            "cycles_per_iteration_per_wave": round(cyc_iter, 1),
