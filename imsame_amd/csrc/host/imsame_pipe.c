@@ -132,30 +132,61 @@ typedef struct {
     uint64_t from, to;
     host_text text, scratch;           /* reused across batches */
     uint64_t off;
+    uint64_t bytes;                    /* record bytes of [from, to) (size_task) */
     int fd, err;
 } rtask;
+
+static int digits(uint64_t v) {
+    int d = 1;
+    while (v >= 10) { v /= 10; d++; }
+    return d;
+}
+
+/* bytes of read r's record: the header line of alignmentFunctions.c:167-168
+ * ("(%lu, %lu) : %d%% %d%% %lu\n $$$$$$$ \n": 22 fixed bytes + the digits)
+ * and build_alignment's text (host_render_size) -- a function of the result
+ * row alone, so every record's file offset is known before any is rendered */
+static uint64_t record_size(const host_seqs *db, const imsame_read_result *x, uint64_t r) {
+    const uint64_t yl = x->ylen, s = x->db_seq;
+    const uint64_t pid = 100 * (uint64_t)x->identities / x->length, pcv = 100 * (uint64_t)x->length / yl;
+    const uint64_t head = 22 + digits(r) + digits(s) + digits(pid < 100 ? pid : 100) + digits(pcv < 100 ? pcv : 100) +
+                          digits(yl);
+    return head + host_render_size(db->start[s + 1] - db->start[s], yl, x);
+}
+
+static void *size_task(void *a) {
+    rtask *t = a;
+    uint64_t n = 0;
+    for (uint64_t r = t->from; r < t->to; r++)
+        if (t->res[r].status == 1) n += record_size(t->db, &t->res[r], r);
+    t->bytes = n;
+    return NULL;
+}
+
+/* read r's record appended to t->text */
+static void render_one(rtask *t, uint64_t r) {
+    const imsame_read_result *x = &t->res[r];
+    const uint64_t yl = x->ylen, s = x->db_seq;
+    const uint64_t pid = 100 * (uint64_t)x->identities / x->length, pcv = 100 * (uint64_t)x->length / yl;
+    if (t->text.len + 160 > t->text.cap) {
+        t->text.cap = (t->text.len + 160) * 2 + 65536;
+        char *b = realloc(t->text.buf, t->text.cap);
+        if (!b) { t->err = ENOMEM; return; }
+        t->text.buf = b;
+    }
+    /* alignmentFunctions.c:167-168 */
+    t->text.len += (size_t)snprintf(t->text.buf + t->text.len, 160,
+                                    "(%" PRIu64 ", %" PRIu64 ") : %d%% %d%% %" PRIu64 "\n $$$$$$$ \n", r, s,
+                                    (int)pid < 100 ? (int)pid : 100, (int)pcv < 100 ? (int)pcv : 100, yl);
+    host_render_scratch(t->db->seq + t->db->start[s], t->db->start[s + 1] - t->db->start[s],
+                        t->q->seq + t->q->start[r], yl, x, t->paths + x->path_off, &t->text, &t->scratch);
+}
 
 static void *render_task(void *a) {
     rtask *t = a;
     t->text.len = 0;
-    for (uint64_t r = t->from; r < t->to; r++) {
-        const imsame_read_result *x = &t->res[r];
-        if (x->status != 1) continue;
-        const uint64_t yl = x->ylen, s = x->db_seq;
-        const uint64_t pid = 100 * (uint64_t)x->identities / x->length, pcv = 100 * (uint64_t)x->length / yl;
-        if (t->text.len + 160 > t->text.cap) {
-            t->text.cap = (t->text.len + 160) * 2 + 65536;
-            char *b = realloc(t->text.buf, t->text.cap);
-            if (!b) { t->err = ENOMEM; return NULL; }
-            t->text.buf = b;
-        }
-        /* alignmentFunctions.c:167-168 */
-        t->text.len += (size_t)snprintf(t->text.buf + t->text.len, 160,
-                                        "(%" PRIu64 ", %" PRIu64 ") : %d%% %d%% %" PRIu64 "\n $$$$$$$ \n", r, s,
-                                        (int)pid < 100 ? (int)pid : 100, (int)pcv < 100 ? (int)pcv : 100, yl);
-        host_render_scratch(t->db->seq + t->db->start[s], t->db->start[s + 1] - t->db->start[s],
-                            t->q->seq + t->q->start[r], yl, x, t->paths + x->path_off, &t->text, &t->scratch);
-    }
+    for (uint64_t r = t->from; r < t->to && !t->err; r++)
+        if (t->res[r].status == 1) render_one(t, r);
     return NULL;
 }
 
@@ -169,6 +200,38 @@ static int write_all(int fd, const char *b, uint64_t n, uint64_t off, int seekab
         b += w; n -= (uint64_t)w; off += (uint64_t)w;
     }
     return 0;
+}
+
+static int write_all(int fd, const char *b, uint64_t n, uint64_t off, int seekable);
+
+/* render [from, to) and pwrite it at t->off as it goes, in pieces of
+ * RW_PIECE bytes: rendering and writing overlap within every thread, and the
+ * threads of a part write disjoint ranges at once (the reference's threads
+ * share one FILE*, alignmentFunctions.c:165-168) */
+#define RW_PIECE (4u << 20)
+static void render_one(rtask *t, uint64_t r);
+static void *render_write_task(void *a) {
+    rtask *t = a;
+    t->text.len = 0;
+    uint64_t done = 0;
+    for (uint64_t r = t->from; r < t->to && !t->err; r++) {
+        if (t->res[r].status != 1) continue;
+        render_one(t, r);
+        if (t->text.len >= RW_PIECE) {
+            t->err = write_all(t->fd, t->text.buf, t->text.len, t->off + done, 1);
+            done += t->text.len;
+            t->text.len = 0;
+        }
+    }
+    if (!t->err && t->text.len) t->err = write_all(t->fd, t->text.buf, t->text.len, t->off + done, 1);
+    done += t->text.len;
+    t->text.len = 0;
+    if (!t->err && done != t->bytes) {                 /* record_size must be exact */
+        fprintf(stderr, "[imsame] internal error: rendered %llu bytes, sized %llu\n", (unsigned long long)done,
+                (unsigned long long)t->bytes);
+        t->err = EIO;
+    }
+    return NULL;
 }
 
 static void *write_task(void *a) {
@@ -230,6 +293,36 @@ static int write_part(rtask *t, int nt, int fd, int seekable, double *secs) {
     return err;
 }
 
+/* seekable output: every slice of [from, to) sized (record_size, in
+ * parallel), given its file offset from *off, then rendered and pwritten by
+ * its thread at once -- no stage waits for a whole part's text */
+static int render_write_part(rtask *t, int nt, const host_seqs *db, const host_seqs *q,
+                             const imsame_read_result *res, const uint32_t *paths, uint64_t from, uint64_t to, int fd,
+                             uint64_t *off, pipe_result *r) {
+    if (to <= from) return 0;
+    const uint64_t n = to - from;
+    if ((uint64_t)nt > n) nt = (int)n;
+    for (int k = 0; k < nt; ++k) {
+        t[k].db = db; t[k].q = q; t[k].res = res; t[k].paths = paths; t[k].fd = fd; t[k].err = 0;
+        t[k].from = from + n * (uint64_t)k / (uint64_t)nt;
+        t[k].to = from + n * (uint64_t)(k + 1) / (uint64_t)nt;
+    }
+    const double t0 = pipe_now();
+    run_pool(t, nt, size_task);
+    for (int k = 0; k < nt; ++k) {
+        t[k].off = *off;
+        *off += t[k].bytes;
+    }
+    r->bytes_out = *off;
+    const double t1 = pipe_now();
+    run_pool(t, nt, render_write_task);
+    r->t_render += t1 - t0;                /* sizing */
+    r->t_write += pipe_now() - t1;         /* render + pwrite, fused */
+    for (int k = 0; k < nt; ++k)
+        if (t[k].err) return t[k].err;
+    return 0;
+}
+
 static int render_batch(rtask *t, int nt, const host_seqs *db, const host_seqs *q, const imsame_read_result *res,
                         const uint32_t *paths, uint64_t from, uint64_t to, int fd, int seekable, uint64_t *off,
                         pipe_result *r) {
@@ -280,7 +373,8 @@ int pipe_render_range(const host_seqs *db, const host_seqs *q, const imsame_read
     rtask *t = calloc((size_t)nt, sizeof *t);
     if (!t) return ENOMEM;
     const int seekable = lseek(fd, 0, SEEK_CUR) >= 0;
-    const int err = render_batch(t, nt, db, q, res, paths, from, to, fd, seekable, off, r);
+    const int err = seekable ? render_write_part(t, nt, db, q, res, paths, from, to, fd, off, r)
+                             : render_batch(t, nt, db, q, res, paths, from, to, fd, seekable, off, r);
     for (int k = 0; k < nt; ++k) { free(t[k].text.buf); free(t[k].scratch.buf); }
     free(t);
     return err;
@@ -443,8 +537,12 @@ int pipe_align_render(pipe_dev *d, int G, const host_seqs *db, const host_seqs *
         if (!pt) break;                                     /* done, past the fatal read, or failed */
         nxt = pt->to;
         const uint64_t hi = pt->to < sr ? pt->to : sr;
-        if (rt && !werr && !rc && hi > pt->from) {
-            /* set nrend & 1 was last written two parts ago: that writer is joined */
+        if (rt && !werr && !rc && hi > pt->from && seekable) {
+            /* a file: offsets from the rows, every thread renders and writes */
+            werr = render_write_part(rt, nt, db, q, res, pt->paths, pt->from, hi, o->out_fd, &off, r);
+        } else if (rt && !werr && !rc && hi > pt->from) {
+            /* a pipe: ordered writes.  Set nrend & 1 was last written two
+             * parts ago: that writer is joined */
             rtask *set = rt + (size_t)(nrend & 1) * nt;
             int used = nt;
             werr = render_part(set, &used, db, q, res, pt->paths, pt->from, hi, o->out_fd, &off, r);

@@ -53,7 +53,11 @@ void fake_result(const imsame_ctx *c, uint64_t r, imsame_read_result *o, uint32_
     const uint64_t off = 1 + (r * 37) % (xl - yl - 1);
     o->status = 1; o->db_seq = s;
     o->bx = (uint32_t)(off + yl - 1); o->by = (uint32_t)(yl - 1);
-    o->length = (uint32_t)yl; o->identities = (uint32_t)(yl - r % 5);
+    o->length = (uint32_t)(yl - 1); o->identities = (uint32_t)(yl - 1 - r % 5);
+    /* backtrackingNW's string heads as the device reports them (nw_finish:
+     * M - ((xlen-1-bx) + length + tail), tail = the walk's end px + py = off) */
+    const uint64_t M = 2 * (xl > yl ? xl : yl);
+    o->head_x = (uint32_t)(M - (xl - 1)); o->head_y = (uint32_t)(M - (yl - 1 + off));
     o->path_len = 1;
     *path = (IMSAME_MOVE_DIAG << 30) | (uint32_t)(yl - 1);
 }
