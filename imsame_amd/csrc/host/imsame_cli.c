@@ -227,8 +227,10 @@ int main(int argc, char **argv) {
             ", \"wall_s\": %.4f}\n",
             G, pr.batches, oj.secs, t_parse_db, t_index, t_parse_q, t_upload, pr.t_align, pr.t_render, pr.t_write, pr.t_tail,
             pr.bytes_out, acc, now_s() - t_wall);
+    const double t_close = now_s();
     host_free_seqs(&db);
     host_free_seqs(&q);
     pipe_close(dv, G);
+    fprintf(stderr, "[imsame] teardown {\"close_s\": %.4f}\n", now_s() - t_close);
     return 0;
 }
