@@ -28,6 +28,7 @@
 #include "nw_kernel.hip"
 #include "nw16_kernel.hip"
 #include "nwl_kernel.hip"
+#include "nwp_kernel.hip"
 #include "seed_kernel.hip"
 
 
@@ -378,7 +379,7 @@ static inline const uint64_t *dev_qs(const imsame_ctx *c) {
 // counters block layout (u64 slots)
 enum { C_NCAND = 0, C_NCAND2, C_NNEXT, C_NCANDB, C_NCAND2B, C_NNEXT2, C_WORKB,   // (round 1b: B, 2)
        C_WORK, C_WORK2, C_PATHS, C_FLAGS, C_ERR, C_HITS, C_CELLS, C_NACC, C_REDO,
-       C_PROF, C_WIN = C_PROF + 5, C_DBG, C_NSLOTS = C_DBG + 8 };
+       C_PROF, C_WIN = C_PROF + 5, C_FBK, C_DBG, C_NSLOTS = C_DBG + 8 };
 
 static double now_ms() {
     struct timespec ts; clock_gettime(CLOCK_MONOTONIC, &ts);
@@ -879,7 +880,7 @@ static void timeline_print(const std::vector<imsame_ctx *> &L) {
     }
 }
 
-struct NwPlan { int G, GPW, xcap, xstride, steps, nstr, k; bool pk, last4, two, lng, np; size_t lds; unsigned blocks, max_blocks;
+struct NwPlan { int G, GPW, xcap, xstride, steps, nstr, k; bool pk, last4, two, lng, lp, np; size_t lds; unsigned blocks, max_blocks;
                 uint32_t slot_words;   // np: bitmap words per XCD partition (arena slots = 8 x 32 x slot_words)
                 uint64_t tb_dw, ck_dw, bnd_dw; int band_w; };
 
@@ -890,6 +891,12 @@ static bool nwl_enabled() {
     static bool on = true;
     std::call_once(f, [] { const char *e = getenv("IMSAME_NWL"); on = !(e && !atoi(e)); });
     return on;
+}
+// ... and on packed pairs (nwp_kernel.hip) where the range proof admits the
+// launch (IMSAME_NWP=0 keeps the int32 nwl_kernel, for A/B runs)
+static bool nwp_enabled() {
+    const char *e = getenv("IMSAME_NWP");
+    return !(e && !atoi(e));
 }
 
 // Rows above its best cell the second nw16 sweep keeps (nw16_kernel.hip).  A
@@ -981,22 +988,25 @@ static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, 
         const char *nb = getenv("IMSAME_NWL_BAND");
         pl->band_w = nb ? std::max(1, std::min(NWL_BAND, atoi(nb))) : NWL_BAND_DEF;
     }
+    pl->lp = pl->lng && nwp_enabled() && nwp_fits(p->igap, p->egap, xcap, ymax);
     pl->k = pl->pk ? nw16_k(c, ncand, rounds) : 0;
     if (pl->pk && pl->k == NW16_K && nw16_k19_ok(ylen_uni, ymax, xcap, p)) {
         pl->k = NW16_K19;
         pl->last4 = true;                   // 150 = 8 x 19 - OFF: last column in slot K-1
     }
-    const NwShape sh = pl->pk ? nw16_shape(ymax, xcap, pl->k) : pl->lng ? nwl_shape(ymax, xcap) : nw_shape(ymax, xcap);
+    const NwShape sh = pl->pk ? nw16_shape(ymax, xcap, pl->k) : pl->lp ? nwp_shape(ymax, xcap)
+                     : pl->lng ? nwl_shape(ymax, xcap) : nw_shape(ymax, xcap);
     pl->G = sh.G; pl->GPW = sh.GPW; pl->nstr = sh.nstr; pl->xcap = sh.xcap; pl->xstride = sh.xstride;
     pl->steps = sh.steps;
-    pl->tb_dw = pl->pk ? nw16_tb_words(sh) : pl->lng ? nwl_tb_words(sh, ymax) : nw_tb_words(sh);
-    pl->ck_dw = pl->two ? nw16_ck_words(sh) : pl->lng ? nwl_ck_words(sh) : 0;
-    pl->bnd_dw = pl->lng ? nwl_seam_words(sh) : 3ull * pl->xcap;
+    pl->tb_dw = pl->pk ? nw16_tb_words(sh) : pl->lp ? nwp_tb_words(sh, ymax) : pl->lng ? nwl_tb_words(sh, ymax) : nw_tb_words(sh);
+    pl->ck_dw = pl->two ? nw16_ck_words(sh) : pl->lp ? nwp_ck_words(sh) : pl->lng ? nwl_ck_words(sh) : 0;
+    pl->bnd_dw = pl->lp ? nwp_seam_words(sh) : pl->lng ? nwl_seam_words(sh) : 3ull * pl->xcap;
     pl->lds = (size_t)wpb * (pl->pk ? nw16_wave_lds(pl->GPW, pl->xstride)
                              : pl->lng ? nwl_wave_lds(pl->xstride) : nw_wave_lds(pl->GPW, pl->xstride));
     int per_cu = 0;
     const bool k5 = pl->k == NW16_K5, k19 = pl->k == NW16_K19;
-    hipError_t oe = pl->lng ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nwl_kernel, wpb * 64, pl->lds)
+    hipError_t oe = pl->lp ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nwp_kernel, wpb * 64, pl->lds)
+                  : pl->lng ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nwl_kernel, wpb * 64, pl->lds)
                   : k19 ? (pl->two ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
                                          &per_cu, nw16_kernel<NW16_K19, true, true, NW16_K19_OFF>, wpb * 64, pl->lds)
                                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(
@@ -1038,7 +1048,7 @@ static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, 
         else { pl->tb_dw = tb_dw; pl->ck_dw = ck_dw; }
     }
     if (!pl->np) { per_cu = std::min(per_cu, 8); part_cu = per_cu; }
-    const uint32_t cpw = pl->pk ? 2 * pl->GPW : pl->GPW;            // candidates per wave pull
+    const uint32_t cpw = (pl->pk || pl->lp) ? 2 * pl->GPW : pl->GPW;    // candidates per wave pull
     const uint64_t waves_needed = (ncand + cpw - 1) / cpw;
     pl->slot_words = (uint32_t)((((uint64_t)c->ncu / 8) * part_cu * wpb + 31) / 32);
     pl->blocks = (unsigned)std::max<uint64_t>(1, pl->np ? (waves_needed + wpb - 1) / wpb
@@ -1202,7 +1212,14 @@ static int launch_nw(imsame_ctx *c, NwPlan &pl, const uint32_t *cread, const uin
         P.win_bottom = wb ? atoi(wb) : NW16_WIN_BOTTOM;
     }
     const bool k5 = pl.k == NW16_K5;
-    if (pl.lng)                        nwl_kernel<<<pl.blocks, 256, pl.lds, s>>>(P);
+    if (pl.lp) {
+        P.rlim = (int32_t)nwp_rlim(ig, eg, (uint64_t)pl.xcap, ymax);
+        const char *ns = getenv("IMSAME_NWP_S");          // tests: a tiny spread drives the int32 fallback
+        P.nwp_s = ns ? atoi(ns) : 0;
+        P.fbk = (uint32_t *)(ctr + C_FBK);
+    }
+    if (pl.lp)                         nwp_kernel<<<pl.blocks, 256, pl.lds, s>>>(P);
+    else if (pl.lng)                   nwl_kernel<<<pl.blocks, 256, pl.lds, s>>>(P);
     else if (pl.k == NW16_K19 && pl.two) nw16_kernel<NW16_K19, true, true, NW16_K19_OFF><<<pl.blocks, 256, pl.lds, s>>>(P);
     else if (pl.k == NW16_K19)         nw16_kernel<NW16_K19, true, false, NW16_K19_OFF><<<pl.blocks, 256, pl.lds, s>>>(P);
     else if (pl.two && pl.last4 && k5) nw16_kernel<NW16_K5, true, true><<<pl.blocks, 256, pl.lds, s>>>(P);
@@ -1217,7 +1234,7 @@ static int launch_nw(imsame_ctx *c, NwPlan &pl, const uint32_t *cread, const uin
     else                  nw_kernel<false><<<pl.blocks, 256, pl.lds, s>>>(P);
     HIPCHK(hipEventRecord(e1, s));
     HIPCHK(hipGetLastError());
-    POISON_SYNC(s, pl.pk ? "nw16_kernel" : pl.lng ? "nwl_kernel" : "nw_kernel", c);
+    POISON_SYNC(s, pl.pk ? "nw16_kernel" : pl.lp ? "nwp_kernel" : pl.lng ? "nwl_kernel" : "nw_kernel", c);
     return wait ? nw_launch_done(c, qi, n, ms) : 0;
 }
 
@@ -1492,6 +1509,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
                 if (pl.pk && pl.k == NW16_K5) st.launch_k5 |= 1ull << st.nw_launches;
                 if (pl.np) st.launch_np |= 1ull << st.nw_launches;
                 if (pl.pk && pl.k == NW16_K19) st.launch_k19 |= 1ull << st.nw_launches;
+                if (pl.lp) st.launch_nwp |= 1ull << st.nw_launches;
             }
             st.ms_nw += ms; st.nw_launches++; st.n_nw += nc;
         };
@@ -1669,6 +1687,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     st.n_accepted = hc[C_NACC];
     st.nw_redo = (uint32_t)hc[C_REDO];
     st.nw_win = (uint32_t)hc[C_WIN];
+    st.nw_fallback = (uint32_t)hc[C_FBK];
     if (getenv("IMSAME_NW_PROF")) {           // diagnostics: nw16 phase cycles (summed over waves)
         const double tot = (double)(hc[C_PROF] + hc[C_PROF + 1] + hc[C_PROF + 2] + hc[C_PROF + 3] + hc[C_PROF + 4]);
         fprintf(stderr, "[nwprof] setup %.3f sweep1 %.3f reduce %.3f sweep2 %.3f walk %.3f (fractions of %.4g wave-cycles)\n",
@@ -1880,7 +1899,7 @@ static int align_impl(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint6
     }
     imsame_stats st = S[0];
     std::vector<std::pair<float, float>> iv = c->nw_iv;
-    st.nw_launches = 0; st.launch_pk = 0; st.launch_k5 = 0; st.launch_np = 0;
+    st.nw_launches = 0; st.launch_pk = 0; st.launch_k5 = 0; st.launch_np = 0; st.launch_k19 = 0; st.launch_nwp = 0;
     for (int k = 0; k < nl; ++k) {
         const imsame_stats &x = S[k];
         if (k) {
@@ -1888,7 +1907,7 @@ static int align_impl(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint6
             st.n_hits += x.n_hits; st.rounds = std::max(st.rounds, x.rounds);
             if (x.err_read < st.err_read) { st.err_read = x.err_read; st.err_dbseq = x.err_dbseq; }
             st.ms_seed += x.ms_seed; st.ms_nw += x.ms_nw; st.nw_bytes += x.nw_bytes; st.n_rewalk += x.n_rewalk;
-            st.nw_redo += x.nw_redo; st.nw_win += x.nw_win;
+            st.nw_redo += x.nw_redo; st.nw_win += x.nw_win; st.nw_fallback += x.nw_fallback;
             st.ms_setup = std::max(st.ms_setup, x.ms_setup); st.ms_d2h += x.ms_d2h;
             iv.insert(iv.end(), L[k]->nw_iv.begin(), L[k]->nw_iv.end());
         }
@@ -1898,6 +1917,8 @@ static int align_impl(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint6
             if ((x.launch_pk >> j) & 1) st.launch_pk |= 1ull << (st.nw_launches + j);
             if ((x.launch_k5 >> j) & 1) st.launch_k5 |= 1ull << (st.nw_launches + j);
             if ((x.launch_np >> j) & 1) st.launch_np |= 1ull << (st.nw_launches + j);
+            if ((x.launch_k19 >> j) & 1) st.launch_k19 |= 1ull << (st.nw_launches + j);
+            if ((x.launch_nwp >> j) & 1) st.launch_nwp |= 1ull << (st.nw_launches + j);
         }
         st.nw_launches += x.nw_launches;
     }
@@ -2191,6 +2212,9 @@ extern "C" int imsame_dev_nw_pairs(imsame_ctx *c, const uint8_t *xs, const uint6
                 (unsigned long long)hc[C_PROF], (unsigned long long)hc[C_PROF + 1], (unsigned long long)hc[C_PROF + 2],
                 (unsigned long long)hc[C_PROF + 3], (unsigned long long)hc[C_PROF + 4], ms);
     }
+    if (getenv("IMSAME_NW_PROF") && pl.lng)   // diagnostics: which long-read kernel, waves that fell back
+        fprintf(stderr, "[nwprof-long] kernel %s blocks %u cand %llu fallback %llu ms %.4f\n",
+                pl.lp ? "nwp" : "nwl", pl.blocks, (unsigned long long)npairs, (unsigned long long)hc[C_FBK], ms);
     int ret = IMSAME_OK;
     if (p->want_paths) {
         if (paths_used) *paths_used = (uint32_t)hc[C_PATHS];

@@ -140,6 +140,27 @@ WV_DEVICE uint32_t base_code(uint8_t b) { return (b >> 1) & 3u; }          // A0
 #define NW16_TBL_LO 0xFCFCFC04u
 #define NW16_TBL_HI 0xFFFFFF00u
 
+// cell s of half h in one lane's traceback words of a step (layout above) ->
+// nw_kernel.hip's nibble: move (0 diag, 1 up, 2 left) | U << 2 | L << 3
+template <int K>
+WV_DEVICE uint32_t tb16_nib(const uint32_t *w, const int s, const int h) {
+    uint32_t nd, up, U, nL;
+    if (K > 10) {
+        const uint32_t wm = w[2 * (s >> 3)], wu = w[2 * (s >> 3) + 1], q = (uint32_t)(s & 7);
+        nd = (wm >> (8 * h + q)) & 1u; up = (wm >> (16 + 8 * h + q)) & 1u;
+        U = (wu >> (16 * h + q)) & 1u; nL = (wu >> (16 * h + 8 + q)) & 1u;
+    } else if (s < 8) {
+        const uint32_t wm = w[0], wu = w[1];
+        nd = (wm >> (8 * h + s)) & 1u; up = (wm >> (16 + 8 * h + s)) & 1u;
+        U = (wu >> (16 * h + s)) & 1u; nL = (wu >> (16 * h + 8 + s)) & 1u;
+    } else {
+        const uint32_t wx = w[2], q = (uint32_t)(s - 8);
+        nd = (wx >> (8 * h + q)) & 1u; up = (wx >> (16 + 8 * h + q)) & 1u;
+        U = (wx >> (16 * h + 2 + q)) & 1u; nL = (wx >> (16 * h + 4 + q)) & 1u;
+    }
+    return (nd ? (up ? 1u : 2u) : 0u) | (U << 2) | ((nL ^ 1u) << 3);
+}
+
 // traceback of half h of group g (layout above) -> nw_kernel.hip's nibble
 // t0: step of the sweep that wrote record 0 (0: one pass, steps indexed by t;
 // two passes: the half's restart step, cells before it were not written)
@@ -150,22 +171,7 @@ struct TbAcc16 {
     __device__ bool has(int i, int j) const { const int t = i + (j + OFF) / K; return t >= t0 && t < t1; }
     __device__ uint32_t nib(int i, int j) const {
         const int l = (j + OFF) / K, s = (j + OFF) - l * K;
-        const uint32_t *w = tb + ((uint32_t)(i + l - t0) * 64u + (uint32_t)(g * G + l)) * (uint32_t)nw16_nrec(K);
-        uint32_t nd, up, U, nL;
-        if (K > 10) {
-            const uint32_t wm = w[2 * (s >> 3)], wu = w[2 * (s >> 3) + 1], q = (uint32_t)(s & 7);
-            nd = (wm >> (8 * h + q)) & 1u; up = (wm >> (16 + 8 * h + q)) & 1u;
-            U = (wu >> (16 * h + q)) & 1u; nL = (wu >> (16 * h + 8 + q)) & 1u;
-        } else if (s < 8) {
-            const uint32_t wm = w[0], wu = w[1];
-            nd = (wm >> (8 * h + s)) & 1u; up = (wm >> (16 + 8 * h + s)) & 1u;
-            U = (wu >> (16 * h + s)) & 1u; nL = (wu >> (16 * h + 8 + s)) & 1u;
-        } else {
-            const uint32_t wx = w[2], q = (uint32_t)(s - 8);
-            nd = (wx >> (8 * h + q)) & 1u; up = (wx >> (16 + 8 * h + q)) & 1u;
-            U = (wx >> (16 * h + 2 + q)) & 1u; nL = (wx >> (16 * h + 4 + q)) & 1u;
-        }
-        return (nd ? (up ? 1u : 2u) : 0u) | (U << 2) | ((nL ^ 1u) << 3);
+        return tb16_nib<K>(tb + ((uint32_t)(i + l - t0) * 64u + (uint32_t)(g * G + l)) * (uint32_t)nw16_nrec(K), s, h);
     }
     __device__ bool match(int i, int j) const { return ((X[i] >> (2 * h)) & 3u) == base_code(Y[j]); }
 };

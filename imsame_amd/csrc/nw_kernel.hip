@@ -74,6 +74,12 @@ struct NwLaunch {
     // taken from a bitmap of free slots in the partition of the XCD it runs on
     // (NULL: persistent launch, slot = the wave's index in the grid)
     uint32_t *slot_bits; uint32_t slot_words;   // words per XCD partition
+    // packed long-read kernel (nwp_kernel.hip): |ig| + |eg| (L + 64) of the
+    // launch (nwp_fits), the T spread checked every block, and the count of
+    // waves that found a value outside the proof's range (their pairs ran
+    // through the int32 nwl_cand instead)
+    int32_t rlim, nwp_s;
+    uint32_t *fbk;
 };
 
 // LDS bytes one wave needs

@@ -109,7 +109,9 @@ struct NwlWalk {
     bool bad, done, need;
 };
 
-__device__ void nwl_walk_band(const NwlBand &bd, NwlWalk &w, const int lane, uint32_t *path, int &guard) {
+// (Band: NwlBand here, NwpBand for the packed long kernel -- has / nib / match)
+template <class Band>
+__device__ void nwl_walk_band(const Band &bd, NwlWalk &w, const int lane, uint32_t *path, int &guard) {
     w.need = false;
     while (!w.done && !w.bad && !w.need) {
         if (w.px <= 0 || w.py <= 0) { w.done = true; break; }
@@ -184,7 +186,8 @@ __device__ void nwl_walk_band(const NwlBand &bd, NwlWalk &w, const int lane, uin
     }
 }
 
-__device__ void nwl_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const uint32_t slot) {
+// candidate c, start to finish (its own LDS record, seams, checkpoints, band)
+__device__ void nwl_cand(const NwLaunch &P, uint8_t *wsm, const int lane, const uint32_t slot, const uint32_t c) {
     constexpr int K = NWL_K;
     const int ig = P.igap, eg = P.egap, IGE = ig + eg;
     uint8_t *X4 = wsm;
@@ -197,11 +200,7 @@ __device__ void nwl_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const 
     uint32_t *ckw = P.ck + (uint64_t)slot * P.ck_wave_dw + lane;
     const int ncks = nwl_ncks(P.steps);
     const int band = (P.band_w > 0 && P.band_w < NWL_BAND) ? P.band_w : NWL_BAND;   // tests: small bands
-    for (;;) {
-        uint32_t c = 0;
-        if (lane == 0) c = wv_atomic_add(P.counter, 1u);
-        c = wv_first(c);
-        if (c >= P.n_cand) break;
+    {
         const uint32_t rd = P.cand_read[c], sid = P.cand_sid[c];
         const uint64_t xo = P.db_start[sid];
         const int xlen = (int)(P.db_start[sid + 1] - xo);
@@ -527,6 +526,16 @@ __device__ void nwl_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const 
         }
         if (P.redo && lane == 0 && nband > nstr) wv_atomic_add(P.redo, (uint32_t)(nband - nstr));
         wv_mem_sync();
+    }
+}
+
+__device__ void nwl_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const uint32_t slot) {
+    for (;;) {
+        uint32_t c = 0;
+        if (lane == 0) c = wv_atomic_add(P.counter, 1u);
+        c = wv_first(c);
+        if (c >= P.n_cand) break;
+        nwl_cand(P, wsm, lane, slot, c);
     }
 }
 

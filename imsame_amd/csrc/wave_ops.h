@@ -31,6 +31,8 @@ WV_DEVICE bool wv_any(bool p) { return __any(p); }
 WV_DEVICE int wv_shfl(int v, int src) { return __shfl(v, src); }
 WV_DEVICE int wv_shfl_xor(int v, int m) { return __shfl_xor(v, m); }
 WV_DEVICE uint32_t wv_first(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+// lane l's v (wave-uniform; every lane must be active)
+WV_DEVICE int wv_readlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 WV_DEVICE uint32_t wv_atomic_add(uint32_t *p, uint32_t v) { return atomicAdd(p, v); }
 WV_DEVICE void wv_atomic_or(uint32_t *p, uint32_t v) { atomicOr(p, v); }
 WV_DEVICE void wv_atomic_min64(unsigned long long *p, unsigned long long v) { atomicMin(p, v); }
@@ -61,6 +63,9 @@ WV_DEVICE uint32_t pk_max(uint32_t a, uint32_t b) { return pk_u(__builtin_elemen
 typedef unsigned short wv_u2 __attribute__((ext_vector_type(2)));
 WV_DEVICE uint32_t pk_maxu(uint32_t a, uint32_t b) {                                             // v_pk_max_u16
     return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(wv_u2, a), __builtin_bit_cast(wv_u2, b)));
+}
+WV_DEVICE uint32_t pk_minu(uint32_t a, uint32_t b) {                                             // v_pk_min_u16
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(wv_u2, a), __builtin_bit_cast(wv_u2, b)));
 }
 // 0xFFFF in each half that is negative.  Opaque on purpose: seen as a sign
 // splat, LLVM turns the bfi/and_or users into per-half v_cmp + v_cndmask.
@@ -171,6 +176,7 @@ inline int wv_shfl(int v, int src) {
 }
 inline int wv_shfl_xor(int v, int m) { return wv_shfl(v, wvemu::t_lane ^ m); }
 inline uint32_t wv_first(uint32_t v) { return (uint32_t)wv_shfl((int)v, 0); }
+inline int wv_readlane(int v, int l) { return wv_shfl(v, l); }
 inline uint32_t wv_atomic_add(uint32_t *p, uint32_t v) {
     return __atomic_fetch_add(p, v, __ATOMIC_SEQ_CST);
 }
@@ -193,6 +199,10 @@ inline uint32_t pk_sub(uint32_t a, uint32_t b) { return pk_map(a, b, [](int x, i
 inline uint32_t pk_max(uint32_t a, uint32_t b) { return pk_map(a, b, [](int x, int y) { return x > y ? x : y; }); }
 inline uint32_t pk_maxu(uint32_t a, uint32_t b) {
     const uint32_t lo = std::max(a & 0xFFFFu, b & 0xFFFFu), hi = std::max(a >> 16, b >> 16);
+    return lo | (hi << 16);
+}
+inline uint32_t pk_minu(uint32_t a, uint32_t b) {
+    const uint32_t lo = std::min(a & 0xFFFFu, b & 0xFFFFu), hi = std::min(a >> 16, b >> 16);
     return lo | (hi << 16);
 }
 inline uint32_t pk_neg_mask(uint32_t a) { return pk_map(a, 0, [](int x, int) { return x < 0 ? -1 : 0; }); }

@@ -141,6 +141,12 @@ typedef struct imsame_stats {
     uint64_t launch_k19;    /* bit k: packed NW launch k ran the 19-column
                                form (8 lanes per pair, reads of one length
                                150: every lane of the wave busy)          */
+    uint64_t launch_nwp;    /* bit k: NW launch k ran the packed long-read
+                               kernel (two long reads per wave, int16
+                               halves in per-lane frames)                 */
+    uint64_t nw_fallback;   /* packed long-read waves whose values left the
+                               int16 range proof: their pairs ran the int32
+                               long-read path instead (same results)      */
 } imsame_stats;
 
 typedef struct imsame_ctx imsame_ctx;

@@ -30,6 +30,7 @@ void sync() { t_wave->bar.arrive_and_wait(); }
 #include "../../imsame_amd/csrc/nw_kernel.hip"
 #include "../../imsame_amd/csrc/nw16_kernel.hip"
 #include "../../imsame_amd/csrc/nwl_kernel.hip"
+#include "../../imsame_amd/csrc/nwp_kernel.hip"
 #include "../../imsame_amd/csrc/seed_kernel.hip"
 
 static void run_wave(const std::function<void(int)> &f) {
@@ -57,6 +58,15 @@ extern "C" uint32_t emu_win_count(void) { const uint32_t r = g_win; g_win = 0; r
 // packed launches that ran the 19-column form (nw16_k19_ok), since the last emu_k19_count()
 static uint32_t g_k19;
 extern "C" uint32_t emu_k19_count(void) { const uint32_t r = g_k19; g_k19 = 0; return r; }
+// long-read launches that ran the packed kernel (nwp_fits), and its waves that
+// fell back to the int32 path, since the last emu_nwp_count()
+static uint32_t g_nwp, g_fbk;
+extern "C" uint32_t emu_nwp_count(uint32_t *fallbacks) {
+    const uint32_t r = g_nwp;
+    if (fallbacks) *fallbacks = g_fbk;
+    g_nwp = g_fbk = 0;
+    return r;
+}
 
 static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, const uint64_t *qs,
                   const uint32_t *cread, const uint32_t *csid, uint32_t n, const imsame_params *p, uint32_t ymax,
@@ -69,6 +79,8 @@ static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, cons
     const bool two = pk && !(p->flags & IMSAME_FLAG_NW16_ONEPASS) && !(op && atoi(op));
     const char *le = getenv("IMSAME_NWL");
     const bool lng = !pk && !(p->flags & IMSAME_FLAG_NW32) && !(le && !atoi(le)) && nwl_fits(p->igap, p->egap, ymax);
+    const char *pe = getenv("IMSAME_NWP");
+    const bool lp = lng && !(pe && !atoi(pe)) && nwp_fits(p->igap, p->egap, xmax, ymax);
     // columns per lane of the packed kernel: imsame_dev.hip:nw16_k picks by the
     // chip's fill; here IMSAME_NW_K=5 selects the latency-bound form
     const char *ke = getenv("IMSAME_NW_K");
@@ -76,12 +88,14 @@ static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, cons
     for (uint32_t k = 0; k < n; ++k) if (qs[cread[k] + 1] - qs[cread[k]] != yuni) yuni = 0;
     const int K = (ke && atoi(ke) == NW16_K5) ? NW16_K5
                 : (pk && nw16_k19_ok(yuni, ymax, xmax, p)) ? NW16_K19 : NW16_K;
-    const NwShape sh = pk ? nw16_shape(ymax, xmax, K) : lng ? nwl_shape(ymax, xmax) : nw_shape(ymax, xmax);
-    std::vector<uint32_t> tb((pk ? nw16_tb_words(sh) : lng ? nwl_tb_words(sh, ymax) : nw_tb_words(sh)) + 64, 0xABABABABu);
-    std::vector<uint32_t> ck(two ? nw16_ck_words(sh) : lng ? nwl_ck_words(sh) : 1, 0xCDCDCDCDu);
+    const NwShape sh = pk ? nw16_shape(ymax, xmax, K) : lp ? nwp_shape(ymax, xmax) : lng ? nwl_shape(ymax, xmax)
+                     : nw_shape(ymax, xmax);
+    std::vector<uint32_t> tb((pk ? nw16_tb_words(sh) : lp ? nwp_tb_words(sh, ymax) : lng ? nwl_tb_words(sh, ymax)
+                              : nw_tb_words(sh)) + 64, 0xABABABABu);
+    std::vector<uint32_t> ck(two ? nw16_ck_words(sh) : lp ? nwp_ck_words(sh) : lng ? nwl_ck_words(sh) : 1, 0xCDCDCDCDu);
     const char *be = getenv("IMSAME_NW_BAND");
     // seam scratch poisoned like fresh device memory: a read before its write shows
-    std::vector<int32_t> bnd((lng ? nwl_seam_words(sh) : (size_t)3 * sh.xcap) + 64, 0x70000000);
+    std::vector<int32_t> bnd((lp ? nwp_seam_words(sh) : lng ? nwl_seam_words(sh) : (size_t)3 * sh.xcap) + 64, 0x70000000);
     std::vector<uint8_t> lds((pk ? nw16_wave_lds(sh.GPW, sh.xstride)
                               : lng ? nwl_wave_lds(sh.xstride) : nw_wave_lds(sh.GPW, sh.xstride)) + 64, 0xA5);
     uint32_t counter = 0;
@@ -105,6 +119,12 @@ static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, cons
         P.band_w = nb ? std::max(1, std::min(NWL_BAND, atoi(nb))) : NWL_BAND_DEF;
     }
     P.redo = &g_redo;
+    if (lp) {                                             // imsame_dev.hip:launch_nw
+        P.rlim = (int32_t)nwp_rlim(p->igap, p->egap, (uint64_t)sh.xcap, ymax);
+        const char *ns = getenv("IMSAME_NWP_S");
+        P.nwp_s = ns ? atoi(ns) : 0;
+        P.fbk = &g_fbk;
+    }
     // queue order by predicted row, as imsame_dev.hip:launch_nw (row_bucket:
     // 8-row buckets, unpredicted first; stable here, any order is correct)
     std::vector<uint32_t> perm;
@@ -128,7 +148,11 @@ static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, cons
     P.win = &g_win;
     bool ymult = true;        // every read length a multiple of NW16_K (imsame_dev.hip: q_len_mult)
     for (uint32_t k = 0; k < n; ++k) ymult = ymult && (qs[cread[k] + 1] - qs[cread[k]]) % NW16_K == 0;
-    if (lng)              run_wave([&](int lane) { nwl_wave(P, lds.data(), lane, 0); });
+    if (lp) {
+        ++g_nwp;
+        run_wave([&](int lane) { nwp_wave(P, lds.data(), lane, 0); });
+    }
+    else if (lng)         run_wave([&](int lane) { nwl_wave(P, lds.data(), lane, 0); });
     else if (pk && K == NW16_K19) {
         ++g_k19;
         if (two) run_wave([&](int lane) { nw16_wave<NW16_K19, true, true, NW16_K19_OFF>(P, lds.data(), lane, 0); });

@@ -294,6 +294,38 @@ def test_long_two_pass_nw_vs_oracle(dev, oracle, band, monkeypatch):
             assert txt == o["text"], k
 
 
+@pytest.mark.parametrize("mode", ["nwp", "nwl", "fallback"])
+def test_packed_long_nw_kernels(dev, oracle, mode, monkeypatch, capfd):
+    """nwp_kernel.hip (two long reads per wave, int16 halves in per-lane
+    frames) against the oracle, against the int32 nwl_kernel (IMSAME_NWP=0)
+    and with a 4-point spread limit (IMSAME_NWP_S=4) that sends every wave
+    to the int32 fallback (nwl_cand) -- the kernel that ran and its fallback
+    count read from the launch's diagnostics line."""
+    from tests.test_host import _long_pairs
+    monkeypatch.setenv("IMSAME_NW_PROF", "1")
+    if mode == "nwl":
+        monkeypatch.setenv("IMSAME_NWP", "0")
+    if mode == "fallback":
+        monkeypatch.setenv("IMSAME_NWP_S", "4")
+    X, Y = _long_pairs(31, 25, 3001, 3001)          # odd: the last wave's B half repeats A
+    p = dev.params(igap=-5, egap=-2, min_coverage=1e-9, min_identity=1e-9)
+    capfd.readouterr()
+    res, paths, _ = dev.nw_pairs(X, Y, p, want_paths=True)
+    err = capfd.readouterr().err
+    line = [l for l in err.splitlines() if l.startswith("[nwprof-long]")]
+    assert line, err[-2000:]
+    f = line[-1].split()
+    kern, fbk = f[f.index("kernel") + 1], int(f[f.index("fallback") + 1])
+    assert kern == ("nwl" if mode == "nwl" else "nwp"), line
+    assert (fbk == 0) if mode == "nwp" else (fbk > 0 if mode == "fallback" else True), line
+    for k in range(len(X)):
+        o = oracle.nw(X[k], Y[k], igap=-5, egap=-2, text=True)
+        for fld in ("score", "bx", "by", "length", "identities", "igaps", "egaps", "head_x", "head_y"):
+            assert int(res[k][fld]) == int(o[fld]), (fld, k, len(X[k]), len(Y[k]))
+        txt, _ = render(X[k], Y[k], res[k], paths[res[k]["path_off"]:res[k]["path_off"] + res[k]["path_len"]])
+        assert txt == o["text"], k
+
+
 def _windows(n, w=1500, T=16):
     """start, middle (around a chunk head of -n_threads T) and end of a query"""
     rpt = n // T
@@ -720,6 +752,8 @@ def test_c5_full_50mbp_database(dev, oracle_memo, rec_bp, cap):
     assert not _cmp(res, exp), _cmp(res, exp)
     if rec_bp > 10_000:
         assert st.n_nw > 0 and (res["status"] == 1).sum() >= 3
+        # the packed long-read kernel ran every long launch, none fell back
+        assert st.launch_nwp != 0 and st.nw_fallback == 0, (hex(st.launch_nwp), st.nw_fallback)
     else:
         assert st.n_nw == 0 and st.n_hits == 0 and (res["status"] == 1).sum() == 0
 

@@ -363,6 +363,33 @@ def test_emulated_long_two_pass_nw_vs_oracle(emu, oracle, band, monkeypatch):
     assert (extra > 20) if band == "70" else True
 
 
+@pytest.mark.parametrize("mode", ["nwp", "fallback"])
+def test_emulated_packed_long_nw(emu, oracle, mode, monkeypatch):
+    """nwp_kernel.hip (emulated): two long reads per wave in int16 halves,
+    each lane in its own frame -- every field equal to the oracle's with no
+    wave leaving the range proof; with a 4-point spread limit (IMSAME_NWP_S)
+    every wave falls back to the int32 nwl_cand and the rows are the same."""
+    cnt = emu.lib.emu_nwp_count
+    cnt.restype = C.c_uint32
+    cnt.argtypes = [C.POINTER(C.c_uint32)]
+    fb = C.c_uint32(0)
+    cnt(C.byref(fb))
+    if mode == "fallback":
+        monkeypatch.setenv("IMSAME_NWP_S", "4")
+    X, Y = _long_pairs(11, 6, 1300, 1500)
+    p = oracle.params(igap=-5, egap=-2, want_paths=1, min_coverage=1e-9, min_identity=1e-9)
+    rc, res, paths, fl = emu.nw_pairs(X, Y, p, paths_cap=100_000)
+    assert rc == 0 and fl == 0
+    assert cnt(C.byref(fb)) == 1
+    assert (fb.value == 0) if mode == "nwp" else (fb.value == 3), fb.value
+    for k in range(len(X)):
+        o = oracle.nw(X[k], Y[k], igap=-5, egap=-2, text=True)
+        for f in ("score", "bx", "by", "length", "identities", "igaps", "egaps", "head_x", "head_y"):
+            assert int(res[k][f]) == int(o[f]), (f, k)
+        txt, _ = imsame_amd.render(X[k], Y[k], res[k], paths[res[k]["path_off"]:res[k]["path_off"] + res[k]["path_len"]])
+        assert txt == o["text"], k
+
+
 def _strip_mix_pairs():
     """163- and 400-column reads in ONE launch: the launch takes the
     multi-strip kernel (ymax > 320) and the 163-column reads have one strip."""
