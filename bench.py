@@ -63,7 +63,7 @@ CONFIGS = {
                         "MAX_READ_SIZE raised to 10001, BASELINE.json configs[4] (2 kbp records: every hit is "
                         "rejected a priori, seed scan only)"),
     # C5 against records long enough to hold a read: the long-read NW runs
-    # (10 kbp x 12 kbp = 120M cells per candidate, int32 multi-strip kernel)
+    # (10 kbp x 12 kbp = 120M cells per candidate, the packed long-read kernel)
     "c5w": dict(reads=4_096, read_len=10_000, ref_bp=50_004_000, record_bp=12_001, ont=True, max_rs=12_001,
                 cpu_sample=0, seeds=(42, 48),
                 workload="C5w: 10 kbp ONT-like reads vs 50 Mbp synthetic reference in 12,001 bp records, "
@@ -76,7 +76,12 @@ def nw_kernel_name(read_len, record_bp, igap=-5, egap=-2):
     """The NW kernel imsame_dev.hip:plan_nw picks for this shape (mirror of
     nw16_kernel.hip:nw16_fits for the default gap parameters)."""
     if read_len > 160:
-        return "nw_kernel" if igap > 0 or egap > 0 else "nwl_kernel"     # nwl_kernel.hip: long reads
+        if igap > 0 or egap > 0:
+            return "nw_kernel"
+        # nwp_kernel.hip:nwp_fits (2 NWP_S2 + |ig| + |eg| (L + 64) + 116 <= 32767): packed
+        # pairs, else the int32 nwl_kernel.hip
+        fits = -igap <= 1024 and -egap <= 16 and 2 * 2308 - igap - egap * (max(read_len, record_bp) + 64) + 116 <= 32767
+        return "nwp_kernel" if fits else "nwl_kernel"
     if igap > 0 or egap > 0:
         return "nw_kernel"
     ycols = -(-read_len // 10) * 10
@@ -385,8 +390,10 @@ def main():
     # launches of the dominant kernel alone (imsame_stats.launch_pk: packed
     # nw16_kernel vs the int32 nw_kernel that takes the small last launches),
     # the average rocprofv3 --stats reports for that kernel name
+    # (launch_nwp: the packed long-read nwp_kernel vs the int32 nwl_kernel)
+    kbits = "launch_nwp" if kernel in ("nwp_kernel", "nwl_kernel") else "launch_pk"
     pk_ms = [m for s_ in stats for j, m in enumerate(s_["launch_ms"])
-             if ((s_["launch_pk"] >> j) & 1) == (1 if kernel == "nw16_kernel" else 0)]
+             if ((s_.get(kbits, 0) >> j) & 1) == (1 if kernel in ("nw16_kernel", "nwp_kernel") else 0)]
     # HBM: the contract's algorithmic figure (2 B/cell), the
     # two-pass kernel's own minimum (nw16_min_bytes_per_cell) and the bytes
     # the PMC counters saw per cell
@@ -407,6 +414,7 @@ def main():
     common = {"traffic": traffic,
               "traffic_over_alg": round(traffic / per_launch, 4) if traffic and per_launch else None,
               "kernel": kernel, "launches": nw_launches,
+              "nw_fallback": sum(s_.get("nw_fallback", 0) for s_ in stats),
               "avg_launch_ms": round(nw_ms / max(nw_launches, 1), 4),
               "kernel_launches": len(pk_ms),
               "kernel_avg_launch_ms": round(sum(pk_ms) / max(len(pk_ms), 1), 4),

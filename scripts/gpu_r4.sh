@@ -62,7 +62,7 @@ run_step() {   # $1 = step, $2 = output suffix
          for grp in "SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_BUSY_CYCLES" \
                     "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE"; do
            i=$((i+1))
-           timeout -s KILL 400 rocprofv3 --pmc $grp --kernel-include-regex 'nw16_kernel|nw_kernel|nwl_kernel|seed_' -T \
+           timeout -s KILL 400 rocprofv3 --pmc $grp --kernel-include-regex 'nw16_kernel|nw_kernel|nwl_kernel|nwp_kernel|seed_' -T \
              -d $O/pmc_${CFG}_${TAG}${X}_p$i -o pmc --output-format csv \
              -- python3 bench.py --config $CFG --steps 1 --warmup 0 --cpu-sample 0 --e2e off \
              > $O/pmc_${CFG}_${TAG}${X}_p$i.json 2> $O/pmc_${CFG}_${TAG}${X}_p$i.err

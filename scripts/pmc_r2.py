@@ -59,6 +59,7 @@ def main():
                    "per pass; FETCH_SIZE/WRITE_SIZE in KiB as reported (HBM bytes = 2 x FETCH_SIZE + WRITE_SIZE, "
                    "MI355X_MICROARCH.md gfx950); SQ cycle counters in quad-cycles", "kernels": res}, f, indent=1)
     nwk = next((k for k in res if k.startswith("nw16_kernel")), None) or next(
+        (k for k in res if k.startswith("nwp_kernel")), None) or next(
         (k for k in res if k.startswith("nwl_kernel")), None) or next(
         (k for k in res if k.startswith("nw_kernel")), None)
     if not nwk:
