@@ -999,8 +999,8 @@ static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, 
     pl->G = sh.G; pl->GPW = sh.GPW; pl->nstr = sh.nstr; pl->xcap = sh.xcap; pl->xstride = sh.xstride;
     pl->steps = sh.steps;
     pl->tb_dw = pl->pk ? nw16_tb_words(sh) : pl->lp ? nwp_tb_words(sh, ymax) : pl->lng ? nwl_tb_words(sh, ymax) : nw_tb_words(sh);
-    pl->ck_dw = pl->two ? nw16_ck_words(sh) : pl->lp ? nwp_ck_words(sh) : pl->lng ? nwl_ck_words(sh) : 0;
-    pl->bnd_dw = pl->lp ? nwp_seam_words(sh) : pl->lng ? nwl_seam_words(sh) : 3ull * pl->xcap;
+    pl->ck_dw = pl->two ? nw16_ck_words(sh) : pl->lp ? nwp_ck_words(sh, ymax) : pl->lng ? nwl_ck_words(sh) : 0;
+    pl->bnd_dw = pl->lp ? nwp_seam_words(sh, ymax) : pl->lng ? nwl_seam_words(sh) : 3ull * pl->xcap;
     pl->lds = (size_t)wpb * (pl->pk ? nw16_wave_lds(pl->GPW, pl->xstride)
                              : pl->lng ? nwl_wave_lds(pl->xstride) : nw_wave_lds(pl->GPW, pl->xstride));
     int per_cu = 0;

@@ -45,10 +45,12 @@
 // neighbours' within +-4 per column, and the sentinels of column 1 (mc[0]
 // never updated, mf = -inf) stay put.
 
-#define NWP_K    NWL_K
-#define NWP_W    NWL_W
+#ifndef NWP_K
+#define NWP_K    10                       // columns per lane
+#endif
+#define NWP_W    (64 * NWP_K)             // columns per strip
 #define NWP_NST  (4 * NWP_K + 7)          // A, B, mcS, u0 per column; I1, I2, outT, outMS, outL; off[2]
-#define NWP_NREC 3                        // traceback dwords per lane per step (TbWords<10>: WM, WU, WX)
+#define NWP_NREC nw16_nrec(NWP_K)         // traceback dwords per lane per step (TbWords<NWP_K>)
 #define NWP_S    1024                     // T spread checked at every block start
 #define NWP_S2   (2 * NWP_S + 4 * 64 + 4) // ... and the spread it allows within the block
 
@@ -61,19 +63,22 @@ __host__ static inline bool nwp_fits(int64_t ig, int64_t eg, uint64_t xcap, uint
     if (!nwl_fits(ig, eg, ymax) || -ig > 1024 || -eg > 16) return false;
     return 2 * NWP_S2 + nwp_rlim(ig, eg, xcap, ymax) + 16 + 100 <= 32767;
 }
-// Launch shape: nwl_kernel's strips, the two records two rows per byte (and
-// at least nwl_kernel's record bytes: a wave that falls back runs nwl_cand in
-// the same LDS)
+// Launch shape: NWP_W-column strips, the two records two rows per byte.  A
+// wave that falls back runs nwl_cand in the same slot and LDS, so every size
+// below is also at least nwl_kernel's (its strips are NWL_W wide).
 __host__ static inline NwShape nwp_shape(uint32_t ymax, uint32_t xcap) {
     NwShape s = nwl_shape(ymax, xcap);
+    s.nstr = std::max(1, (int)((ymax + NWP_W - 1) / NWP_W));
     s.xstride = std::max(s.xstride, ((s.xcap + 1) / 2 + 16 + 15) & ~15);
     return s;
 }
-__host__ static inline uint64_t nwp_ck_words(const NwShape &s) {
-    return std::max<uint64_t>((uint64_t)s.nstr * nwl_ncks(s.steps) * NWP_NST * 64, nwl_ck_words(s));
+__host__ static inline uint64_t nwp_ck_words(const NwShape &s, uint32_t ymax) {
+    return std::max<uint64_t>((uint64_t)s.nstr * nwl_ncks(s.steps) * NWP_NST * 64, nwl_ck_words(nwl_shape(ymax, s.xcap)));
 }
 // seams: six planes per strip (T, mf score, l0 of each half, absolute)
-__host__ static inline uint64_t nwp_seam_words(const NwShape &s) { return (uint64_t)s.nstr * (s.xcap + 1) * 6; }
+__host__ static inline uint64_t nwp_seam_words(const NwShape &s, uint32_t ymax) {
+    return std::max<uint64_t>((uint64_t)s.nstr * (s.xcap + 1) * 6, nwl_seam_words(nwl_shape(ymax, s.xcap)));
+}
 __host__ __device__ static inline uint64_t nwp_band_words() { return (uint64_t)(NWL_BAND + NWL_CK + 64) * 64 * NWP_NREC; }
 // pass 1: each half's last-column records (NWP_K packed cells + the two frame
 // offsets per row); pass 2: the band + a path scratch per half; and whatever
@@ -81,7 +86,7 @@ __host__ __device__ static inline uint64_t nwp_band_words() { return (uint64_t)(
 __host__ static inline uint64_t nwp_tb_words(const NwShape &s, uint32_t ymax) {
     const uint64_t p1 = (uint64_t)2 * s.xcap * (NWP_K + 2) + 64;
     const uint64_t p2 = nwp_band_words() + 2 * ((uint64_t)s.xcap + ymax + 64 + 1);
-    return std::max(std::max(p1, p2), nwl_tb_words(s, ymax));
+    return std::max(std::max(p1, p2), nwl_tb_words(nwl_shape(ymax, s.xcap), ymax));
 }
 
 // 2-bit code of row i of half h (two rows per byte: A bits 0-1 / 4-5, B 2-3 / 6-7)

@@ -92,10 +92,10 @@ static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, cons
                      : nw_shape(ymax, xmax);
     std::vector<uint32_t> tb((pk ? nw16_tb_words(sh) : lp ? nwp_tb_words(sh, ymax) : lng ? nwl_tb_words(sh, ymax)
                               : nw_tb_words(sh)) + 64, 0xABABABABu);
-    std::vector<uint32_t> ck(two ? nw16_ck_words(sh) : lp ? nwp_ck_words(sh) : lng ? nwl_ck_words(sh) : 1, 0xCDCDCDCDu);
+    std::vector<uint32_t> ck(two ? nw16_ck_words(sh) : lp ? nwp_ck_words(sh, ymax) : lng ? nwl_ck_words(sh) : 1, 0xCDCDCDCDu);
     const char *be = getenv("IMSAME_NW_BAND");
     // seam scratch poisoned like fresh device memory: a read before its write shows
-    std::vector<int32_t> bnd((lp ? nwp_seam_words(sh) : lng ? nwl_seam_words(sh) : (size_t)3 * sh.xcap) + 64, 0x70000000);
+    std::vector<int32_t> bnd((lp ? nwp_seam_words(sh, ymax) : lng ? nwl_seam_words(sh) : (size_t)3 * sh.xcap) + 64, 0x70000000);
     std::vector<uint8_t> lds((pk ? nw16_wave_lds(sh.GPW, sh.xstride)
                               : lng ? nwl_wave_lds(sh.xstride) : nw_wave_lds(sh.GPW, sh.xstride)) + 64, 0xA5);
     uint32_t counter = 0;
