@@ -203,11 +203,14 @@ __device__ void nwp_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const 
             return !real || (abs(ta) <= 2 * S && abs(tb_) <= 2 * S && min(ma, mb) >= -GLO && max(ma, mb) <= MHI &&
                              min(la, lb) >= -GLO && max(la, lb) <= MHI);
         };
-        // W = steps [t - 64, t) of the last lane (its frame of that block): lane l row t - 127 + l
-        auto seam_flush = [&](const int t, const int ts) {
+        // W = steps [t - 64, t) of the last lane: lane l row t - 127 + l.  Only
+        // the rows of the block that began at step tb (its frame: the last
+        // lane's, not yet moved); after a partial last block the lanes below
+        // hold rows the previous flush wrote, in the previous frame
+        auto seam_flush = [&](const int t, const int tb) {
             const int oa = wv_readlane(off[0], 63), ob = wv_readlane(off[1], 63);
             const int r = t - 127 + lane;
-            if (r >= 1 && r < xmax && r >= ts - 63) {
+            if (r >= 1 && r < xmax && r >= tb - 63) {
                 seam_wr[r] = pk_score(W0, 0) + oa;          seam_wr[SP + r] = pk_score(W0, 1) + ob;
                 seam_wr[2 * SP + r] = pk_score(W1, 0) + oa; seam_wr[3 * SP + r] = pk_score(W1, 1) + ob;
                 seam_wr[4 * SP + r] = pk_score(W2, 0) + oa; seam_wr[5 * SP + r] = pk_score(W2, 1) + ob;
@@ -389,9 +392,10 @@ __device__ void nwp_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const 
             xs = xsel_row(ts - 1 - lane);             // as the left neighbour would hand it over
             if (seam_in) seam_load(ts);
             const int head_end = 66, tail_beg = xmin - 2;          // fast steps: every lane in rows [2, xmin - 1)
-            int t = ts;
+            int t = ts, tb = ts;                      // tb: the current block's first step
             while (t < t1) {
-                if (seam_out && t > ts) seam_flush(t, ts);
+                if (seam_out && t > ts) seam_flush(t, tb);
+                tb = t;
                 if (CKS && (t - 1) % NWL_CK == 0) save((t - 1) / NWL_CK);
                 bool bad = rebase();
                 if (seam_in) { bad = !seam_take(t) || bad; seam_load(t + 64); }
@@ -420,7 +424,7 @@ __device__ void nwp_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const 
                 }
                 if (t < te) { step(true, true, TB, BEST, t, A, B, I2, I1); ++t; }   // t1 odd: the sweep's end
             }
-            if (seam_out) seam_flush(t, ts);
+            if (seam_out) seam_flush(t, tb);
             return false;
         };
 

@@ -170,6 +170,9 @@ static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, cons
     else if (pk)          run_wave([&](int lane) { nw16_wave<NW16_K, false, false>(P, lds.data(), lane, 0); });
     else if (sh.nstr > 1) run_wave([&](int lane) { nw_wave<true>(P, lds.data(), lane, 0); });
     else             run_wave([&](int lane) { nw_wave<false>(P, lds.data(), lane, 0); });
+    if (const char *dump = getenv("IMSAME_EMU_DUMP_SEAM")) {       // debugging: the seam scratch as left
+        if (FILE *f = fopen(dump, "wb")) { fwrite(bnd.data(), 4, bnd.size(), f); fclose(f); }
+    }
     return 0;
 }
 

@@ -390,6 +390,36 @@ def test_emulated_packed_long_nw(emu, oracle, mode, monkeypatch):
         assert txt == o["text"], k
 
 
+def test_emulated_packed_long_seams_equal_int32(emu, oracle, monkeypatch, tmp_path):
+    """The packed long kernel's seams (absolute T, mf score and l0 of every
+    strip's right edge, written from per-lane frames) equal the int32
+    nwl_kernel's for every row, including the rows of a partial last block
+    (a record of 1100 rows: the last block of each strip has 10 steps) --
+    and the rows equal the oracle's."""
+    rng = np.random.default_rng(1)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    x = acgt[rng.integers(0, 4, 1100)]
+    y = np.concatenate([x[100:], acgt[rng.integers(0, 4, 400)]])
+    X, Y = [x.tobytes()], [y.tobytes()]
+    p = oracle.params(igap=-5, egap=-2, want_paths=1, min_coverage=1e-9, min_identity=1e-9)
+    seams = {}
+    for k, on in (("nwp", "1"), ("nwl", "0")):
+        monkeypatch.setenv("IMSAME_NWP", on)
+        monkeypatch.setenv("IMSAME_EMU_DUMP_SEAM", str(tmp_path / k))
+        rc, res, _, fl = emu.nw_pairs(X, Y, p, paths_cap=100_000)
+        assert rc == 0 and fl == 0
+        o = oracle.nw(X[0], Y[0], igap=-5, egap=-2)
+        for f in ("score", "bx", "by", "length", "identities"):
+            assert int(res[0][f]) == int(o[f]), (k, f)
+        seams[k] = np.fromfile(tmp_path / k, dtype=np.int32)
+    xl, SP = len(x), len(x) + 1
+    for st in range((len(y) + 639) // 640 - 1):
+        for pl in range(3):                   # nwp: planes (T, mf, l0) x halves; nwl: (T, mf, l0)
+            a = seams["nwp"][st * 6 * SP + 2 * pl * SP:][:SP][1:xl]
+            b = seams["nwl"][st * 3 * SP + pl * SP:][:SP][1:xl]
+            assert np.array_equal(a, b), (st, pl, np.nonzero(a != b)[0][:8] + 1)
+
+
 def _strip_mix_pairs():
     """163- and 400-column reads in ONE launch: the launch takes the
     multi-strip kernel (ymax > 320) and the 163-column reads have one strip."""
