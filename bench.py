@@ -569,9 +569,9 @@ def run_e2e(ref, rst, q, qs, a):
         if p.returncode != 0 or not m:
             return {"error": f"rc {p.returncode}: {p.stderr[-300:].decode(errors='replace')}"}
         ph = json.loads(m.group(1))
-        td = re.search(rb"\[imsame\] teardown (\{.*\})", p.stderr)          # device close after the phases line
-        if td:
-            ph.update(json.loads(td.group(1)))
+        tm = re.search(rb"\[imsame\] teardown (\{.*\})", p.stderr)          # device close after the phases line
+        if tm:
+            ph.update(json.loads(tm.group(1)))
         ph = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in ph.items()}
         ph.update({"process_wall_s": round(wall, 3), "output": "file" if out == outf else "/dev/null (disk full)",
                    "output_fs": mount_fs(td), "cli_args": extra,
