@@ -25,21 +25,25 @@
 //
 // Range.  A 10 kbp x 12 kbp matrix holds scores up to ~4e4: no one int16
 // frame holds them.  Each LANE keeps each half relative to its own frame
-// off[h] (int32), moved every 64-step block to the lane's current T (B[0]), so
-// its values stay near 0; the left neighbour's row state (T, mf, l0) is
-// shifted into this lane's frame as it arrives (dl = off(left) - off(own), one
-// v_pk_add per value per step), and seams hold absolute int32.  With every T
-// a lane or its neighbour holds inside +-NWP_S of its frame at the block start
-// (so +-NWP_S2 during the block), the recurrence bounds the rest:
-//   gap terms (u0, l0) >= T - |ig| - |eg|*(L + 64), L = max(xcap, ycap): a gap
-//     term is a maximum (>= some T of the frame) less its drift;
-//   maxima (mcS, mfS) <= T + 9 + |ig| + |eg|*(L + 64): T >= up + s and left + s;
-// so every compared difference fits int16 when 2*NWP_S2 + |ig| + |eg|*(L+64)
-// + 16 does (nwp_fits: records up to ~14 kbp at the default gaps).  Each block
-// start checks the T spread (own T, neighbour frames, seam rows) and, as a
-// tripwire for the bounds above, the gap terms and maxima; a wave that finds
-// any value outside abandons its pair and runs both candidates through
-// nwl_cand (int32) instead -- same results, counted in NwLaunch::fbk.
+// off[h] (int32), moved every 64-step block to the lane's current T (B[0]);
+// the left neighbour's row state (T, mf, l0) is shifted into this lane's frame
+// as it arrives (dl = off(left) - off(own), one v_pk_add per value per step),
+// and seams hold absolute int32.  The reference's recurrence is not smooth --
+// an up or left term decays from the FIRST maximum of its column or row, so
+// neighbouring cells can differ by thousands -- so nothing is assumed about
+// the spread: every block start reduces the wave's absolute extremes per half
+// (T, gap terms u0 / l0, maxima mcS / mf, and the seam rows of the block) and
+// bounds every compared difference of the block by them (every frame is one
+// of the wave's T; within a block a T moves <= 4 per step and a gap term falls
+// <= 64 |eg|):
+//     maxima - T  <= (Mmax - Tmin) + (Tmax - Tmin) + NWP_G + 7
+//     T - gap     <= (Tmax - Gmin) + (Tmax - Tmin) + NWP_G + 64|eg| + 20
+// A wave whose bound reaches 2^15 abandons its pair before that block and runs
+// both candidates through nwl_cand (int32) instead -- same results, counted
+// in NwLaunch::fbk.  The traceback signs compare against the maxima the cell
+// computes anyway (d0 - max(d0, lu), l0 - lu), which the second bound covers.
+// nwp_fits only keeps launches that are likely to pass (records up to ~14 kbp
+// at the default gaps: the drift |eg| (L + 64) plus a budget for the spread).
 //
 // Column 0 (lane 0 of strip 0) keeps frame 0: its T is s(x, y) and its
 // neighbours' within +-4 per column, and the sentinels of column 1 (mc[0]
@@ -51,14 +55,15 @@
 #define NWP_W    (64 * NWP_K)             // columns per strip
 #define NWP_NST  (4 * NWP_K + 7)          // A, B, mcS, u0 per column; I1, I2, outT, outMS, outL; off[2]
 #define NWP_NREC nw16_nrec(NWP_K)         // traceback dwords per lane per step (TbWords<NWP_K>)
-#define NWP_S    1024                     // T spread checked at every block start
-#define NWP_S2   (2 * NWP_S + 4 * 64 + 4) // ... and the spread it allows within the block
+#define NWP_G    (4 * 64 + 64)            // how far a T moves within a 64-step block (+4 per step; column 0: +-44)
+#define NWP_S2   2308                     // nwp_fits: the T spread it budgets
 
 // |ig| + |eg| (L + 64): the drift bound of the launch (NwLaunch::rlim)
 __host__ static inline int64_t nwp_rlim(int64_t ig, int64_t eg, uint64_t xcap, uint64_t ymax) {
     return -ig + -eg * (int64_t)(std::max<uint64_t>(xcap, ymax) + 64);
 }
-// does the launch fit the packed long kernel?  (nwl_fits, and the range above)
+// is the launch likely to fit the packed long kernel?  (nwl_fits, and the range
+// above with a budget of NWP_S2 for the T spread)
 __host__ static inline bool nwp_fits(int64_t ig, int64_t eg, uint64_t xcap, uint64_t ymax) {
     if (!nwl_fits(ig, eg, ymax) || -ig > 1024 || -eg > 16) return false;
     return 2 * NWP_S2 + nwp_rlim(ig, eg, xcap, ymax) + 16 + 100 <= 32767;
@@ -112,8 +117,8 @@ __device__ void nwp_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const 
     const int ig = P.igap, eg = P.egap;
     const uint32_t H = NW16_H, NBIG = pk1(-NW16_BIG) ^ NW16_H, PBIG = pk1(NW16_BIG) ^ NW16_H;
     const uint32_t EGN = pk1(-eg), IGEN = pk1(-(ig + eg));      // gap magnitudes (biased subtracts)
-    const int S = P.nwp_s > 0 ? min(P.nwp_s, NWP_S) : NWP_S;    // tests: tiny spreads force the fallback
-    const int GLO = NWP_S2 + P.rlim, MHI = NWP_S2 + 9 + P.rlim;  // gap terms >= -GLO, maxima <= MHI
+    const int64_t LIM = P.nwp_s > 0 ? P.nwp_s : 32767 - 16;     // tests: a tiny limit forces the fallback
+    const int DEC = 64 * -eg + 16;                                // a gap term's fall within a block
     uint8_t *X2 = wsm;
     int *red = (int *)(wsm + P.xstride);                          // 64 lanes x 8 ints, then the walks
     uint32_t *tbw = P.tb + (uint64_t)slot * P.tb_wave_dw;
@@ -194,14 +199,10 @@ __device__ void nwp_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const 
 #pragma unroll
             for (int p = 0; p < 6; ++p) N[p] = seam_rd[p * SP + r];
         };
-        // N -> R in lane 0's (new) frame; false if a real row falls outside the bounds
-        auto seam_take = [&](const int t) {
+        // N -> R in lane 0's (new) frame (rebase() counted the rows in the wave's extremes)
+        auto seam_take = [&]() {
             const int oa = wv_readlane(off[0], 0), ob = wv_readlane(off[1], 0);
-            const int ta = N[0] - oa, tb_ = N[1] - ob, ma = N[2] - oa, mb = N[3] - ob, la = N[4] - oa, lb = N[5] - ob;
-            R0 = pk2(ta, tb_) ^ H; R1 = pk2(ma, mb) ^ H; R2 = pk2(la, lb) ^ H;
-            const bool real = t + lane < xmax;
-            return !real || (abs(ta) <= 2 * S && abs(tb_) <= 2 * S && min(ma, mb) >= -GLO && max(ma, mb) <= MHI &&
-                             min(la, lb) >= -GLO && max(la, lb) <= MHI);
+            R0 = pk2(N[0] - oa, N[1] - ob) ^ H; R1 = pk2(N[2] - oa, N[3] - ob) ^ H; R2 = pk2(N[4] - oa, N[5] - ob) ^ H;
         };
         // W = steps [t - 64, t) of the last lane: lane l row t - 127 + l.  Only
         // the rows of the block that began at step tb (its frame: the last
@@ -359,7 +360,7 @@ __device__ void nwp_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const 
         };
         // block start: move the frame to the lane's T (B[0], its last row) and
         // check the ranges; true if any value is outside them
-        auto rebase = [&]() {
+        auto rebase = [&](const int t) {
             const uint32_t D = leadc0 ? 0u : (B[0] ^ H);
             off[0] += (int)(int16_t)(D & 0xFFFFu); off[1] += (int)(int16_t)(D >> 16);
             uint32_t hi = 0, lo = 0xFFFFFFFFu, glo = 0xFFFFFFFFu, mhi = 0;
@@ -379,11 +380,39 @@ __device__ void nwp_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const 
             hi = pk_maxu(hi, pk_maxu(i12hi, outT)); lo = pk_minu(lo, pk_minu(i12lo, outT));
             glo = pk_minu(glo, outL); mhi = pk_maxu(mhi, outMS);
             const int la = wv_shr1(off[0]), lb = wv_shr1(off[1]);
-            const int da = lane ? la - off[0] : 0, db = lane ? lb - off[1] : 0;
-            dl = pk2(da, db);
-            return abs(da) > S || abs(db) > S || max(pk_score(hi, 0), pk_score(hi, 1)) > S ||
-                   min(pk_score(lo, 0), pk_score(lo, 1)) < -S || min(pk_score(glo, 0), pk_score(glo, 1)) < -GLO ||
-                   max(pk_score(mhi, 0), pk_score(mhi, 1)) > MHI;
+            dl = lane ? pk2(la - off[0], lb - off[1]) : 0u;
+            // the wave's extremes, absolute, per half: T, gap terms, maxima (and
+            // the seam rows lane 0 takes in this block)
+            int ex[2][4];                              // T max, -T min, -gap min, max-term max
+            for (int h = 0; h < 2; ++h) {
+                ex[h][0] = pk_score(hi, h) + off[h]; ex[h][1] = -(pk_score(lo, h) + off[h]);
+                ex[h][2] = -(pk_score(glo, h) + off[h]); ex[h][3] = pk_score(mhi, h) + off[h];
+                if (seam_in && t + lane < xmax) {
+                    ex[h][0] = max(ex[h][0], N[h]); ex[h][1] = max(ex[h][1], -N[h]);
+                    ex[h][2] = max(ex[h][2], -N[4 + h]); ex[h][3] = max(ex[h][3], N[2 + h]);
+                }
+            }
+            for (int o = 32; o > 0; o >>= 1)
+                for (int h = 0; h < 2; ++h)
+                    for (int k = 0; k < 4; ++k) ex[h][k] = max(ex[h][k], wv_shfl_xor(ex[h][k], o));
+            // every lane's frame is one of the wave's T, so within a block (T
+            // moves <= G per step and crosses lanes exactly; gap terms fall
+            // <= DEC) the compared differences are bounded by
+            //   maxima - T  <= (Mmax - Tmin) + span + G + 7
+            //   T - gap     <= (Tmax - Gmin) + span + G + DEC + 4
+            // (span = Tmax - Tmin); both must stay below 2^15
+            bool bad = false;
+            for (int h = 0; h < 2; ++h) {
+                const int64_t span = (int64_t)ex[h][0] + ex[h][1];
+                bad = bad || (int64_t)ex[h][3] + ex[h][1] + span + NWP_G + 7 > LIM ||
+                      (int64_t)ex[h][0] + ex[h][2] + span + NWP_G + DEC + 4 > LIM;
+            }
+#ifdef IMSAME_WAVE_EMU
+            if (bad && lane == 0 && getenv("IMSAME_NWP_DEBUG"))
+                fprintf(stderr, "[nwp] st %d t %d: T [%d, %d] gap >= %d max <= %d | B: T [%d, %d] gap >= %d max <= %d\n",
+                        st, t, -ex[0][1], ex[0][0], -ex[0][2], ex[0][3], -ex[1][1], ex[1][0], -ex[1][2], ex[1][3]);
+#endif
+            return bad;
         };
         // run steps [ts, t1) from the state before step ts (ts = 1 mod NWL_CK)
         // in blocks of 64 steps; true if a block start found a value out of range
@@ -397,8 +426,8 @@ __device__ void nwp_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const 
                 if (seam_out && t > ts) seam_flush(t, tb);
                 tb = t;
                 if (CKS && (t - 1) % NWL_CK == 0) save((t - 1) / NWL_CK);
-                bool bad = rebase();
-                if (seam_in) { bad = !seam_take(t) || bad; seam_load(t + 64); }
+                bool bad = rebase(t);
+                if (seam_in) { seam_take(); seam_load(t + 64); }
                 xq = xsel_row(t + lane);
                 if (wv_any(bad)) return true;
                 const int te = min(t + 64, t1);
