@@ -35,6 +35,10 @@ run_step() {   # $1 = step, $2 = output suffix
            ok_or_stop $? benchq$X ;;
     e2e) timeout -k 10 900 python -u bench.py --cpu-sample 0 --steps 1 --e2e on > $O/bench_e2e_${TAG}$X.json \
            2> $O/bench_e2e_${TAG}$X.err; ok_or_stop $? e2e$X ;;
+    # e2e with CLI flags: e2ef:-batch_reads+250000 (+ stands for a space)
+    e2ef:*) F=${s#e2ef:}; F=${F//+/ }; FS=$(echo "$F" | tr -c 'a-z0-9\n' '_')
+           IMSAME_E2E_ARGS="$F" timeout -k 10 900 python -u bench.py --cpu-sample 0 --steps 1 --e2e on \
+           > $O/bench_e2e${FS}_${TAG}$X.json 2> $O/bench_e2e${FS}_${TAG}$X.err; ok_or_stop $? "e2e$FS$X" ;;
     c3) timeout -k 10 900 python -u bench.py --config c3 --steps 2 $BQ > $O/bench_c3_${TAG}$X.json \
            2> $O/bench_c3_${TAG}$X.err; ok_or_stop $? c3$X ;;
     c5w) timeout -k 10 900 python -u bench.py --config c5w --steps 1 --warmup 0 > $O/bench_c5w_${TAG}$X.json \
