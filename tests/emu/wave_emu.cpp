@@ -1,28 +1,66 @@
 // wave_emu.cpp -- TEST INFRASTRUCTURE: runs the device kernel source
-// (imsame_amd/csrc/{nw,seed}_kernel.hip) on the CPU.  Each wave is 64 host
-// threads; DPP / ballot / shuffle are lock-step exchanges (wave_ops.h,
-// IMSAME_WAVE_EMU).  The round orchestration below mirrors
-// imsame_dev.hip:imsame_dev_align with host memory in place of HBM.
-// Built by tests/emu/Makefile into tests/emu/build/libwave_emu.so.
+// (imsame_amd/csrc/{nw,seed}_kernel.hip) on the CPU.  Each wave is 64 lanes
+// on ONE host thread as user-space fibers (ucontext): a lane runs until its
+// next cross-lane op, which hands over to the next lane, so DPP / ballot /
+// shuffle are lock-step exchanges (wave_ops.h, IMSAME_WAVE_EMU) at the cost
+// of 64 context switches.  Launches run several waves on host threads, each
+// with its own arena slot, as the device does.  Sanitizer builds
+// (scripts/sanitize.sh) use one host thread per lane and a barrier instead.
+// The round orchestration below mirrors imsame_dev.hip:imsame_dev_align with
+// host memory in place of HBM.  Built by tests/emu/Makefile into
+// tests/emu/build/libwave_emu.so.
 #define IMSAME_WAVE_EMU 1
-#include <barrier>
+#include <algorithm>
 #include <functional>
+#include <memory>
 #include <thread>
 #include <vector>
 #include <stdio.h>
 #include <string.h>
 #include <math.h>
+#if defined(__SANITIZE_ADDRESS__) || defined(__SANITIZE_THREAD__)
+#define EMU_THREADS 1
+#include <barrier>
+#else
+#include <ucontext.h>
+#endif
 #include "../../imsame_amd/csrc/wave_ops.h"
 
 namespace wvemu {
+thread_local Wave *t_wave;
+thread_local int t_lane;
+thread_local uint64_t *t_xch;
+#ifdef EMU_THREADS
 struct Wave {
     std::barrier<> bar{64};
     uint64_t xch[64];
 };
-thread_local Wave *t_wave;
-thread_local int t_lane;
-thread_local uint64_t *t_xch;
 void sync() { t_wave->bar.arrive_and_wait(); }
+#else
+struct Wave {
+    ucontext_t ctx[64], caller;
+    uint64_t xch[64];
+    const std::function<void(int)> *f;
+    std::unique_ptr<char[]> stacks;
+};
+constexpr size_t STACK = 1u << 20;
+// every lane has arrived once the last one hands over to lane 0
+void sync() {
+    Wave *w = t_wave;
+    const int me = t_lane, nx = (me + 1) & 63;
+    t_lane = nx;
+    swapcontext(&w->ctx[me], &w->ctx[nx]);
+}
+// a lane's body; when it ends, the next lane (waiting in its last sync) ends
+// too, and the last one returns to the caller
+static void fiber_entry() {
+    Wave *w = t_wave;
+    const int l = t_lane;
+    (*w->f)(l);
+    if (l < 63) { t_lane = l + 1; setcontext(&w->ctx[l + 1]); }
+    setcontext(&w->caller);
+}
+#endif
 }  // namespace wvemu
 
 #include "../../include/imsame_dev.h"
@@ -34,6 +72,7 @@ void sync() { t_wave->bar.arrive_and_wait(); }
 #include "../../imsame_amd/csrc/seed_kernel.hip"
 
 static void run_wave(const std::function<void(int)> &f) {
+#ifdef EMU_THREADS
     wvemu::Wave w;
     std::vector<std::thread> th;
     th.reserve(64);
@@ -43,6 +82,35 @@ static void run_wave(const std::function<void(int)> &f) {
             f(l);
         });
     for (auto &t : th) t.join();
+#else
+    auto w = std::make_unique<wvemu::Wave>();
+    w->f = &f;
+    w->stacks.reset(new char[64 * wvemu::STACK]);
+    for (int l = 0; l < 64; ++l) {
+        getcontext(&w->ctx[l]);
+        w->ctx[l].uc_stack.ss_sp = w->stacks.get() + (size_t)l * wvemu::STACK;
+        w->ctx[l].uc_stack.ss_size = wvemu::STACK;
+        w->ctx[l].uc_link = nullptr;
+        makecontext(&w->ctx[l], wvemu::fiber_entry, 0);
+    }
+    wvemu::t_wave = w.get(); wvemu::t_lane = 0; wvemu::t_xch = w->xch;
+    swapcontext(&w->caller, &w->ctx[0]);
+    wvemu::t_wave = nullptr;
+#endif
+}
+
+// waves w = 0 .. nw-1 of one launch, each on a host thread of its own: f(lane, w)
+static void run_waves(int nw, const std::function<void(int, int)> &f) {
+    std::vector<std::thread> th;
+    for (int w = 1; w < nw; ++w) th.emplace_back([&f, w] { run_wave([&f, w](int l) { f(l, w); }); });
+    run_wave([&f](int l) { f(l, 0); });
+    for (auto &t : th) t.join();
+}
+// host threads the launches use (each wave holds a 64 MB stack block)
+static int emu_threads() {
+    const char *e = getenv("IMSAME_EMU_THREADS");
+    const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
+    return std::max(1, e ? atoi(e) : std::min(hw, 8));
 }
 
 // waves whose nw16 traceback band missed a path (NwLaunch::redo), since the last emu_redo_count()
@@ -90,14 +158,21 @@ static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, cons
                 : (pk && nw16_k19_ok(yuni, ymax, xmax, p)) ? NW16_K19 : NW16_K;
     const NwShape sh = pk ? nw16_shape(ymax, xmax, K) : lp ? nwp_shape(ymax, xmax) : lng ? nwl_shape(ymax, xmax)
                      : nw_shape(ymax, xmax);
-    std::vector<uint32_t> tb((pk ? nw16_tb_words(sh) : lp ? nwp_tb_words(sh, ymax) : lng ? nwl_tb_words(sh, ymax)
-                              : nw_tb_words(sh)) + 64, 0xABABABABu);
-    std::vector<uint32_t> ck(two ? nw16_ck_words(sh) : lp ? nwp_ck_words(sh, ymax) : lng ? nwl_ck_words(sh) : 1, 0xCDCDCDCDu);
+    // waves of the launch (one arena slot each), as many as it has tasks
+    const uint32_t cpw = (pk || lp) ? 2u * (uint32_t)sh.GPW : (uint32_t)sh.GPW;
+    const int nwv = (int)std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)emu_threads(), (n + cpw - 1) / cpw));
+    const size_t tb_slot = (pk ? nw16_tb_words(sh) : lp ? nwp_tb_words(sh, ymax) : lng ? nwl_tb_words(sh, ymax)
+                            : nw_tb_words(sh)) + 64;
+    const size_t ck_slot = two ? nw16_ck_words(sh) : lp ? nwp_ck_words(sh, ymax) : lng ? nwl_ck_words(sh) : 1;
+    std::vector<uint32_t> tb(tb_slot * nwv, 0xABABABABu);
+    std::vector<uint32_t> ck(ck_slot * nwv, 0xCDCDCDCDu);
     const char *be = getenv("IMSAME_NW_BAND");
     // seam scratch poisoned like fresh device memory: a read before its write shows
-    std::vector<int32_t> bnd((lp ? nwp_seam_words(sh, ymax) : lng ? nwl_seam_words(sh) : (size_t)3 * sh.xcap) + 64, 0x70000000);
-    std::vector<uint8_t> lds((pk ? nw16_wave_lds(sh.GPW, sh.xstride)
-                              : lng ? nwl_wave_lds(sh.xstride) : nw_wave_lds(sh.GPW, sh.xstride)) + 64, 0xA5);
+    const size_t bnd_slot = (lp ? nwp_seam_words(sh, ymax) : lng ? nwl_seam_words(sh) : (size_t)3 * sh.xcap) + 64;
+    std::vector<int32_t> bnd(bnd_slot * nwv, 0x70000000);
+    const size_t lds_slot = (pk ? nw16_wave_lds(sh.GPW, sh.xstride)
+                              : lng ? nwl_wave_lds(sh.xstride) : nw_wave_lds(sh.GPW, sh.xstride)) + 64;
+    std::vector<uint8_t> lds(lds_slot * nwv, 0xA5);
     uint32_t counter = 0;
     NwLaunch P;
     memset(&P, 0, sizeof P);
@@ -105,14 +180,14 @@ static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, cons
     P.cand_read = cread; P.cand_sid = csid; P.n_cand = n;
     P.igap = (int32_t)p->igap; P.egap = (int32_t)p->egap;
     P.G = sh.G; P.GPW = sh.GPW; P.xcap = sh.xcap; P.xstride = sh.xstride; P.steps = sh.steps;
-    P.tb = tb.data(); P.tb_wave_dw = tb.size();
-    P.bnd = bnd.data(); P.bnd_wave = bnd.size();
+    P.tb = tb.data(); P.tb_wave_dw = tb_slot;
+    P.bnd = bnd.data(); P.bnd_wave = bnd_slot;
     P.minlen = ml.data(); P.n_minlen = ymax + 1;
     P.minident = mi.data(); P.n_minident = xmax + ymax + 2;
     P.counter = &counter; P.out = out;
     P.paths = paths; P.paths_cap = pcap; P.paths_used = pused; P.want_paths = p->want_paths;
     P.flags = flags;
-    P.ck = ck.data(); P.ck_wave_dw = ck.size();
+    P.ck = ck.data(); P.ck_wave_dw = ck_slot;
     P.band_w = be ? std::max(0, atoi(be)) : 200;        // imsame_dev.hip:nw16_band_rows
     if (lng) {                                            // imsame_dev.hip:plan_nw
         const char *nb = getenv("IMSAME_NWL_BAND");
@@ -150,26 +225,26 @@ static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, cons
     for (uint32_t k = 0; k < n; ++k) ymult = ymult && (qs[cread[k] + 1] - qs[cread[k]]) % NW16_K == 0;
     if (lp) {
         ++g_nwp;
-        run_wave([&](int lane) { nwp_wave(P, lds.data(), lane, 0); });
+        run_waves(nwv, [&](int lane, int w) { nwp_wave(P, lds.data() + w * lds_slot, lane, (uint32_t)w); });
     }
-    else if (lng)         run_wave([&](int lane) { nwl_wave(P, lds.data(), lane, 0); });
+    else if (lng)         run_waves(nwv, [&](int lane, int w) { nwl_wave(P, lds.data() + w * lds_slot, lane, (uint32_t)w); });
     else if (pk && K == NW16_K19) {
         ++g_k19;
-        if (two) run_wave([&](int lane) { nw16_wave<NW16_K19, true, true, NW16_K19_OFF>(P, lds.data(), lane, 0); });
-        else     run_wave([&](int lane) { nw16_wave<NW16_K19, true, false, NW16_K19_OFF>(P, lds.data(), lane, 0); });
+        if (two) run_waves(nwv, [&](int lane, int w) { nw16_wave<NW16_K19, true, true, NW16_K19_OFF>(P, lds.data() + w * lds_slot, lane, (uint32_t)w); });
+        else     run_waves(nwv, [&](int lane, int w) { nw16_wave<NW16_K19, true, false, NW16_K19_OFF>(P, lds.data() + w * lds_slot, lane, (uint32_t)w); });
     }
     else if (pk && K == NW16_K5) {
-        if (two && ymult)     run_wave([&](int lane) { nw16_wave<NW16_K5, true, true>(P, lds.data(), lane, 0); });
-        else if (two)         run_wave([&](int lane) { nw16_wave<NW16_K5, false, true>(P, lds.data(), lane, 0); });
-        else if (pk && ymult) run_wave([&](int lane) { nw16_wave<NW16_K5, true, false>(P, lds.data(), lane, 0); });
-        else if (pk)          run_wave([&](int lane) { nw16_wave<NW16_K5, false, false>(P, lds.data(), lane, 0); });
+        if (two && ymult)     run_waves(nwv, [&](int lane, int w) { nw16_wave<NW16_K5, true, true>(P, lds.data() + w * lds_slot, lane, (uint32_t)w); });
+        else if (two)         run_waves(nwv, [&](int lane, int w) { nw16_wave<NW16_K5, false, true>(P, lds.data() + w * lds_slot, lane, (uint32_t)w); });
+        else if (pk && ymult) run_waves(nwv, [&](int lane, int w) { nw16_wave<NW16_K5, true, false>(P, lds.data() + w * lds_slot, lane, (uint32_t)w); });
+        else if (pk)          run_waves(nwv, [&](int lane, int w) { nw16_wave<NW16_K5, false, false>(P, lds.data() + w * lds_slot, lane, (uint32_t)w); });
     }
-    else if (two && ymult) run_wave([&](int lane) { nw16_wave<NW16_K, true, true>(P, lds.data(), lane, 0); });
-    else if (two)         run_wave([&](int lane) { nw16_wave<NW16_K, false, true>(P, lds.data(), lane, 0); });
-    else if (pk && ymult) run_wave([&](int lane) { nw16_wave<NW16_K, true, false>(P, lds.data(), lane, 0); });
-    else if (pk)          run_wave([&](int lane) { nw16_wave<NW16_K, false, false>(P, lds.data(), lane, 0); });
-    else if (sh.nstr > 1) run_wave([&](int lane) { nw_wave<true>(P, lds.data(), lane, 0); });
-    else             run_wave([&](int lane) { nw_wave<false>(P, lds.data(), lane, 0); });
+    else if (two && ymult) run_waves(nwv, [&](int lane, int w) { nw16_wave<NW16_K, true, true>(P, lds.data() + w * lds_slot, lane, (uint32_t)w); });
+    else if (two)         run_waves(nwv, [&](int lane, int w) { nw16_wave<NW16_K, false, true>(P, lds.data() + w * lds_slot, lane, (uint32_t)w); });
+    else if (pk && ymult) run_waves(nwv, [&](int lane, int w) { nw16_wave<NW16_K, true, false>(P, lds.data() + w * lds_slot, lane, (uint32_t)w); });
+    else if (pk)          run_waves(nwv, [&](int lane, int w) { nw16_wave<NW16_K, false, false>(P, lds.data() + w * lds_slot, lane, (uint32_t)w); });
+    else if (sh.nstr > 1) run_waves(nwv, [&](int lane, int w) { nw_wave<true>(P, lds.data() + w * lds_slot, lane, (uint32_t)w); });
+    else             run_waves(nwv, [&](int lane, int w) { nw_wave<false>(P, lds.data() + w * lds_slot, lane, (uint32_t)w); });
     if (const char *dump = getenv("IMSAME_EMU_DUMP_SEAM")) {       // debugging: the seam scratch as left
         if (FILE *f = fopen(dump, "wb")) { fwrite(bnd.data(), 4, bnd.size(), f); fclose(f); }
     }
@@ -340,18 +415,30 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
             const int L = l_env ? atoi(l_env) : seed_lanes(na);
             if (L <= 1) {
                 for (uint32_t i = 0; i < na; ++i) { uint64_t h = 0; seed_one(SL, i, h); nhits += h; }
-            } else {                   // seed_group_kernel: one 64-lane wave at a time
-                std::vector<uint2> lds(64 * SPEC_BIG);
+            } else {                   // seed_group_kernel: 64-lane waves, several host threads
+                const uint64_t nwaves = ((uint64_t)na * L + 63) / 64;
+                const int nt = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)emu_threads(), nwaves));
+                std::vector<uint2> lds((size_t)nt * 64 * SPEC_BIG);
                 std::atomic<unsigned long long> wh{0};
-                for (uint64_t w0 = 0; w0 < (uint64_t)na * L; w0 += 64)
-                    run_wave([&](int lane) {
-                        uint64_t h = 0;
-                        const uint32_t gidx = (uint32_t)((w0 + lane) / L);
-                        if (L == 64) seed_group<64, SPEC_BIG>(SL, gidx, lane, lane, lds.data() + lane * SPEC_BIG, h);
-                        else if (L == 16) seed_group<16>(SL, gidx, lane % 16, lane, lds.data() + lane * SPEC_MAX, h);
-                        else         seed_group<4>(SL, gidx, lane % 4, lane, lds.data() + lane * SPEC_MAX, h);
-                        wh += h;
-                    });
+                std::atomic<uint64_t> next_wave{0};
+                std::vector<std::thread> th;
+                auto worker = [&](int t) {
+                    for (uint64_t wv; (wv = next_wave++) < nwaves;) {
+                        const uint64_t w0 = wv * 64;
+                        uint2 *ld = lds.data() + (size_t)t * 64 * SPEC_BIG;
+                        run_wave([&](int lane) {
+                            uint64_t h = 0;
+                            const uint32_t gidx = (uint32_t)((w0 + lane) / L);
+                            if (L == 64) seed_group<64, SPEC_BIG>(SL, gidx, lane, lane, ld + lane * SPEC_BIG, h);
+                            else if (L == 16) seed_group<16>(SL, gidx, lane % 16, lane, ld + lane * SPEC_MAX, h);
+                            else         seed_group<4>(SL, gidx, lane % 4, lane, ld + lane * SPEC_MAX, h);
+                            wh += h;
+                        });
+                    }
+                };
+                for (int t = 1; t < nt; ++t) th.emplace_back(worker, t);
+                worker(0);
+                for (auto &x : th) x.join();
                 nhits += wh;
             }
         };
