@@ -227,6 +227,16 @@ int main(int argc, char **argv) {
             ", \"wall_s\": %.4f}\n",
             G, pr.batches, oj.secs, t_parse_db, t_index, t_parse_q, t_upload, pr.t_align, pr.t_render, pr.t_write, pr.t_tail,
             pr.bytes_out, acc, now_s() - t_wall);
+    /* IMSAME_FAST_EXIT=1: leave the device contexts and the heap to process
+     * exit (the output is closed and stdout flushed; the kernel driver releases
+     * the GPU memory), skipping hipFree of the arenas and the runtime's exit
+     * handlers */
+    const char *fe = getenv("IMSAME_FAST_EXIT");
+    if (fe && atoi(fe)) {
+        fprintf(stderr, "[imsame] teardown {\"close_s\": 0, \"fast_exit\": 1}\n");
+        fflush(stderr);
+        _exit(0);
+    }
     const double t_close = now_s();
     host_free_seqs(&db);
     host_free_seqs(&q);

@@ -501,11 +501,15 @@ static int lane_add(imsame_ctx *c) {
 }
 
 extern "C" int imsame_dev_open(int device, imsame_ctx **out) {
+    const bool dbg = getenv("IMSAME_DEBUG_OPEN") != nullptr;   // diagnostics: where the open's time goes
+    const double t0 = dbg ? now_ms() : 0;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) return IMSAME_E_HIP;
+    const double t1 = dbg ? now_ms() : 0;
     imsame_ctx *c = nullptr;
     int rc = ctx_create(device, &c);
     if (rc) return rc;
+    const double t2 = dbg ? now_ms() : 0;
     // Stream creation order fixes the hardware queues: the runtime gives each
     // new stream a queue of its own until GPU_MAX_HW_QUEUES are in use, then
     // shares the least used one.  So the compute streams of this context and
@@ -524,6 +528,9 @@ extern "C" int imsame_dev_open(int device, imsame_ctx **out) {
             rc = IMSAME_E_HIP;
     }
     if (rc) { imsame_dev_close(c); return rc; }
+    if (dbg)
+        fprintf(stderr, "[imsame] open_ms {\"runtime\": %.2f, \"context\": %.2f, \"lanes_streams\": %.2f}\n", t1 - t0,
+                t2 - t1, now_ms() - t2);
     *out = c;
     return IMSAME_OK;
 }
