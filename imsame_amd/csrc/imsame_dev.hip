@@ -1752,6 +1752,7 @@ static double union_ms(std::vector<std::pair<float, float>> v) {
 // Reads per lane below which a call is not split (a lane must fill the chip)
 #define LANE_MIN 32768
 #define LANE_READS 40000
+#define LANES_DEF 3
 
 // Hand lane l's finished reads [a, b) to an imsame_dev_align_parts callback,
 // with its paths copied to the host (path_off of those rows index them).
@@ -1819,14 +1820,16 @@ static int align_impl(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint6
     // LANE_READS reads for its first NW launch to fill the chip's wave slots
     // on its own (~0.9 candidates per read, 8 per wave: 40k reads -> 4.5k
     // waves against 4 per SIMD x 1024 SIMDs), and a hardware queue of its own
-    // (lanes_for_queues).  C2 with 8 queues: 1M reads -> 4 lanes (1-2 % faster
-    // than 8, profiles/r3q16/, r3ln/), its 1/8 shard (125k) -> 3 (1-3 % faster
-    // than 2, r2w_*).  IMSAME_LANES overrides (tests, A/B runs).
+    // (lanes_for_queues), and at most LANES_DEF: with the 19-column NW form
+    // and round 1b, 3 lanes are as fast as 4 on 1M reads (108.08 vs 108.05
+    // ms) and on the 1/8 shard, faster on the 1/2 shard (58.0 vs 58.4 ms) and
+    // on the 1/4 shard (31.7 vs 34.4-34.7 ms), and 8 lanes are slower
+    // (profiles/r4i/, r4j/).  IMSAME_LANES overrides (tests, A/B runs).
     const char *le = getenv("IMSAME_LANES");
     const char *lre = getenv("IMSAME_LANE_READS");
     const uint64_t lane_reads = std::max<uint64_t>(1, lre ? strtoull(lre, nullptr, 10) : LANE_READS);
     int nl = le ? std::max(1, std::min(LANES_MAX, atoi(le)))
-                : (int)std::max<uint64_t>(1, std::min<uint64_t>(lanes_for_queues(), n / lane_reads));
+                : (int)std::max<uint64_t>(1, std::min<uint64_t>(std::min(lanes_for_queues(), LANES_DEF), n / lane_reads));
     const char *lme = getenv("IMSAME_LANE_MIN");
     const uint64_t lane_min = lme ? strtoull(lme, nullptr, 10) : LANE_MIN;
     while (nl > 1 && n < (uint64_t)nl * lane_min) --nl;

@@ -383,7 +383,7 @@ def test_headline_mode_parity():
     assert p.returncode == 0, p.stderr[-3000:].decode(errors="replace")
     d = json.loads(p.stdout.decode().strip().splitlines()[-1])
     print(d)
-    assert d["lanes"] == 4, d                  # 8 queues: 4 lanes of two streams each
+    assert d["lanes"] == 3, d                  # 8 queues hold 4 lanes of two streams; LANES_DEF = 3
     assert d["reads_compared"] >= 4500 and d["identical"] == d["reads_compared"], d
     assert d["accepted"] > 850_000
 
