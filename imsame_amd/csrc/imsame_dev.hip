@@ -30,6 +30,7 @@
 #include "nwl_kernel.hip"
 #include "nwp_kernel.hip"
 #include "seed_kernel.hip"
+#include "round_policy.h"
 
 
 #define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
@@ -1360,19 +1361,11 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     if (const char *pc = getenv("IMSAME_DEV_PATHS_CAP")) want_cap = strtoull(pc, nullptr, 10);   // test hook
     if ((rc = paths_setup(c, p, want_cap, &pcap))) return rc;
     if (n == 0) { if (stats) *stats = st; return IMSAME_OK; }
-    // speculation from a read's first weak candidate on (seed_kernel.hip:
-    // spec_after_first); a round then emits up to n * spec_weak + n candidates
-    // (reads with a rejection emit <= n in all, S.spec below)
-    const char *sw_env = getenv("IMSAME_SPEC_WEAK");
-    const uint32_t spec_weak = (uint32_t)std::max(1, std::min(SPEC_MAX, sw_env ? atoi(sw_env) : SPEC_WEAK));
-    // candidate lists: 2 per read (up to SPEC_MAX for small calls -- long
-    // reads, few per call, fill launches by speculating)
-    // (IMSAME_CCAP_MULT: candidates per read the lists hold, default 2 -- round
-    // 1b's speculation width is bounded by the room left after round 1)
-    const char *cm_env = getenv("IMSAME_CCAP_MULT");
-    const uint64_t cmult = cm_env ? (uint64_t)std::max(2, std::min(SPEC_BIG, atoi(cm_env))) : 2u;
-    const uint64_t ccap = std::max<uint64_t>((uint64_t)n * std::max<uint64_t>(spec_weak > 1 ? spec_weak + 1 : 2, cmult),
-                                             std::min<uint64_t>((uint64_t)n * SPEC_MAX, 1u << 20));
+    // the rounds' policy (round_policy.h, shared with the CPU emulator):
+    // list capacity, speculation, budgets, scan group sizes, round 1b
+    const uint32_t short_y = std::min<uint32_t>(ycap, NW_W / 2);
+    const RoundPolicy RP = RoundPolicy::make(n, ycap, short_y, c->nlanes);
+    const uint64_t ccap = RP.ccap;
     if (c->res.ensure((uint64_t)n * 64) || c->cur_p.ensure((uint64_t)n * 8) || c->cur_h.ensure((uint64_t)n * 4) ||
         c->memo.ensure((uint64_t)n * 4 * MEMO) || c->nmemo.ensure(n) || c->rstat.ensure(n) ||
         c->act0.ensure((uint64_t)n * 4) || c->act1.ensure((uint64_t)n * 4) || c->act2.ensure((uint64_t)n * 4) ||
@@ -1388,26 +1381,8 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         for (const DBuf *b : scr)
             if ((rc = b->poison(s))) return rc;
     }
-    // predicted rows for the packed kernel's first-sweep traceback windows:
-    // ON by default (IMSAME_NW_WINDOW=0 turns them off).  Round 2 measured them
-    // 1-3 % slower (the window steps spilled at 4 waves per SIMD, and round 1b
-    // was off with them, profiles/r2s_ab_*.json); at 3 waves per SIMD (no
-    // spills) and with round 1b they take C2's NW busy time from 113.4 to
-    // 107.4 ms and the step from 119.9 to 113.9 ms (profiles/r4d/).
-    const char *win_env = getenv("IMSAME_NW_WINDOW");
-    int32_t *crow = (win_env && !atoi(win_env)) ? nullptr : c->crow.as<int32_t>();
-    // speculation: round 1 emits one candidate per read (most reads accept
-    // it); later rounds emit up to SPEC_MAX, bounded by the candidate buffers
-    const char *spec_env = getenv("IMSAME_SPEC");
-    const uint32_t spec_later = spec_env ? (uint32_t)std::max(1, std::min(SPEC_MAX, atoi(spec_env))) : (uint32_t)SPEC_MAX;
-    const char *bud_env = getenv("IMSAME_SEED_BUDGET");
-    const uint32_t budget1 = bud_env ? (uint32_t)std::max(0, atoi(bud_env)) : SEED_BUDGET1;
-    // budget growth per round: 8x; a lane of < 100k reads (an 8-GPU shard of
-    // C2) 64x, so its third round finishes the random reads' scans instead of
-    // leaving a latency-bound fourth round of tiny launches (C2 shard 1/8:
-    // 23.4 -> 20.1 ms per step; no effect from 1/4 up, profiles/r2u_*, r2v_*)
-    const char *grow_env = getenv("IMSAME_SEED_GROW");
-    const uint32_t grow = grow_env ? (uint32_t)std::max(2, atoi(grow_env)) : (n < 100000 ? 64u : 8u);
+    // predicted rows for the packed kernel's first-sweep traceback windows
+    int32_t *crow = RP.window ? c->crow.as<int32_t>() : nullptr;
     const uint8_t *qd = dev_q(c);
     const uint64_t *qsd = dev_qs(c);
     uint64_t *ctr = c->ctr.as<uint64_t>();
@@ -1421,19 +1396,11 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     HIPCHK(hipGetLastError());
     st.ms_setup = now_ms() - t_start;
 
-    const uint32_t short_y = std::min<uint32_t>(ycap, NW_W / 2);
-    const char *l64_env = getenv("IMSAME_SEED_L64");
-    // (C2 1/8 shard: 18.5 vs 19.2 ms per step, round 2's ~2k reads scan in a
-    // third of the time; 32768 also takes round 1b's 17k: 18.9; C2 unchanged;
-    // profiles/r3l64/)
-    const uint64_t seed_l64_below = l64_env ? strtoull(l64_env, nullptr, 10) : 8192;
-    const char *r1b_env = getenv("IMSAME_ROUND1B");
-    // (on under IMSAME_DEBUG_POISON too: the poisoned suite must run the
-    // concurrent path -- two streams on the shared arena, slot bitmap,
+    // (round 1b runs under IMSAME_DEBUG_POISON too: the poisoned suite must
+    // run the concurrent path -- two streams on the shared arena, slot bitmap,
     // C_PATHS / C_FLAGS counters; POISON_SYNC waits for one stream only)
     // (with predicted traceback windows, round 1's launch is ordered by row;
     // round 1b's candidates carry no prediction and keep their order)
-    const bool r1b_on = !(r1b_env && !atoi(r1b_env)) && ycap <= short_y;
     uint32_t nact = n;
     uint32_t *act = c->act0.as<uint32_t>(), *nxt = c->act1.as<uint32_t>();
     while (nact) {
@@ -1453,10 +1420,10 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         S.nmemo = c->nmemo.as<uint8_t>(); S.rstat = c->rstat.as<uint8_t>();
         S.minraw = c->minraw.as<uint64_t>(); S.n_minraw = ymax + 1;
         S.max_rs = p->max_read_size; S.short_ylen = short_y; S.max_rec = c->max_rec;
-        // (a round's candidates fit the ccap-entry lists: nact x spec <= ccap)
-        S.spec = (st.rounds == 1) ? 1u : (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(spec_later, ccap / nact));
-        S.spec_weak = spec_weak;
-        S.budget = seed_budget(budget1, (uint32_t)st.rounds, grow);
+        const uint32_t rnd = (uint32_t)st.rounds;
+        S.spec = RP.spec(rnd, nact);
+        S.spec_weak = RP.spec_weak;
+        S.budget = RP.budget(rnd);
         S.next = nxt; S.nnext = (uint32_t *)(ctr + C_NNEXT);
         S.cbase = c->cbase.as<uint32_t>(); S.ccnt = c->ccnt.as<uint32_t>(); S.perr = c->perr.as<uint32_t>();
         S.cread = c->cread.as<uint32_t>(); S.csid = c->csid.as<uint32_t>(); S.ncand = (uint32_t *)(ctr + C_NCAND);
@@ -1469,22 +1436,8 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         S.wstart = c->use_wstart ? c->wstart.as<uint64_t>() : nullptr;
         S.minlen = c->minlen.as<uint32_t>(); S.n_minlen = ymax + 1;
         S.minident = c->minident.as<uint32_t>(); S.n_minident = xcap + ymax + 2;
-        const char *l_env = getenv(st.rounds == 1 && getenv("IMSAME_SEED_L1") ? "IMSAME_SEED_L1" : "IMSAME_SEED_L");
-        // group size from the reads the device scans at once: this lane's
-        // times the call's lanes (C2, 8 lanes of 125k: 4 lanes per read in
-        // round 1 instead of 16, whose extra windows a true read never needs;
-        // +1.9 %, profiles/r2am_*)
-        auto pick_L = [&](uint32_t na) {
-            int L = l_env ? atoi(l_env) : seed_lanes((uint32_t)std::min<uint64_t>((uint64_t)na * c->nlanes, 0xFFFFFFFFu));
-            // a whole wave per read where few reads scan (the later rounds: each
-            // read's remaining windows 64 at a time), IMSAME_SEED_L64 = the read
-            // count (over all lanes) below which (0: never); those groups may
-            // emit up to SPEC_BIG candidates per read
-            if (!l_env && (uint64_t)na * c->nlanes < seed_l64_below) L = 64;
-            return L;
-        };
         auto seed_launch = [&](const SeedLaunch &SL, uint32_t na, hipStream_t ss, hipEvent_t e0, hipEvent_t e1) -> int {
-            const int L = pick_L(na);
+            const int L = RP.pick_L(rnd, na);
             const size_t slds = 256 * SEED_LDS_PER_LANE;
             HIPCHK(hipEventRecord(e0, ss));
             if (L >= 64)      seed_group_kernel<64, SPEC_BIG><<<nblk((uint64_t)na * 64, 256), 256, 256 * SPEC_BIG * 8, ss>>>(SL);
@@ -1534,8 +1487,6 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
             HIPCHK(hipGetLastError());
             return 0;
         };
-        if (st.rounds >= 2 && !spec_env && pick_L(nact) >= 64)   // whole-wave groups: up to SPEC_BIG
-            S.spec = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(SPEC_BIG, ccap / nact));
         if ((rc = seed_launch(S, nact, s, c->ev0, c->ev1))) return rc;
         uint64_t hc[3];
         HIPCHK(hipMemcpyAsync(hc, ctr + C_NCAND, 24, hipMemcpyDeviceToHost, s));
@@ -1555,7 +1506,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         // non-persistent (they share the arena and its slot bitmap);
         // IMSAME_ROUND1B=0 turns it off.
         NwPlan pla = {};
-        bool r1b = st.rounds == 1 && r1b_on && hc[2] > 0 && n2 == 0 && ccap > n1;
+        bool r1b = RP.r1b(rnd, n1, n2, hc[2]);
         if (r1b && n1 && (rc = plan_nw(c, short_y, xcap, n1, p, c->q_len_mult, &pla, true, c->q_len_uni))) return rc;
         if (r1b && n1 && !pla.np) r1b = false;
         if (r1b) {
@@ -1570,10 +1521,8 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
             SeedLaunch Sb = S;
             Sb.active = nxt; Sb.n_active = npz;
             Sb.spec = 1;
-            // up to SPEC_MAX per read, SPEC_BIG where whole-wave groups scan (their lists hold it)
-            Sb.spec_weak = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(pick_L(npz) >= 64 ? SPEC_BIG : SPEC_MAX,
-                                                                              (ccap - n1) / npz));
-            Sb.budget = seed_budget(budget1, 2, grow);
+            Sb.spec_weak = RP.r1b_spec_weak(n1, npz);
+            Sb.budget = RP.r1b_budget();
             Sb.next = act2; Sb.nnext = (uint32_t *)(ctr + C_NNEXT2);
             Sb.cread = c->cread.as<uint32_t>() + n1; Sb.csid = c->csid.as<uint32_t>() + n1;
             Sb.ncand = (uint32_t *)(ctr + C_NCANDB); Sb.crow = nullptr;

@@ -70,6 +70,7 @@ static void fiber_entry() {
 #include "../../imsame_amd/csrc/nwl_kernel.hip"
 #include "../../imsame_amd/csrc/nwp_kernel.hip"
 #include "../../imsame_amd/csrc/seed_kernel.hip"
+#include "../../imsame_amd/csrc/round_policy.h"
 
 static void run_wave(const std::function<void(int)> &f) {
 #ifdef EMU_THREADS
@@ -348,22 +349,14 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
     imsame_build_tables(p, db_len, ymax, xcap, mr, ml, mi);
     const uint32_t n = (uint32_t)(read_to - read_from);
     std::vector<uint64_t> cur_p(n);
-    // imsame_dev.hip:align_one -- speculation from a weak first candidate, candidate capacity
-    const char *sw_env = getenv("IMSAME_SPEC_WEAK");
-    const uint32_t spec_weak = (uint32_t)std::max(1, std::min(SPEC_MAX, sw_env ? atoi(sw_env) : SPEC_WEAK));
-    const char *cm_env = getenv("IMSAME_CCAP_MULT");
-    const size_t cmult = cm_env ? (size_t)std::max(2, std::min(SPEC_BIG, atoi(cm_env))) : 2u;
-    const size_t ccap = std::max<size_t>((size_t)n * std::max<size_t>(spec_weak > 1 ? spec_weak + 1 : 2, cmult),
-                                         std::min<size_t>((size_t)n * SPEC_MAX, 1u << 20));
+    // the rounds' policy: the device's own (round_policy.h, imsame_dev.hip:align_one), one lane
+    const uint32_t short_y = std::min<uint32_t>(ycap, NW_W / 2);
+    const RoundPolicy RP = RoundPolicy::make(n, ycap, short_y, 1);
+    const size_t ccap = RP.ccap;
     std::vector<uint32_t> cur_h(n), memo((size_t)n * MEMO), act(n), nxt(n), act2(n), cr(ccap), cs(ccap), cr2(ccap), cs2(ccap);
     std::vector<uint32_t> cbase(n), ccnt(n), perr(n);
     std::vector<int32_t> crow(ccap);
-    const char *win_env = getenv("IMSAME_NW_WINDOW");
-    int32_t *crowp = (win_env && !atoi(win_env)) ? nullptr : crow.data();     // imsame_dev.hip: on by default
-    const char *spec_env = getenv("IMSAME_SPEC");
-    const uint32_t spec_later = spec_env ? (uint32_t)std::max(1, std::min(SPEC_MAX, atoi(spec_env))) : (uint32_t)SPEC_MAX;
-    const char *bud_env = getenv("IMSAME_SEED_BUDGET");
-    const uint32_t budget1 = bud_env ? (uint32_t)std::max(0, atoi(bud_env)) : SEED_BUDGET1;
+    int32_t *crowp = RP.window ? crow.data() : nullptr;
     std::vector<uint8_t> nmemo(n), rstat(n);
     std::vector<imsame_read_result> o1(ccap), o2(ccap);
     // per-candidate results poisoned like reused device buffers: a candidate the
@@ -374,9 +367,6 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
     for (uint32_t k = 0; k < n; ++k) init_one(I, k);
     uint32_t nc[3] = {0, 0, 0}, pused = 0, flags = 0;
     unsigned long long err = ~0ull, nhits = 0, cells = 0, nacc = 0;
-    const uint32_t short_y = std::min<uint32_t>(ycap, NW_W / 2);
-    const char *r1b_env = getenv("IMSAME_ROUND1B");
-    const bool r1b_on = !(r1b_env && !atoi(r1b_env)) && ycap <= short_y;
     uint32_t nact = n;
     imsame_stats st;
     memset(&st, 0, sizeof st);
@@ -397,22 +387,17 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
         S.minlen = ml.data(); S.n_minlen = ymax + 1;
         S.minident = mi.data(); S.n_minident = xcap + ymax + 2;
         S.max_rs = p->max_read_size; S.short_ylen = short_y; S.max_rec = max_rec;
-        S.spec = (st.rounds == 1) ? 1u : (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(spec_later, ccap / nact));
-        {   // imsame_dev.hip:align_one -- whole-wave groups may emit up to SPEC_BIG
-            const char *le = getenv("IMSAME_SEED_L");
-            if (st.rounds >= 2 && !spec_env && (le ? atoi(le) : seed_lanes(nact)) >= 64)
-                S.spec = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(SPEC_BIG, ccap / nact));
-        }
-        S.spec_weak = spec_weak;
-        S.budget = seed_budget(budget1, (uint32_t)st.rounds);
+        const uint32_t rnd = (uint32_t)st.rounds;
+        S.spec = RP.spec(rnd, nact);
+        S.spec_weak = RP.spec_weak;
+        S.budget = RP.budget(rnd);
         S.next = nxt.data(); S.nnext = &nc[2];
         S.cbase = cbase.data(); S.ccnt = ccnt.data(); S.perr = perr.data();
         S.cread = cr.data(); S.csid = cs.data(); S.ncand = &nc[0]; S.crow = crowp;
         S.cread2 = cr2.data(); S.csid2 = cs2.data(); S.ncand2 = &nc[1];
         S.err = &err; S.nhits = &nhits;
-        const char *l_env = getenv("IMSAME_SEED_L");
         auto run_seed = [&](const SeedLaunch &SL, uint32_t na) {
-            const int L = l_env ? atoi(l_env) : seed_lanes(na);
+            const int L = RP.pick_L(rnd, na);
             if (L <= 1) {
                 for (uint32_t i = 0; i < na; ++i) { uint64_t h = 0; seed_one(SL, i, h); nhits += h; }
             } else {                   // seed_group_kernel: 64-lane waves, several host threads
@@ -430,8 +415,9 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
                             uint64_t h = 0;
                             const uint32_t gidx = (uint32_t)((w0 + lane) / L);
                             if (L == 64) seed_group<64, SPEC_BIG>(SL, gidx, lane, lane, ld + lane * SPEC_BIG, h);
-                            else if (L == 16) seed_group<16>(SL, gidx, lane % 16, lane, ld + lane * SPEC_MAX, h);
-                            else         seed_group<4>(SL, gidx, lane % 4, lane, ld + lane * SPEC_MAX, h);
+                            else if (L >= 16) seed_group<16>(SL, gidx, lane % 16, lane, ld + lane * SPEC_MAX, h);
+                            else if (L >= 4) seed_group<4>(SL, gidx, lane % 4, lane, ld + lane * SPEC_MAX, h);
+                            else         seed_group<2>(SL, gidx, lane % 2, lane, ld + lane * SPEC_MAX, h);
                             wh += h;
                         });
                     }
@@ -456,16 +442,14 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
         if (nc[0] + nc[1] + nc[2] == 0) break;
         // round 1b (imsame_dev.hip:align_one): the reads round 1 paused scan on
         // (weak-first speculation, round 2's budget) before round 1's NW results
-        if (st.rounds == 1 && r1b_on && nc[2] > 0 && nc[1] == 0 && ccap > nc[0]) {
+        if (RP.r1b(rnd, nc[0], nc[1], nc[2])) {
             const uint32_t n1 = nc[0], npz = nc[2];
             uint32_t nb[3] = {0, 0, 0};
             SeedLaunch Sb = S;
             Sb.active = nxt.data(); Sb.n_active = npz;
             Sb.spec = 1;
-            const int Lb = l_env ? atoi(l_env) : seed_lanes(npz);
-            Sb.spec_weak = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(Lb >= 64 ? SPEC_BIG : SPEC_MAX,
-                                                                              (ccap - n1) / npz));
-            Sb.budget = seed_budget(budget1, 2);
+            Sb.spec_weak = RP.r1b_spec_weak(n1, npz);
+            Sb.budget = RP.r1b_budget();
             Sb.next = act2.data(); Sb.nnext = &nb[2];
             Sb.cread = cr.data() + n1; Sb.csid = cs.data() + n1; Sb.ncand = &nb[0]; Sb.crow = nullptr;
             Sb.ncand2 = &nb[1];

@@ -541,6 +541,9 @@ def test_emulated_pipeline_seed_budget(emu, oracle, budget, lanes, spec, weak, m
     monkeypatch.setenv("IMSAME_SEED_L", lanes)
     monkeypatch.setenv("IMSAME_SPEC", spec)
     monkeypatch.setenv("IMSAME_SPEC_WEAK", weak)
+    r1b = emu.lib.emu_r1b_count
+    r1b.restype = C.c_uint32
+    r1b()
     rounds = 0
     for name in ("borrowed", "reads_vs_reads", "toolong"):
         case = G.e2e_case(name)
@@ -554,7 +557,9 @@ def test_emulated_pipeline_seed_budget(emu, oracle, budget, lanes, spec, weak, m
         for f in PARITY_FIELDS:
             assert np.array_equal(r1[f][:n], r2[f][:n]), (name, budget, f)
         rounds = max(rounds, st.rounds)
-    assert rounds >= (2 if budget != "0" else 1)
+    # a budget pauses reads: they resume in round 2, or in round 1b (the
+    # device's policy, round_policy.h, gives small calls round 2's budget x 64)
+    assert rounds >= 2 or r1b() > 0 or budget == "0", rounds
 
 
 def test_thresholds_match_long_double_tests(emu, oracle):
