@@ -3,6 +3,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <emmintrin.h>
 #include <pthread.h>
 #include <unistd.h>
 #include "imsame_host.h"
@@ -276,42 +277,60 @@ uint64_t host_render_scratch(const uint8_t *X, uint64_t xlen, const uint8_t *Y, 
     /* the last block's match line pairs X with up to 60 bytes past ry[M]:
      * zero there, as in the reference's memset buffers (never a '*') */
     memset(ry + M + 1, 0, IMSAME_ALIGN_LEN + 4);
-    uint64_t hx = M, hy = M, k;
-    for (k = xlen - 1; k > r->bx; k--) rx[hx--] = '-';
-    for (k = ylen - 1; k > r->by; k--) ry[hy--] = '-';
+    /* right to left; every run is a contiguous copy or fill ending at hx / hy */
+    uint64_t hx = M, hy = M;
+#define FILL(buf, h, c, n) do { const uint64_t n_ = (n); memset((buf) + (h) + 1 - n_, (c), n_); (h) -= n_; } while (0)
+#define COPY(buf, h, src, p, n) do { const uint64_t n_ = (n); memcpy((buf) + (h) + 1 - n_, (src) + (p) + 1 - n_, n_); (h) -= n_; } while (0)
+    FILL(rx, hx, '-', xlen - 1 - r->bx);
+    FILL(ry, hy, '-', ylen - 1 - r->by);
     uint64_t px = r->bx, py = r->by;
     for (uint32_t e = 0; e < r->path_len; ++e) {
         const uint32_t mv = path[e] >> 30, n = path[e] & 0x3FFFFFFFu;
         if (mv == IMSAME_MOVE_DIAG) {
-            for (uint32_t d = 0; d < n; ++d) { rx[hx--] = (char)X[px--]; ry[hy--] = (char)Y[py--]; }
+            COPY(rx, hx, X, px, n); COPY(ry, hy, Y, py, n);
+            px -= n; py -= n;
         } else if (mv == IMSAME_MOVE_UP) {
-            for (uint32_t d = 0; d < n; ++d) { ry[hy--] = '-'; rx[hx--] = (char)X[px - d]; }
+            FILL(ry, hy, '-', n); COPY(rx, hx, X, px, n);
             px -= n; py -= 1;
         } else {
-            for (uint32_t d = 0; d < n; ++d) { rx[hx--] = '-'; ry[hy--] = (char)Y[py - d]; }
+            FILL(rx, hx, '-', n); COPY(ry, hy, Y, py, n);
             py -= n; px -= 1;
         }
     }
-    for (k = 0; k < px; k++) rx[hx--] = '-';
-    for (k = 0; k < py; k++) ry[hy--] = '-';
-    if (px >= py) for (k = 0; k < px; k++) ry[hy--] = ' ';
-    else          for (k = 0; k < py; k++) rx[hx--] = ' ';
+    FILL(rx, hx, '-', px);
+    FILL(ry, hy, '-', py);
+    if (px >= py) FILL(ry, hy, ' ', px);
+    else          FILL(rx, hx, ' ', py);
+#undef FILL
+#undef COPY
     /* build_alignment's loop (:233-271): the strings are [hx+1, M] and [hy+1, M]
      * (the reference prints bytes of rec_X/rec_Y up to index M) */
     text_reserve(t, host_render_size(xlen, ylen, r));
     char *o = t->buf + t->len;
     uint64_t i = hx + 1, j = hy + 1, ident = 0;
+    const __m128i dash = _mm_set1_epi8('-'), star = _mm_set1_epi8('*'), space = _mm_set1_epi8(' ');
     while (i <= M && j <= M) {
         const uint64_t nx = M - i + 1 < IMSAME_ALIGN_LEN ? M - i + 1 : IMSAME_ALIGN_LEN;
         const uint64_t ny = M - j + 1 < IMSAME_ALIGN_LEN ? M - j + 1 : IMSAME_ALIGN_LEN;
         memcpy(o, rx + i, nx); o += nx; *o++ = '\n';
         memcpy(o, ry + j, ny); o += ny; *o++ = '\n';
-        for (uint64_t b = 0; b < nx; b++) {
-            const char a = rx[i + b], c = ry[j + b];
-            const int star = a != '-' && c != '-' && a == c;
-            ident += star;
-            *o++ = star ? '*' : ' ';
+        /* the match line, 16 columns at a time: '*' where both are the same
+         * base (neither a gap) */
+        uint64_t b = 0;
+        for (; b + 16 <= nx; b += 16) {
+            const __m128i a = _mm_loadu_si128((const __m128i *)(rx + i + b));
+            const __m128i c = _mm_loadu_si128((const __m128i *)(ry + j + b));
+            const __m128i m = _mm_andnot_si128(_mm_cmpeq_epi8(a, dash), _mm_cmpeq_epi8(a, c));
+            _mm_storeu_si128((__m128i *)(o + b), _mm_or_si128(_mm_and_si128(m, star), _mm_andnot_si128(m, space)));
+            ident += (uint64_t)__builtin_popcount((unsigned)_mm_movemask_epi8(m));
         }
+        for (; b < nx; b++) {
+            const char a = rx[i + b], c = ry[j + b];
+            const int st = a != '-' && c != '-' && a == c;
+            ident += st;
+            o[b] = st ? '*' : ' ';
+        }
+        o += nx;
         *o++ = '\n';
         i += nx; j += ny;
     }
