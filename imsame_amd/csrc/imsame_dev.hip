@@ -434,6 +434,7 @@ static int hw_queues() {
 // late, profiles/r3_c2_timeline.txt) -- so queues / 2, <= 8 (C2, 8 queues:
 // 4 lanes, 119.3-119.9 vs 121.0-121.6 ms with 8, profiles/r3q16/).
 #define LANES_MAX 8
+#define LANES_DEF 3                 // lanes a call uses by default (align_impl); more are added on demand
 static int lanes_for_queues() { return std::max(1, std::min(LANES_MAX, hw_queues() / 2)); }
 
 extern "C" int imsame_dev_count(void) {
@@ -516,7 +517,7 @@ extern "C" int imsame_dev_open(int device, imsame_ctx **out) {
     // shares the least used one.  So the compute streams of this context and
     // its lanes come first, one queue each, and the upload stream last, on the
     // last lane's queue (that lane starts after the whole upload anyway).
-    for (int k = 1; k < lanes_for_queues() && !rc; ++k) rc = lane_add(c);
+    for (int k = 1; k < std::min(lanes_for_queues(), LANES_DEF) && !rc; ++k) rc = lane_add(c);
     if (!rc && hipStreamCreateWithFlags(&c->ustream, hipStreamNonBlocking) != hipSuccess) rc = IMSAME_E_HIP;
     // round 1b's streams (align_one) after the lanes' compute streams: they
     // share the hardware queues the runtime has left (created here, not in a
@@ -1701,7 +1702,6 @@ static double union_ms(std::vector<std::pair<float, float>> v) {
 // Reads per lane below which a call is not split (a lane must fill the chip)
 #define LANE_MIN 32768
 #define LANE_READS 40000
-#define LANES_DEF 3
 
 // Hand lane l's finished reads [a, b) to an imsame_dev_align_parts callback,
 // with its paths copied to the host (path_off of those rows index them).
