@@ -481,9 +481,9 @@ static int ctx_create(int device, imsame_ctx **out) {
     HIPCHK(hipSetDevice(device));
     imsame_ctx *c = new imsame_ctx();
     c->device = device;
-    hipDeviceProp_t prop;
-    HIPCHK(hipGetDeviceProperties(&prop, device));
-    c->ncu = prop.multiProcessorCount;
+    // CU count: one attribute query (hipGetDeviceProperties fills the whole
+    // struct and costs milliseconds per context)
+    HIPCHK(hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, device));
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(hipEventCreate(&c->ev0));
     HIPCHK(hipEventCreate(&c->ev1));
@@ -518,6 +518,7 @@ extern "C" int imsame_dev_open(int device, imsame_ctx **out) {
     // its lanes come first, one queue each, and the upload stream last, on the
     // last lane's queue (that lane starts after the whole upload anyway).
     for (int k = 1; k < std::min(lanes_for_queues(), LANES_DEF) && !rc; ++k) rc = lane_add(c);
+    const double t3 = dbg ? now_ms() : 0;
     if (!rc && hipStreamCreateWithFlags(&c->ustream, hipStreamNonBlocking) != hipSuccess) rc = IMSAME_E_HIP;
     // round 1b's streams (align_one) after the lanes' compute streams: they
     // share the hardware queues the runtime has left (created here, not in a
@@ -531,8 +532,8 @@ extern "C" int imsame_dev_open(int device, imsame_ctx **out) {
     }
     if (rc) { imsame_dev_close(c); return rc; }
     if (dbg)
-        fprintf(stderr, "[imsame] open_ms {\"runtime\": %.2f, \"context\": %.2f, \"lanes_streams\": %.2f}\n", t1 - t0,
-                t2 - t1, now_ms() - t2);
+        fprintf(stderr, "[imsame] open_ms {\"runtime\": %.2f, \"context\": %.2f, \"lanes\": %.2f, \"streams\": %.2f}\n",
+                t1 - t0, t2 - t1, t3 - t2, now_ms() - t3);
     *out = c;
     return IMSAME_OK;
 }
