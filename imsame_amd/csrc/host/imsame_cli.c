@@ -223,10 +223,10 @@ int main(int argc, char **argv) {
             pr.st.rounds, pr.st.n_nw, pr.st.nw_cells, pr.st.ms_seed, pr.st.ms_nw, pr.st.ms_total);
     fprintf(stderr, "[imsame] phases {\"devices\": %d, \"parts\": %" PRIu64 ", \"open_s\": %.4f, \"parse_db_s\": %.4f, \"index_s\": %.4f, "
             "\"parse_query_s\": %.4f, \"upload_s\": %.4f, \"align_s\": %.4f, \"render_busy_s\": %.4f, "
-            "\"write_busy_s\": %.4f, \"render_tail_s\": %.4f, \"bytes_out\": %" PRIu64 ", \"accepted\": %" PRIu64
-            ", \"wall_s\": %.4f}\n",
+            "\"write_busy_s\": %.4f, \"render_tail_s\": %.4f, \"pwrite_sum_s\": %.4f, \"pwrite_max_s\": %.4f, "
+            "\"bytes_out\": %" PRIu64 ", \"accepted\": %" PRIu64 ", \"wall_s\": %.4f}\n",
             G, pr.batches, oj.secs, t_parse_db, t_index, t_parse_q, t_upload, pr.t_align, pr.t_render, pr.t_write, pr.t_tail,
-            pr.bytes_out, acc, now_s() - t_wall);
+            pr.t_pwrite_sum, pr.t_pwrite_max, pr.bytes_out, acc, now_s() - t_wall);
     /* IMSAME_FAST_EXIT=1: leave the device contexts and the heap to process
      * exit (the output is closed and stdout flushed; the kernel driver releases
      * the GPU memory), skipping hipFree of the arenas and the runtime's exit

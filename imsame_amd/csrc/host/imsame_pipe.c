@@ -134,6 +134,7 @@ typedef struct {
     uint64_t off;
     uint64_t bytes;                    /* record bytes of [from, to) (size_task) */
     int fd, err;
+    double t_pw;                       /* seconds in pwrite (render_write_task) */
 } rtask;
 
 static int digits(uint64_t v) {
@@ -218,12 +219,18 @@ static void *render_write_task(void *a) {
         if (t->res[r].status != 1) continue;
         render_one(t, r);
         if (t->text.len >= RW_PIECE) {
+            const double w0 = pipe_now();
             t->err = write_all(t->fd, t->text.buf, t->text.len, t->off + done, 1);
+            t->t_pw += pipe_now() - w0;
             done += t->text.len;
             t->text.len = 0;
         }
     }
-    if (!t->err && t->text.len) t->err = write_all(t->fd, t->text.buf, t->text.len, t->off + done, 1);
+    if (!t->err && t->text.len) {
+        const double w0 = pipe_now();
+        t->err = write_all(t->fd, t->text.buf, t->text.len, t->off + done, 1);
+        t->t_pw += pipe_now() - w0;
+    }
     done += t->text.len;
     t->text.len = 0;
     if (!t->err && done != t->bytes) {                 /* record_size must be exact */
@@ -315,9 +322,14 @@ static int render_write_part(rtask *t, int nt, const host_seqs *db, const host_s
     }
     r->bytes_out = *off;
     const double t1 = pipe_now();
+    for (int k = 0; k < nt; ++k) t[k].t_pw = 0;
     run_pool(t, nt, render_write_task);
     r->t_render += t1 - t0;                /* sizing */
     r->t_write += pipe_now() - t1;         /* render + pwrite, fused */
+    for (int k = 0; k < nt; ++k) {         /* diagnostics: the threads' pwrite time */
+        r->t_pwrite_sum += t[k].t_pw;
+        if (t[k].t_pw > r->t_pwrite_max) r->t_pwrite_max = t[k].t_pw;
+    }
     for (int k = 0; k < nt; ++k)
         if (t[k].err) return t[k].err;
     return 0;

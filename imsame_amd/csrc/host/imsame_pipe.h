@@ -42,6 +42,7 @@ typedef struct {
     double t_render;             /* render threads' busy wall, summed per part */
     double t_write;              /* pwrite wall, summed per part             */
     double t_tail;               /* last part delivered -> output complete   */
+    double t_pwrite_sum, t_pwrite_max;   /* render threads' pwrite seconds: summed, one thread's most */
 } pipe_result;
 
 /* parse "-devices" values: "N" (devices 0..N-1) or "d0,d1,..." */
