@@ -321,6 +321,10 @@ static int render_write_part(rtask *t, int nt, const host_seqs *db, const host_s
         *off += t[k].bytes;
     }
     r->bytes_out = *off;
+    if (getenv("IMSAME_FALLOCATE") && nt) {   /* experiment: the part's blocks allocated before its writes */
+        const uint64_t a = t[0].off;
+        if (*off > a) (void)posix_fallocate(fd, (off_t)a, (off_t)(*off - a));
+    }
     const double t1 = pipe_now();
     for (int k = 0; k < nt; ++k) t[k].t_pw = 0;
     run_pool(t, nt, render_write_task);
