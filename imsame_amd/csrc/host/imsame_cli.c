@@ -227,12 +227,13 @@ int main(int argc, char **argv) {
             "\"bytes_out\": %" PRIu64 ", \"accepted\": %" PRIu64 ", \"wall_s\": %.4f}\n",
             G, pr.batches, oj.secs, t_parse_db, t_index, t_parse_q, t_upload, pr.t_align, pr.t_render, pr.t_write, pr.t_tail,
             pr.t_pwrite_sum, pr.t_pwrite_max, pr.bytes_out, acc, now_s() - t_wall);
-    /* IMSAME_FAST_EXIT=1: leave the device contexts and the heap to process
-     * exit (the output is closed and stdout flushed; the kernel driver releases
-     * the GPU memory), skipping hipFree of the arenas and the runtime's exit
-     * handlers */
-    const char *fe = getenv("IMSAME_FAST_EXIT");
-    if (fe && atoi(fe)) {
+    /* The device contexts and the heap are left to process exit (the output
+     * is closed and stdout flushed; the kernel driver releases the GPU
+     * memory): hipFree of the arenas and the runtime's exit handlers cost
+     * 0.04-0.14 s of a 0.7-0.9 s C2 run (profiles/r4l/, r4m/).
+     * IMSAME_CLEAN_EXIT=1 tears everything down (leak checks). */
+    const char *ce = getenv("IMSAME_CLEAN_EXIT"), *fe = getenv("IMSAME_FAST_EXIT");
+    if (!(ce && atoi(ce)) && !(fe && !atoi(fe))) {
         fprintf(stderr, "[imsame] teardown {\"close_s\": 0, \"fast_exit\": 1}\n");
         fflush(stderr);
         _exit(0);
