@@ -463,6 +463,7 @@ def main():
                        + ("" if world == 1 or a.dist_backend == "nccl" else
                           f"; REHEARSAL: {a.dist_backend} collectives, device {gpu} shared by all ranks")},
             "roofline": roofline,
+            "seed_roofline": seed_roofline(last, hi - lo, a.read_len),
             "parity": parity,
             "cpu_baseline": cpu,
             "e2e": e2e,
@@ -493,6 +494,33 @@ def main():
     rpin.free()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def seed_roofline(st, n_reads, read_len):
+    """The seed scan's memory work against its kernels' own time (SURVEY
+    8(d)): per read its bases, per probed window two CSR offsets, per CSR
+    entry read the entry, per ungapped extension the database and query bytes
+    it loads (16-byte chunk pairs), counted by the kernels
+    (imsame_stats.seed_*).  Time = the seed launches' HIP-event durations
+    summed over lanes (they share the chip with NW launches of other lanes).
+    The scan is a chain of dependent random probes (offsets -> entries ->
+    record bytes), so the rate it reaches is latency-bound: `probes_per_s`
+    and `bytes_per_probe` are the model, the HBM fraction is context."""
+    wins, ents, ch = st.get("seed_windows", 0), st.get("seed_entries", 0), st.get("seed_ext_chunks", 0)
+    ms = st.get("ms_seed", 0.0)
+    if not wins or not ms:
+        return None
+    survey = n_reads * read_len + 8 * wins + 4 * st["n_hits"] + 32 * ch       # SURVEY 8(d) widths
+    built = n_reads * read_len + 16 * wins + 8 * ents + 32 * ch               # u64 offsets, 8-byte entries
+    t = ms / 1e3
+    return {"bound": "latency (dependent random probes)", "kernel_ms": round(ms, 3),
+            "windows": wins, "entries": ents, "hits": st["n_hits"], "ext_chunk_pairs": ch,
+            "bytes_survey_model": survey, "bytes_as_built": built,
+            "achieved_gbs": round(built / t / 1e9, 2), "peak_gbs": HBM_PEAK_GBS,
+            "frac": round(built / t / 1e9 / HBM_PEAK_GBS, 4),
+            "probes_per_s": round(wins / t, 1), "entries_per_s": round(ents / t, 1),
+            "bytes_per_probe": round(built / wins, 2),
+            "ext_bytes_per_hit": round(32 * ch / max(st["n_hits"], 1), 1)}
 
 
 # MI355X_MICROARCH.md: a wave issues one VALU instruction over 2 cycles

@@ -380,7 +380,7 @@ static inline const uint64_t *dev_qs(const imsame_ctx *c) {
 // counters block layout (u64 slots)
 enum { C_NCAND = 0, C_NCAND2, C_NNEXT, C_NCANDB, C_NCAND2B, C_NNEXT2, C_WORKB,   // (round 1b: B, 2)
        C_WORK, C_WORK2, C_PATHS, C_FLAGS, C_ERR, C_HITS, C_CELLS, C_NACC, C_REDO,
-       C_PROF, C_WIN = C_PROF + 5, C_FBK, C_DBG, C_NSLOTS = C_DBG + 8 };
+       C_PROF, C_WIN = C_PROF + 5, C_FBK, C_SWORK, C_DBG = C_SWORK + 3, C_NSLOTS = C_DBG + 8 };
 
 static double now_ms() {
     struct timespec ts; clock_gettime(CLOCK_MONOTONIC, &ts);
@@ -1432,6 +1432,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         S.crow = crow;
         S.cread2 = c->cread2.as<uint32_t>(); S.csid2 = c->csid2.as<uint32_t>(); S.ncand2 = (uint32_t *)(ctr + C_NCAND2);
         S.err = (unsigned long long *)(ctr + C_ERR); S.nhits = (unsigned long long *)(ctr + C_HITS);
+        S.nwork = (unsigned long long *)(ctr + C_SWORK);
         S.dbg = getenv("IMSAME_DEBUG_ROUNDS") ? (unsigned long long *)(ctr + C_DBG) : nullptr;
         if (S.dbg) HIPCHK(hipMemsetAsync(S.dbg, 0, 8 * 8, s));
         S.wcap = c->use_wcap ? c->wcap.as<uint64_t>() : nullptr;
@@ -1641,6 +1642,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     HIPCHK(hipStreamSynchronize(s));
     st.ms_d2h = now_ms() - t_d2h;
     st.n_hits = hc[C_HITS];
+    st.seed_windows = hc[C_SWORK]; st.seed_entries = hc[C_SWORK + 1]; st.seed_ext_chunks = hc[C_SWORK + 2];
     st.nw_cells = hc[C_CELLS];
     st.n_accepted = hc[C_NACC];
     st.nw_redo = (uint32_t)hc[C_REDO];
@@ -1868,6 +1870,8 @@ static int align_impl(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint6
             if (x.err_read < st.err_read) { st.err_read = x.err_read; st.err_dbseq = x.err_dbseq; }
             st.ms_seed += x.ms_seed; st.ms_nw += x.ms_nw; st.nw_bytes += x.nw_bytes; st.n_rewalk += x.n_rewalk;
             st.nw_redo += x.nw_redo; st.nw_win += x.nw_win; st.nw_fallback += x.nw_fallback;
+            st.seed_windows += x.seed_windows; st.seed_entries += x.seed_entries;
+            st.seed_ext_chunks += x.seed_ext_chunks;
             st.ms_setup = std::max(st.ms_setup, x.ms_setup); st.ms_d2h += x.ms_d2h;
             iv.insert(iv.end(), L[k]->nw_iv.begin(), L[k]->nw_iv.end());
         }

@@ -50,6 +50,10 @@ struct SeedLaunch {
     uint32_t *cread2, *csid2, *ncand2;     // class 1: longer reads
     unsigned long long *err;               // min (read << 32 | record)
     unsigned long long *nhits;
+    // the scan's memory work (bench roofline of the seed stage, optional):
+    // [0] windows probed (two CSR offsets each), [1] CSR entries read, [2]
+    // 16-byte chunk pairs (database + query) loaded by ungapped extensions
+    unsigned long long *nwork = nullptr;
     unsigned long long *dbg;               // diagnostics (IMSAME_DEBUG_ROUNDS): reads per scan outcome
                                            // (seed_outcome), NULL: off
 };
@@ -101,9 +105,10 @@ __device__ __forceinline__ bool byte_eq(const Bytes16 &a, const Bytes16 &b, int 
 // byte-serial walk of the reference runs over 16-byte chunks (one round of
 // loads per chunk instead of per byte); the first chunk of each direction is
 // fetched before either walk starts.
+// (*nch, when given, counts the 16-byte chunk pairs loaded)
 __device__ __forceinline__ uint64_t ungapped_raw(const uint8_t *__restrict__ db, const uint8_t *__restrict__ q,
                                                  int64_t pd0, int64_t pq0, int64_t xs, int64_t xe, int64_t ys,
-                                                 int64_t ye, int64_t dbl, int64_t ql) {
+                                                 int64_t ye, int64_t dbl, int64_t ql, uint32_t *nch = nullptr) {
     int64_t end_x = pd0 - 1, beg_x = end_x - IMSAME_FIXED_K + 1;
     int sc = IMSAME_FIXED_K * IMSAME_POINT, best_r = sc, best_l = sc;
     uint32_t idents = IMSAME_FIXED_K;
@@ -112,6 +117,7 @@ __device__ __forceinline__ uint64_t ungapped_raw(const uint8_t *__restrict__ db,
     Bytes16 rd = load16(db, pd0), rq = load16(q, pq0);
     Bytes16 ld = rd, lq = rq;
     if (lwin) { ld = load16(db, bx0 - 15); lq = load16(q, by0 - 15); }
+    uint32_t nc = lwin ? 2 : 1;
     const int64_t fx = min(min(dbl - 1, xe), pd0 + (min(ql - 1, ye) - pq0));
     for (int64_t x = pd0, y = pq0; sc > 0 && x <= fx;) {
         const int64_t n = min((int64_t)16, fx - x + 1);
@@ -125,7 +131,7 @@ __device__ __forceinline__ uint64_t ungapped_raw(const uint8_t *__restrict__ db,
             }
         }
         x += n; y += n;
-        if (sc > 0 && x <= fx) { rd = load16(db, x); rq = load16(q, y); }
+        if (sc > 0 && x <= fx) { rd = load16(db, x); rq = load16(q, y); ++nc; }
     }
     sc = best_r;                        // left pass restarts from the right max, best_l stays 48 (:339)
     const int64_t lx = max(max((int64_t)0, xs), bx0 - (by0 - max((int64_t)0, ys)));
@@ -144,16 +150,21 @@ __device__ __forceinline__ uint64_t ungapped_raw(const uint8_t *__restrict__ db,
                 }
             }
             x -= n; y -= n;
-            if (sc > 0 && x >= lx && x >= 15 && y >= 15) { ld = load16(db, x - 15); lq = load16(q, y - 15); }
+            if (sc > 0 && x >= lx && x >= 15 && y >= 15) { ld = load16(db, x - 15); lq = load16(q, y - 15); ++nc; }
         }
     }
     for (; sc > 0 && x >= lx; --x, --y) {                 // the first 15 bytes of a buffer
         if (db[x] == q[y]) { sc += IMSAME_POINT; ++idents; } else sc -= IMSAME_POINT;
         if (best_l <= sc) { best_l = sc; beg_x = x; }
     }
+    if (nch) *nch += nc;
     const uint64_t t_len = (uint64_t)(end_x - beg_x);
     return (uint64_t)idents * IMSAME_POINT - (t_len - idents) * IMSAME_POINT;
 }
+
+// a thread's scan work: hits extended, and for the seed roofline windows
+// probed, CSR entries read, extension chunk pairs loaded
+struct SeedTally { uint64_t hits = 0, wins = 0, ents = 0; uint32_t chunks = 0; };
 
 // Chunk heads (IMSAME.c:414,430-452): read r opens its
 // chunk iff it starts where the chunk's first read from_c = i*floor(n/T)
@@ -216,7 +227,7 @@ __device__ __forceinline__ uint32_t spec_after_first(const SeedLaunch &S, uint32
     return (nm == 0 && S.spec_weak > spec && weak_hit(raw, ylen)) ? S.spec_weak : spec;
 }
 
-__device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint64_t &hits) {
+__device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, SeedTally &tl) {
     const uint64_t r = S.active[idx], k = r - S.read_from;
     const uint64_t rs = S.q_start[r], re = S.q_start[r + 1];
     const uint64_t ylen = re - rs;
@@ -264,8 +275,10 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint
             code = ((code << 2) | base2(S.q[p])) & (NBUCKETS - 1);
         }
         const uint64_t lo = S.off[code], hi = S.off[code + 1];
+        ++tl.wins;
         for (uint64_t e = lo + h; e < hi; ++e, ++h) {
             const uint2 ent = S.ent[e];
+            ++tl.ents;
             const uint32_t sid = ent.y;
             bool skip = false;
 #pragma unroll
@@ -281,9 +294,9 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, uint
             --budget;
             const int64_t xs = (int64_t)S.db_start[sid];
             const int64_t xe = (sid == S.n_db - 1) ? (int64_t)S.db_len : (int64_t)S.db_start[sid + 1] - 1;
-            ++hits;
+            ++tl.hits;
             const uint64_t raw = ungapped_raw(S.db, S.q, xs + ent.x, (int64_t)p + 1, xs, xe, ys, ye,
-                                              (int64_t)S.db_len, (int64_t)S.q_len);
+                                              (int64_t)S.db_len, (int64_t)S.q_len, &tl.chunks);
             if (mraw != ~0ull && raw >= mraw) {                      // e < min_e (:139)
                 const uint64_t xlen = S.db_start[sid + 1] - S.db_start[sid];
                 if (xlen > S.max_rs || ylen > S.max_rs) {            // terror (:155) if reached
@@ -374,7 +387,7 @@ __device__ __forceinline__ bool emit_has(const uint32_t (&em)[SM], uint32_t ne, 
 
 // SM: the most candidates a read may emit (its list in LDS, emit[] in registers)
 template <int L, int SM = SPEC_MAX>
-__device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane, uint2 *lst, uint64_t &hits) {
+__device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane, uint2 *lst, SeedTally &tl) {
     const bool gvalid = gidx < S.n_active;
     const int gbase = lane - wl;                                  // first lane of the group
     uint64_t r = 0, k = 0, rs = 0, re = 0, ylen = 0, up_to = 0, p = 0;
@@ -413,8 +426,10 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
             const uint32_t need = (ne == 0 && nm == 0 && S.spec_weak > spec ? S.spec_weak : spec) - ne;
             const uint32_t code = kmer_code_at(S.q, pw);
             const uint64_t wbase = S.off[code], hi = S.off[code + 1];
+            ++tl.wins;
             for (uint64_t e = wbase + (wl == 0 ? h : 0u); e < hi; ++e) {
                 const uint2 ent = S.ent[e];
+                ++tl.ents;
                 const uint32_t sid = ent.y;
                 bool skip = emit_has(emit, ne, sid);
                 for (uint32_t m = 0; m < nm; ++m) skip |= S.memo[k * MEMO + m] == sid;
@@ -425,7 +440,7 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
                 const int64_t xs = (int64_t)S.db_start[sid];
                 const int64_t xe = (sid == S.n_db - 1) ? (int64_t)S.db_len : (int64_t)S.db_start[sid + 1] - 1;
                 const uint64_t raw = ungapped_raw(S.db, S.q, xs + ent.x, (int64_t)pw + 1, xs, xe, ys, ye,
-                                                  (int64_t)S.db_len, (int64_t)S.q_len);
+                                                  (int64_t)S.db_len, (int64_t)S.q_len, &tl.chunks);
                 if (mraw != ~0ull && raw >= mraw) {                      // e < min_e (:139)
                     const uint64_t xlen = S.db_start[sid + 1] - S.db_start[sid];
                     const bool bad = xlen > S.max_rs || ylen > S.max_rs;   // terror (:155) if reached
@@ -437,7 +452,7 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
                 }
             }
         }
-        hits += ev;
+        tl.hits += ev;
         wv_lds_sync();                                    // lane lists written -> read by the group
         // ---- merge in window order (every lane of the group runs the same merge)
         uint32_t tot = 0;
@@ -619,6 +634,24 @@ __device__ __forceinline__ void init_one(const InitLaunch &I, uint32_t k) {
 }
 
 #ifndef IMSAME_WAVE_EMU
+// the wave's tallies summed first: one atomic per counter per wave (every
+// lane of the wave reaches this)
+__device__ __forceinline__ unsigned long long wave_sum64(unsigned long long v) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned lo = (unsigned)__shfl_xor((int)(unsigned)v, o), hi = (unsigned)__shfl_xor((int)(unsigned)(v >> 32), o);
+        v += ((unsigned long long)hi << 32) | lo;
+    }
+    return v;
+}
+__device__ __forceinline__ void seed_tally_flush(const SeedLaunch &S, const SeedTally &tl) {
+    const unsigned long long h = wave_sum64(tl.hits);
+    const bool lead = (threadIdx.x & 63) == 0;
+    if (lead && h) atomicAdd(S.nhits, h);
+    if (S.nwork) {
+        const unsigned long long w = wave_sum64(tl.wins), e = wave_sum64(tl.ents), c = wave_sum64(tl.chunks);
+        if (lead && w) { atomicAdd(S.nwork, w); atomicAdd(S.nwork + 1, e); atomicAdd(S.nwork + 2, c); }
+    }
+}
 __global__ void accept_window_kernel(const SeedLaunch S, const imsame_read_result *res, uint32_t n, uint64_t *wout) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k < n) accept_window_one(S, res, k, wout);
@@ -629,16 +662,16 @@ __global__ __launch_bounds__(256) void seed_group_kernel(SeedLaunch S) {
     const int lane = threadIdx.x & 63, wl = lane % L;
     uint2 *lst = (uint2 *)smem + threadIdx.x * SM;
     const uint32_t gidx = (blockIdx.x * blockDim.x + threadIdx.x) / L;
-    uint64_t hits = 0;
-    seed_group<L, SM>(S, gidx, wl, lane, lst, hits);
-    if (hits) atomicAdd(S.nhits, (unsigned long long)hits);
+    SeedTally tl;
+    seed_group<L, SM>(S, gidx, wl, lane, lst, tl);
+    seed_tally_flush(S, tl);
 }
 
 __global__ __launch_bounds__(256) void seed_kernel(SeedLaunch S) {
     const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
-    uint64_t hits = 0;
-    if (idx < S.n_active) seed_one(S, idx, hits);
-    if (hits) atomicAdd(S.nhits, (unsigned long long)hits);
+    SeedTally tl;
+    if (idx < S.n_active) seed_one(S, idx, tl);
+    seed_tally_flush(S, tl);
 }
 
 __global__ void update_kernel(UpdLaunch U) {

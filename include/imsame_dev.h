@@ -147,6 +147,12 @@ typedef struct imsame_stats {
     uint64_t nw_fallback;   /* packed long-read waves whose values left the
                                int16 range proof: their pairs ran the int32
                                long-read path instead (same results)      */
+    uint64_t seed_windows;  /* seed scan work (seed roofline): k-mer windows
+                               probed (two CSR offsets each), CSR entries
+                               read, 16-byte chunk pairs (database + query)
+                               loaded by ungapped extensions              */
+    uint64_t seed_entries;
+    uint64_t seed_ext_chunks;
 } imsame_stats;
 
 typedef struct imsame_ctx imsame_ctx;

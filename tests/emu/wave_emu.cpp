@@ -366,7 +366,7 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
     InitLaunch I = {qsv.data(), read_from, n, res, cur_p.data(), cur_h.data(), nmemo.data(), rstat.data(), act.data()};
     for (uint32_t k = 0; k < n; ++k) init_one(I, k);
     uint32_t nc[3] = {0, 0, 0}, pused = 0, flags = 0;
-    unsigned long long err = ~0ull, nhits = 0, cells = 0, nacc = 0;
+    unsigned long long err = ~0ull, nhits = 0, cells = 0, nacc = 0, swin = 0, sent = 0, sch = 0;
     uint32_t nact = n;
     imsame_stats st;
     memset(&st, 0, sizeof st);
@@ -399,12 +399,16 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
         auto run_seed = [&](const SeedLaunch &SL, uint32_t na) {
             const int L = RP.pick_L(rnd, na);
             if (L <= 1) {
-                for (uint32_t i = 0; i < na; ++i) { uint64_t h = 0; seed_one(SL, i, h); nhits += h; }
+                for (uint32_t i = 0; i < na; ++i) {
+                    SeedTally tl;
+                    seed_one(SL, i, tl);
+                    nhits += tl.hits; swin += tl.wins; sent += tl.ents; sch += tl.chunks;
+                }
             } else {                   // seed_group_kernel: 64-lane waves, several host threads
                 const uint64_t nwaves = ((uint64_t)na * L + 63) / 64;
                 const int nt = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)emu_threads(), nwaves));
                 std::vector<uint2> lds((size_t)nt * 64 * SPEC_BIG);
-                std::atomic<unsigned long long> wh{0};
+                std::atomic<unsigned long long> wh{0}, ww{0}, we{0}, wc{0};
                 std::atomic<uint64_t> next_wave{0};
                 std::vector<std::thread> th;
                 auto worker = [&](int t) {
@@ -412,20 +416,20 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
                         const uint64_t w0 = wv * 64;
                         uint2 *ld = lds.data() + (size_t)t * 64 * SPEC_BIG;
                         run_wave([&](int lane) {
-                            uint64_t h = 0;
+                            SeedTally h;
                             const uint32_t gidx = (uint32_t)((w0 + lane) / L);
                             if (L == 64) seed_group<64, SPEC_BIG>(SL, gidx, lane, lane, ld + lane * SPEC_BIG, h);
                             else if (L >= 16) seed_group<16>(SL, gidx, lane % 16, lane, ld + lane * SPEC_MAX, h);
                             else if (L >= 4) seed_group<4>(SL, gidx, lane % 4, lane, ld + lane * SPEC_MAX, h);
                             else         seed_group<2>(SL, gidx, lane % 2, lane, ld + lane * SPEC_MAX, h);
-                            wh += h;
+                            wh += h.hits; ww += h.wins; we += h.ents; wc += h.chunks;
                         });
                     }
                 };
                 for (int t = 1; t < nt; ++t) th.emplace_back(worker, t);
                 worker(0);
                 for (auto &x : th) x.join();
-                nhits += wh;
+                nhits += wh; swin += ww; sent += we; sch += wc;
             }
         };
         auto nw_upd = [&](uint32_t *r, uint32_t *s_, uint32_t nc_, imsame_read_result *o, uint32_t y, const int32_t *row,
@@ -472,6 +476,7 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
         std::swap(act, nxt);
     }
     st.n_reads = n; st.n_hits = nhits; st.nw_cells = cells; st.n_accepted = nacc;
+    st.seed_windows = swin; st.seed_entries = sent; st.seed_ext_chunks = sch;
     st.err_read = ~0ull;
     int ret = 0;
     if (err != ~0ull) { st.err_read = err >> 32; st.err_dbseq = err & 0xFFFFFFFFull; ret = IMSAME_E_READ_TOO_LONG; }
