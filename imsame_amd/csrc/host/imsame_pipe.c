@@ -140,10 +140,11 @@ typedef struct {
     struct wqueue *wq;
 } rtask;
 
-/* A part's single writer: the render threads hand it full pieces (one in
- * flight per thread, double-buffered), it pwrites them at their offsets.  One
- * writer takes ~21 GB/s from the page cache where 16 concurrent ones shared
- * ~13 (profiles/r4g/wrate_r4g.txt, r4m/) */
+/* A part's single writer (IMSAME_ONE_WRITER=1): the render threads hand it
+ * full pieces (one in flight per thread, double-buffered), it pwrites them at
+ * their offsets.  The write-rate micro reached ~21 GB/s from one writer with
+ * a cache-hot source (profiles/r4g/wrate_r4g.txt); with freshly rendered
+ * pieces it reached ~9.7 GB/s, below 16 writers' ~12.7 (profiles/r4n/). */
 typedef struct wqueue {
     pthread_mutex_t mu;
     pthread_cond_t cv_item, cv_free;
@@ -403,8 +404,13 @@ static int render_write_part(rtask *t, int nt, const host_seqs *db, const host_s
     wqueue w = {.mu = PTHREAD_MUTEX_INITIALIZER, .cv_item = PTHREAD_COND_INITIALIZER,
                 .cv_free = PTHREAD_COND_INITIALIZER, .producers = nt, .fd = fd};
     for (int k = 0; k < nt; ++k) { t[k].t_pw = 0; t[k].inflight = 0; t[k].wq = &w; }
+    /* every render thread pwrites its own pieces (the default: ~12.7 GB/s of
+     * the box's page cache for the 3 GB of C2), or IMSAME_ONE_WRITER=1 hands
+     * them to one writer thread (measured ~9.7 GB/s: the copies into the page
+     * cache then run on one core, profiles/r4n/) */
+    const char *ow = getenv("IMSAME_ONE_WRITER");
     pthread_t wth;
-    const int wstarted = pthread_create(&wth, NULL, writer_task, &w) == 0;
+    const int wstarted = ow && atoi(ow) && pthread_create(&wth, NULL, writer_task, &w) == 0;
     if (!wstarted)                             /* no writer thread: every render thread writes its own pieces */
         for (int k = 0; k < nt; ++k) t[k].wq = NULL;
     run_pool(t, nt, render_write_task);

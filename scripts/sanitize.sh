@@ -31,7 +31,7 @@ gcc -O1 $SAN -D_FILE_OFFSET_BITS=64 -Wall -o $B/pipe_race_asan tests/san/pipe_ra
 gcc -O1 -g -fno-omit-frame-pointer -fsanitize=thread -DRW_PIECE=4096 -D_FILE_OFFSET_BITS=64 -Wall \
     -o $B/pipe_race_tsan_small tests/san/pipe_race.c tests/san/fake_dev.c $HOST -lpthread -lm
 TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1" $B/pipe_race_tsan $B 2>&1 | tee -a "$OUT/pipe_race.log"
-TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1" $B/pipe_race_tsan_small $B 2>&1 | tee -a "$OUT/pipe_race.log"
+IMSAME_ONE_WRITER=1 TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1" $B/pipe_race_tsan_small $B 2>&1 | tee -a "$OUT/pipe_race.log"
 ASAN_OPTIONS="detect_leaks=1" UBSAN_OPTIONS="print_stacktrace=1" $B/pipe_race_asan $B 2>&1 | tee -a "$OUT/pipe_race.log"
 
 echo "== 2. CPU suite with asan+ubsan oracle, emulator, host library" | tee "$OUT/cpu_suite_asan.log"
