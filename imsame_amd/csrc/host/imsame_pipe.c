@@ -396,9 +396,15 @@ static int render_write_part(rtask *t, int nt, const host_seqs *db, const host_s
         *off += t[k].bytes;
     }
     r->bytes_out = *off;
-    if (getenv("IMSAME_FALLOCATE") && nt) {   /* experiment: the part's blocks allocated before its writes */
+    /* the part's blocks allocated before its writes, so the threads' pwrites
+     * only copy (C2 on the box's overlay fs: render tail 0.24 -> 0.19 s and
+     * 0.33 -> 0.29 s in two A/B pairs, profiles/r4n, r4o).  fallocate(2), not
+     * posix_fallocate: where the filesystem lacks it this is a no-op instead
+     * of glibc's byte-per-block emulation.  IMSAME_FALLOCATE=0 turns it off. */
+    const char *fa = getenv("IMSAME_FALLOCATE");
+    if ((!fa || atoi(fa)) && nt) {
         const uint64_t a = t[0].off;
-        if (*off > a) (void)posix_fallocate(fd, (off_t)a, (off_t)(*off - a));
+        if (*off > a) (void)fallocate(fd, 0, (off_t)a, (off_t)(*off - a));
     }
     const double t1 = pipe_now();
     wqueue w = {.mu = PTHREAD_MUTEX_INITIALIZER, .cv_item = PTHREAD_COND_INITIALIZER,
