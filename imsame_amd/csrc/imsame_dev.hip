@@ -1810,7 +1810,16 @@ static int align_impl(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint6
     for (int k = 0; k < nl; ++k) L[k]->nlanes = nl;
 
 
-    std::vector<uint64_t> cut(nl + 1), used(nl, 0);
+    // PIECES (callback calls only): each lane's share is cut into `ns`
+    // pieces, piece i on lane i % nl, so the first nl pieces -- a prefix of
+    // the range -- are handed over while the lanes align the rest, and the
+    // caller's output of that prefix overlaps the device (IMSAME_LANE_PARTS;
+    // 1: one piece per lane)
+    const char *lpe = getenv("IMSAME_LANE_PARTS");
+    int ns = (fn && lpe) ? std::max(1, std::min(16, atoi(lpe))) : 1;
+    while (ns > 1 && n < (uint64_t)(nl * ns) * lane_min) --ns;
+    const int np = nl * ns;
+    std::vector<uint64_t> cut(np + 1), used(np, 0);
     // lane k's share grows linearly, weight 1 + x (2k/(nl-1) - 1): equal lanes
     // reach their latency-bound phases (update, next seed scan) at the same
     // moment and leave the chip idle together; x = 0.4 for 8 lanes (C2: +0.7 %
@@ -1818,23 +1827,27 @@ static int align_impl(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint6
     const char *ske = getenv("IMSAME_LANE_SKEW");
     const double skew = ske ? std::max(0.0, std::min(0.9, atof(ske))) : (nl >= 8 ? 0.4 : 0.0);
     {
-        std::vector<double> w(nl), acc(nl + 1, 0.0);
-        for (int k = 0; k < nl; ++k) w[k] = 1.0 + skew * (nl > 1 ? 2.0 * k / (nl - 1) - 1.0 : 0.0);
-        for (int k = 0; k < nl; ++k) acc[k + 1] = acc[k] + w[k];
-        for (int k = 0; k <= nl; ++k) cut[k] = read_from + (uint64_t)((double)n * acc[k] / acc[nl]);
-        cut[0] = read_from; cut[nl] = read_to;
+        std::vector<double> w(np), acc(np + 1, 0.0);
+        for (int i = 0; i < np; ++i) w[i] = 1.0 + skew * (nl > 1 ? 2.0 * (i % nl) / (nl - 1) - 1.0 : 0.0);
+        for (int i = 0; i < np; ++i) acc[i + 1] = acc[i] + w[i];
+        for (int i = 0; i <= np; ++i) cut[i] = read_from + (uint64_t)((double)n * acc[i] / acc[np]);
+        cut[0] = read_from; cut[np] = read_to;
     }
-    std::vector<imsame_stats> S(nl);
-    std::vector<int> R(nl, 0);
+    std::vector<imsame_stats> S(np);
+    std::vector<int> R(np, 0);
     std::vector<std::thread> th;
     // each lane runs on its own host thread (lane 0 on the caller's) and,
-    // with a callback, hands over its reads as soon as they are final
+    // with a callback, hands over each piece as soon as its reads are final;
+    // a hard error ends the lane (the caller stops on it)
     auto lane_run = [&](int k) {
-        R[k] = align_one(L[k], cut[k], cut[k + 1], n_threads_semantic, p, res + (cut[k] - read_from), nullptr, 0,
-                         &used[k], &S[k]);
-        if (fn) {
-            const int rd = deliver_part(L[k], p, cut[k], cut[k + 1], R[k], used[k], S[k].err_read, fn, user);
-            if (rd) R[k] = rd;
+        for (int i = k; i < np; i += nl) {
+            R[i] = align_one(L[k], cut[i], cut[i + 1], n_threads_semantic, p, res + (cut[i] - read_from), nullptr, 0,
+                             &used[i], &S[i]);
+            if (fn) {
+                const int rd = deliver_part(L[k], p, cut[i], cut[i + 1], R[i], used[i], S[i].err_read, fn, user);
+                if (rd) R[i] = rd;
+            }
+            if (R[i] && R[i] != IMSAME_E_PATHS && R[i] != IMSAME_E_READ_TOO_LONG) break;
         }
     };
     for (int k = 1; k < nl; ++k) th.emplace_back(lane_run, k);
@@ -1849,9 +1862,10 @@ static int align_impl(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint6
     for (int r : R)
         if (r == IMSAME_E_READ_TOO_LONG) ret = IMSAME_E_READ_TOO_LONG;
     // one result set: each lane's paths follow the previous lanes' (parts:
-    // each part's rows index its own paths, handed over in the callback)
+    // each part's rows index its own paths, handed over in the callback;
+    // without a callback a lane runs one piece, np == nl)
     uint64_t base = 0;
-    for (int k = 0; k < nl; ++k) {
+    for (int k = 0; k < np; ++k) {
         if (p->want_paths && k && !fn)
             for (uint64_t r = cut[k]; r < cut[k + 1]; ++r) {
                 imsame_read_result &x = res[r - read_from];
@@ -1861,8 +1875,9 @@ static int align_impl(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint6
     }
     imsame_stats st = S[0];
     std::vector<std::pair<float, float>> iv = c->nw_iv;
+    for (int k = 1; k < nl; ++k) iv.insert(iv.end(), L[k]->nw_iv.begin(), L[k]->nw_iv.end());
     st.nw_launches = 0; st.launch_pk = 0; st.launch_k5 = 0; st.launch_np = 0; st.launch_k19 = 0; st.launch_nwp = 0;
-    for (int k = 0; k < nl; ++k) {
+    for (int k = 0; k < np; ++k) {
         const imsame_stats &x = S[k];
         if (k) {
             st.n_reads += x.n_reads; st.n_accepted += x.n_accepted; st.n_nw += x.n_nw; st.nw_cells += x.nw_cells;
@@ -1873,7 +1888,6 @@ static int align_impl(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint6
             st.seed_windows += x.seed_windows; st.seed_entries += x.seed_entries;
             st.seed_ext_chunks += x.seed_ext_chunks;
             st.ms_setup = std::max(st.ms_setup, x.ms_setup); st.ms_d2h += x.ms_d2h;
-            iv.insert(iv.end(), L[k]->nw_iv.begin(), L[k]->nw_iv.end());
         }
         for (uint64_t j = 0; j < std::min<uint64_t>(x.nw_launches, IMSAME_LAUNCH_STATS); ++j) {
             if (st.nw_launches + j >= IMSAME_LAUNCH_STATS) break;
@@ -1892,6 +1906,9 @@ static int align_impl(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint6
     st.lanes = (uint64_t)nl;
     c->paths_split = true; c->paths_n = used[0]; c->paths_on_host = false;
     c->lane_paths.assign(used.begin() + 1, used.end());
+    if (np != nl) {                    // pieces: the lanes' buffers hold only their last piece's paths
+        c->paths_split = false; c->paths_n = 0; c->lane_paths.clear();
+    }
     if (paths_used) *paths_used = base;
     if (p->want_paths && base && !fn) {
         if (base > paths_cap || !paths) { if (ret == IMSAME_OK) ret = IMSAME_E_PATHS; }

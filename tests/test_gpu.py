@@ -713,8 +713,9 @@ def test_cli_devices_matches_reference_golden(name):
 
 def test_cli_multi_device_output_identical(tmp_path):
     """C2 shape (2 Mbp, 12k reads) through the CLI: one context vs three
-    (-devices 0,0,0) with batches of 1000 reads, one render thread, and 4
-    lanes handing over their parts out of order -- identical .align bytes."""
+    (-devices 0,0,0) with batches of 1000 reads, one render thread, 4
+    lanes handing over their parts out of order, and 3 lanes of 2 pieces each
+    -- identical .align bytes."""
     ref, rst = synth.make_reference_arr(2_000_000, 2_000, seed=42)
     q, qs = synth.make_reads_arr(ref, 12_000, 150, seed=43)
     dbf, qf = str(tmp_path / "db.fa"), str(tmp_path / "q.fa")
@@ -722,14 +723,15 @@ def test_cli_multi_device_output_identical(tmp_path):
     synth.write_fasta(qf, q, qs, "read", width=0)
     outs = []
     for extra, env in (([], {}), (["-devices", "0,0,0", "-batch_reads", "1000"], {}), (["-render_threads", "1"], {}),
-                       ([], {"IMSAME_LANES": "4", "IMSAME_LANE_MIN": "1000"})):
+                       ([], {"IMSAME_LANES": "4", "IMSAME_LANE_MIN": "1000"}),
+                       ([], {"IMSAME_LANES": "3", "IMSAME_LANE_PARTS": "2", "IMSAME_LANE_MIN": "1000"})):
         o = str(tmp_path / f"o{len(outs)}.align")
         p = subprocess.run([CLI, "-query", qf, "-db", dbf, "-out", o, "-n_threads", "16", *extra],
                            stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=300, env=dict(os.environ, **env))
         assert p.returncode == 0, p.stderr[-2000:]
         assert b'"accepted"' in p.stderr
         outs.append(open(o, "rb").read())
-    assert outs[0] == outs[1] == outs[2] == outs[3]
+    assert all(o == outs[0] for o in outs[1:])
     assert outs[0].count(b" $$$$$$$ \n") > 10_000
 
 
@@ -787,10 +789,13 @@ def test_align_parts_hand_over_every_lane(dev, monkeypatch):
     dev.index(ref, rst)
     dev.set_query(q, qs)
     whole, pw, _ = dev.align(n_threads=7, want_paths=True)
-    for lanes in ("1", "4"):
+    monkeypatch.setenv("IMSAME_LANE_MIN", "1000")
+    for lanes, pieces in (("1", "1"), ("4", "1"), ("3", "3")):
         monkeypatch.setenv("IMSAME_LANES", lanes)
+        monkeypatch.setenv("IMSAME_LANE_PARTS", pieces)       # pieces per lane, handed over in turn
         res, parts, st = dev.align_parts(n_threads=7, want_paths=True)
-        assert st.lanes == int(lanes) and len(parts) == int(lanes)
+        assert st.lanes == int(lanes) and len(parts) == int(lanes) * int(pieces)
+        assert st.n_reads == len(qs)
         cov = sorted((a, b) for a, b, *_ in parts)
         assert cov[0][0] == 0 and cov[-1][1] == len(qs) and all(x[1] == y[0] for x, y in zip(cov, cov[1:]))
         assert all(s == 0 and e == 2 ** 64 - 1 for _, _, s, e, _ in parts)
