@@ -271,6 +271,7 @@ struct imsame_ctx {
     int device = 0, ncu = 0;
     hipStream_t stream = nullptr;
     hipStream_t ustream = nullptr;    // query uploads (imsame_dev_set_query_range_async)
+    bool ustream_own = false;         // ... a stream of its own, or the last lane's
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     // round 1b (align_one): a second stream and event pair, created on first use
     hipStream_t stream_b = nullptr;
@@ -517,9 +518,18 @@ extern "C" int imsame_dev_open(int device, imsame_ctx **out) {
     // shares the least used one.  So the compute streams of this context and
     // its lanes come first, one queue each, and the upload stream last, on the
     // last lane's queue (that lane starts after the whole upload anyway).
-    for (int k = 1; k < std::min(lanes_for_queues(), LANES_DEF) && !rc; ++k) rc = lane_add(c);
+    const int nl = std::min(lanes_for_queues(), LANES_DEF);
+    for (int k = 1; k < nl && !rc; ++k) rc = lane_add(c);
     const double t3 = dbg ? now_ms() : 0;
-    if (!rc && hipStreamCreateWithFlags(&c->ustream, hipStreamNonBlocking) != hipSuccess) rc = IMSAME_E_HIP;
+    // the query upload runs on the last lane's compute stream (that lane's
+    // rounds wait for the upload's last part anyway): each stream with a
+    // hardware queue of its own costs ~19 ms of the open (IMSAME_DEBUG_OPEN,
+    // profiles/r4r/; creating them on parallel threads gains nothing, the
+    // runtime serialises it); a context without lanes has a stream of its own
+    // for it, so its rounds overlap the upload
+    if (!rc && !c->subs.empty()) c->ustream = c->subs.back()->stream;
+    else if (!rc && hipStreamCreateWithFlags(&c->ustream, hipStreamNonBlocking) == hipSuccess) c->ustream_own = true;
+    else if (!rc) rc = IMSAME_E_HIP;
     // round 1b's streams (align_one) after the lanes' compute streams: they
     // share the hardware queues the runtime has left (created here, not in a
     // call: creating one while other lanes run stalled a CLI call for 4.8 s,
@@ -546,11 +556,13 @@ static void lane_unalias(imsame_ctx *l) {
 
 extern "C" void imsame_dev_close(imsame_ctx *c) {
     if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->ustream) (void)hipStreamSynchronize(c->ustream);    // before the lane that may own it goes
+    if (!c->ustream_own) c->ustream = nullptr;
     for (imsame_ctx *l : c->subs) { lane_unalias(l); imsame_dev_close(l); }
     c->subs.clear();
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    if (c->ustream) (void)hipStreamSynchronize(c->ustream);
     DBuf *bufs[] = {&c->db, &c->db_start, &c->off, &c->ent, &c->brk, &c->codes, &c->fill, &c->big, &c->q,
                     &c->q_start, &c->res, &c->cur_p, &c->cur_h, &c->memo, &c->nmemo, &c->rstat, &c->act0,
                     &c->act1, &c->cread, &c->csid, &c->cread2, &c->csid2, &c->cout, &c->cout2, &c->ctr,
@@ -568,7 +580,7 @@ extern "C" void imsame_dev_close(imsame_ctx *c) {
         for (hipEvent_t e : c->q_part_ev) (void)hipEventDestroy(e);
     if (!c->is_sub && c->h_q_start) (void)hipHostFree(c->h_q_start);
     if (c->stream) (void)hipStreamDestroy(c->stream);
-    if (c->ustream) (void)hipStreamDestroy(c->ustream);
+    if (c->ustream && c->ustream_own) (void)hipStreamDestroy(c->ustream);
     delete c;
 }
 
@@ -1813,10 +1825,13 @@ static int align_impl(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint6
     // PIECES (callback calls only): each lane's share is cut into `ns`
     // pieces, piece i on lane i % nl, so the first nl pieces -- a prefix of
     // the range -- are handed over while the lanes align the rest, and the
-    // caller's output of that prefix overlaps the device (IMSAME_LANE_PARTS;
-    // 1: one piece per lane)
+    // caller's output of that prefix overlaps the device.  3 pieces: the CLI
+    // at C2 writes its 3 GB with a render tail of 0.125-0.132 s instead of
+    // 0.18-0.19 s, the alignment 0.122-0.123 -> 0.132-0.135 s, process wall
+    // 0.70-0.77 -> 0.70-0.72 s (2 pieces: tail 0.140 s; profiles/r4p/, r4q/).
+    // IMSAME_LANE_PARTS overrides (1: one piece per lane).
     const char *lpe = getenv("IMSAME_LANE_PARTS");
-    int ns = (fn && lpe) ? std::max(1, std::min(16, atoi(lpe))) : 1;
+    int ns = !fn ? 1 : lpe ? std::max(1, std::min(16, atoi(lpe))) : 3;
     while (ns > 1 && n < (uint64_t)(nl * ns) * lane_min) --ns;
     const int np = nl * ns;
     std::vector<uint64_t> cut(np + 1), used(np, 0);
