@@ -585,10 +585,11 @@ def run_e2e(ref, rst, q, qs, a):
         free = shutil.disk_usage(td).free
         need = 4 * 1024 ** 3                         # ~3.3 KB of text per accepted read at C2
         out = outf if free > need else "/dev/null"
-        t0 = time.monotonic()
         extra = os.environ.get("IMSAME_E2E_ARGS", "").split()          # experiments, e.g. -batch_reads N
+        env = dict(os.environ, IMSAME_T_LAUNCH="%.6f" % time.time())   # the CLI reports main entry / exit from it
+        t0 = time.monotonic()
         p = subprocess.run([cli, "-query", qf, "-db", dbf, "-out", out, "-n_threads", str(a.n_threads)] + extra,
-                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=900)
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=900, env=env)
         wall = time.monotonic() - t0
         if os.environ.get("IMSAME_E2E_LOG"):                            # diagnostics: the CLI's stderr
             with open(os.path.join(REPO, "gpurun_out", os.environ["IMSAME_E2E_LOG"]), "wb") as f:
@@ -601,6 +602,8 @@ def run_e2e(ref, rst, q, qs, a):
         if tm:
             ph.update(json.loads(tm.group(1)))
         ph = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in ph.items()}
+        if ph.get("exit_at_s", -1) >= 0:                # process start before main / exit after the last line
+            ph["after_exit_s"] = round(wall - ph["exit_at_s"], 4)
         ph.update({"process_wall_s": round(wall, 3), "output": "file" if out == outf else "/dev/null (disk full)",
                    "output_fs": mount_fs(td), "cli_args": extra,
                    "reads_per_s_e2e": round(len(qs) / wall, 1),

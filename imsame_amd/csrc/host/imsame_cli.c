@@ -36,6 +36,15 @@ static double now_s(void) {
     clock_gettime(CLOCK_MONOTONIC, &ts);
     return ts.tv_sec + ts.tv_nsec * 1e-9;
 }
+/* diagnostics: seconds since the wall-clock instant IMSAME_T_LAUNCH (set by
+ * bench.py just before it starts the process), -1 without it */
+static double since_launch(void) {
+    const char *e = getenv("IMSAME_T_LAUNCH");
+    if (!e) return -1;
+    struct timespec ts;
+    clock_gettime(CLOCK_REALTIME, &ts);
+    return ts.tv_sec + ts.tv_nsec * 1e-9 - atof(e);
+}
 
 /* terror(), commonFunctions.c:10-13 */
 static void terror(const char *s) {
@@ -77,6 +86,7 @@ static void usage(void) {
 }
 
 int main(int argc, char **argv) {
+    const double t_main = since_launch();
     /* one hardware queue per alignment lane (include/imsame_dev.h: the library
      * runs at most one lane per queue and never sets this itself); a value in
      * the environment is kept.  Before the first HIP call. */
@@ -234,7 +244,8 @@ int main(int argc, char **argv) {
      * IMSAME_CLEAN_EXIT=1 tears everything down (leak checks). */
     const char *ce = getenv("IMSAME_CLEAN_EXIT"), *fe = getenv("IMSAME_FAST_EXIT");
     if (!(ce && atoi(ce)) && !(fe && !atoi(fe))) {
-        fprintf(stderr, "[imsame] teardown {\"close_s\": 0, \"fast_exit\": 1}\n");
+        fprintf(stderr, "[imsame] teardown {\"close_s\": 0, \"fast_exit\": 1, \"main_at_s\": %.4f, \"exit_at_s\": %.4f}\n",
+                t_main, since_launch());
         fflush(stderr);
         _exit(0);
     }
