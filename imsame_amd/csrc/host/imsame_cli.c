@@ -253,6 +253,7 @@ int main(int argc, char **argv) {
     host_free_seqs(&db);
     host_free_seqs(&q);
     pipe_close(dv, G);
-    fprintf(stderr, "[imsame] teardown {\"close_s\": %.4f}\n", now_s() - t_close);
+    fprintf(stderr, "[imsame] teardown {\"close_s\": %.4f, \"main_at_s\": %.4f, \"exit_at_s\": %.4f}\n",
+            now_s() - t_close, t_main, since_launch());
     return 0;
 }
