@@ -39,6 +39,7 @@ if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
+from imsame_amd.dist import host_threads_per_rank  # noqa: E402  (numpy only: no torch, no HIP)
 
 METRIC = "reads aligned/sec (node), 1M×150bp vs 50Mbp ref, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md, chip-level parameters
@@ -156,6 +157,9 @@ def parse():
                          "N-rank run (RCCL all-reduce of the clock and counters) execute next to the library's streams")
     ap.add_argument("--device", type=int, default=None,
                     help="HIP device of this rank (default LOCAL_RANK; a fixed value rehearses N ranks on one card)")
+    ap.add_argument("--device-count-override", type=int, default=None, metavar="N",
+                    help="rehearsal: the --gpus launcher takes N GPUs as visible (counted without HIP it sees "
+                         "fewer) and rank r uses device LOCAL_RANK mod the real count")
     ap.add_argument("--shard", default=None, metavar="R/N",
                     help="diagnostic: on one GPU, time only rank R's shard of an N-GPU strong-scaling run")
     ap.add_argument("--upload", choices=("async", "sync"), default="async",
@@ -202,15 +206,6 @@ def host_cpu():
     return {"model": model, "nproc": nproc, "affinity": aff, "cgroup_quota_cpus": quota, "usable": usable}
 
 
-def visible_gpus():
-    """GPUs this process may use, counted WITHOUT initialising HIP (the rank
-    launcher forks children afterwards): torch.cuda.device_count() does not
-    start the runtime on this image (it reads the KFD topology), and it
-    honours HIP/ROCR/CUDA_VISIBLE_DEVICES."""
-    import torch
-    return torch.cuda.device_count()
-
-
 def launch_ranks(a):
     """`--gpus N` without a launcher: start N rank processes of this script,
     one per GPU -- the fan-out IMSAME does with pthread_create over read
@@ -223,10 +218,14 @@ def launch_ranks(a):
     import signal
     import socket
     import subprocess
+    from imsame_amd.dist import visible_gpus           # KFD topology + *_VISIBLE_DEVICES: no torch, no HIP
+    n_real = visible_gpus()
     if a.device is None:
-        n = visible_gpus()
+        n = a.device_count_override if a.device_count_override is not None else n_real
         if a.gpus > n:
             sys.exit(f"bench.py: --gpus {a.gpus} but {n} GPU(s) visible (--device D rehearses N ranks on one card)")
+        if a.device_count_override is not None and n_real < 1:
+            sys.exit("bench.py: --device-count-override needs at least one visible GPU")
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -235,7 +234,7 @@ def launch_ranks(a):
     for r in range(a.gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus),
                    LOCAL_WORLD_SIZE=str(a.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
-                   IMSAME_BENCH_LAUNCHED="1")
+                   IMSAME_BENCH_LAUNCHED="1", IMSAME_BENCH_VISIBLE=str(n_real))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
     rc = 0
     try:
@@ -270,6 +269,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     gpu = local if a.device is None else a.device
+    if a.device is None and a.device_count_override is not None:       # rehearsal: ranks share the real cards
+        gpu = local % max(1, int(os.environ.get("IMSAME_BENCH_VISIBLE", "1")))
+    # host threads of this rank: an equal share of the job's usable CPUs
+    # (upload host pass, imsame_dev.hip:host_threads_cap); set before the
+    # library is loaded (it reads the variable once)
+    hc = host_cpu()
+    threads = host_threads_per_rank(hc["usable"], world)
+    os.environ.setdefault("IMSAME_HOST_THREADS", str(threads))
     backend = None
     if world > 1 or a.dist:
         import torch
@@ -468,6 +475,11 @@ def main():
             "cpu_baseline": cpu,
             "e2e": e2e,
             "ranks": {"world": world, "backend": ("rccl" if backend == "nccl" else backend),
+                      "device": gpu, "host_cpus_usable": hc["usable"],
+                      "host_threads_per_rank": int(os.environ["IMSAME_HOST_THREADS"]),
+                      "lane_wait": os.environ.get("IMSAME_WAIT", "yield"),
+                      "launcher_visible_gpus": (int(os.environ["IMSAME_BENCH_VISIBLE"])
+                                                if "IMSAME_BENCH_VISIBLE" in os.environ else None),
                       "launcher": "bench.py" if os.environ.get("IMSAME_BENCH_LAUNCHED") else
                                   ("torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ or world > 1
                                    else None),
@@ -485,6 +497,7 @@ def main():
                        "ms_nw_last_end": round(last["ms_nw_last"], 3),
                        "ms_align_call": round(last["ms_total"], 3),
                        "ms_host_setup": round(last["ms_setup"], 3), "ms_d2h_results": round(last["ms_d2h"], 3),
+                       "nw_accounting": nw_accounting(last, hi - lo, parity),
                        "nw_launch_cand": last["launch_cand"],
                        "nw_launch_ms": [round(x, 3) for x in last["launch_ms"]]},
         }
@@ -494,6 +507,28 @@ def main():
     rpin.free()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def nw_accounting(st, n_reads, parity):
+    """The device's NW work against the reference's (alignmentFunctions.c:
+    126-186 runs one NW per e-value-passing hit, in visiting order, until one
+    is accepted).  Device: n_nw = the distinct (read, record) pairs up to each
+    read's accepted one -- the reference's work without its repeats of an
+    already rejected record -- plus `spec_extra`, the candidates a read
+    emitted past its accepted one (speculation, round_policy.h), counted by
+    update_kernel.  Oracle on the parity windows (when the checker ran): the
+    same distinct count, and the reference's own count with the repeats."""
+    n = max(n_reads, 1)
+    waste = st.get("nw_spec_waste", 0)
+    out = {"nw_per_read": round(st["n_nw"] / n, 4), "spec_extra_per_read": round(waste / n, 4),
+           "needed_per_read": round((st["n_nw"] - waste) / n, 4),
+           "spec_extra_frac": round(waste / max(st["n_nw"], 1), 4)}
+    if parity and parity.get("oracle_nw_distinct") is not None:
+        m = max(parity["reads_compared"], 1)
+        out["windows_oracle_distinct_per_read"] = round(parity["oracle_nw_distinct"] / m, 4)
+        if parity.get("oracle_nw_reference") is not None:
+            out["nw_ref_per_read"] = round(parity["oracle_nw_reference"] / m, 4)
+    return out
 
 
 def seed_roofline(st, n_reads, read_len):
@@ -625,7 +660,8 @@ def timed_parity(ref, rst, q, qs, res, lo, hi, a, params):
     o = Oracle.load()
     po = o.params(max_read_size=params.max_read_size)
     t0 = time.time()
-    out = P.check_windows(o, ref, rst, q, qs, res, lo, P.windows(lo, hi, len(qs), a.n_threads), a.n_threads, po)
+    out = P.check_windows(o, ref, rst, q, qs, res, lo, P.windows(lo, hi, len(qs), a.n_threads), a.n_threads, po,
+                          count_ref=True)
     out["oracle_s"] = round(time.time() - t0, 2)
     out["rows_of"] = "the last timed step"
     return out

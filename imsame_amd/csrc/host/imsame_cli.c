@@ -18,6 +18,7 @@
  * to stderr.
  */
 #define _GNU_SOURCE
+#include <errno.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -50,6 +51,16 @@ static double since_launch(void) {
 static void terror(const char *s) {
     printf("ERR**** %s ****\n", s);
     exit(-1);
+}
+
+/* The output could not be written: the parts are written in parallel into
+ * ranges allocated ahead (fallocate), so a failed run would leave zero-filled
+ * holes after the last complete part -- cut the file back to the bytes known
+ * complete (a prefix of whole records), then fail as the reference does. */
+static void out_failed(int fd, uint64_t bytes_ok) {
+    if (ftruncate(fd, (off_t)bytes_ok) != 0 && errno != EINVAL && errno != ESPIPE)
+        fprintf(stderr, "[imsame] could not cut the output back: %s\n", strerror(errno));
+    terror("Could not write the output file");
 }
 
 /* device contexts, opened on a thread of their own (overlapping the parse) */
@@ -207,7 +218,7 @@ int main(int argc, char **argv) {
         const double tr = now_s();
         uint64_t off = 0;
         if (out_fd >= 0 && pipe_render_range(&db, &q, res, paths, 0, q.n, out_fd, render_threads, &off, &pr))
-            terror("Could not write the output file");
+            out_failed(out_fd, pr.bytes_ok);
         pr.t_tail = now_s() - tr;
         pr.stop = q.n;
         for (uint64_t r = 0; r < q.n; r++) pr.accepted += res[r].status == 1;
@@ -217,9 +228,10 @@ int main(int argc, char **argv) {
         pipe_opts po = {.T = T, .prm = prm, .out_fd = out_fd, .render_threads = render_threads,
                         .batch_reads = batch_reads};
         rc = pipe_align_render(dv, G, &db, &q, &po, &pr);
+        if (pr.write_errno && out_fd >= 0) out_failed(out_fd, pr.bytes_ok);
         if (rc && rc != IMSAME_E_READ_TOO_LONG) terror(imsame_strerror(rc));
     }
-    if (out_fd >= 0) close(out_fd);
+    if (out_fd >= 0 && close(out_fd) != 0) terror("Could not write the output file");
     if (rc == IMSAME_E_READ_TOO_LONG) terror("Read size reached for gapped alignment.");
     const uint64_t acc = pr.accepted;
     printf("[INFO] Alignments computed in %e seconds.\n", now_s() - t0);
@@ -228,15 +240,18 @@ int main(int argc, char **argv) {
            acc, q.n, db.n, prm.min_e, (int)(100 * prm.min_coverage));
     printf("[INFO] The Jaccard-index is: %Le\n", (long double)acc / ((db.n + q.n) - acc));
     printf("[INFO] Deallocating heap memory.\n");
-    fflush(stdout);
+    if (fflush(stdout) != 0 || ferror(stdout)) {       /* a late error on stdout is an error */
+        fprintf(stderr, "[imsame] error writing stdout\n");
+        _exit(1);
+    }
     fprintf(stderr, "[imsame] rounds=%" PRIu64 " nw=%" PRIu64 " cells=%" PRIu64 " seed_ms=%.3f nw_ms=%.3f total_ms=%.3f\n",
             pr.st.rounds, pr.st.n_nw, pr.st.nw_cells, pr.st.ms_seed, pr.st.ms_nw, pr.st.ms_total);
     fprintf(stderr, "[imsame] phases {\"devices\": %d, \"parts\": %" PRIu64 ", \"open_s\": %.4f, \"parse_db_s\": %.4f, \"index_s\": %.4f, "
             "\"parse_query_s\": %.4f, \"upload_s\": %.4f, \"align_s\": %.4f, \"render_busy_s\": %.4f, "
-            "\"write_busy_s\": %.4f, \"render_tail_s\": %.4f, \"pwrite_sum_s\": %.4f, \"pwrite_max_s\": %.4f, "
+            "\"write_busy_s\": %.4f, \"render_tail_s\": %.4f, \"pwrite_sum_s\": %.4f, \"pwrite_max_s\": %.4f, \"writer_wait_max_s\": %.4f, "
             "\"bytes_out\": %" PRIu64 ", \"accepted\": %" PRIu64 ", \"wall_s\": %.4f}\n",
             G, pr.batches, oj.secs, t_parse_db, t_index, t_parse_q, t_upload, pr.t_align, pr.t_render, pr.t_write, pr.t_tail,
-            pr.t_pwrite_sum, pr.t_pwrite_max, pr.bytes_out, acc, now_s() - t_wall);
+            pr.t_pwrite_sum, pr.t_pwrite_max, pr.t_wait_max, pr.bytes_out, acc, now_s() - t_wall);
     /* The device contexts and the heap are left to process exit (the output
      * is closed and stdout flushed; the kernel driver releases the GPU
      * memory): hipFree of the arenas and the runtime's exit handlers cost

@@ -423,9 +423,17 @@ static int render_write_part(rtask *t, int nt, const host_seqs *db, const host_s
     if (wstarted) pthread_join(wth, NULL);
     r->t_render += t1 - t0;                /* sizing */
     r->t_write += pipe_now() - t1;         /* render + write, overlapped */
-    r->t_pwrite_sum += w.t_busy;           /* diagnostics: the writer's pwrite seconds, */
-    for (int k = 0; k < nt; ++k)           /* and the longest a render thread waited for it */
-        if (t[k].t_pw > r->t_pwrite_max) r->t_pwrite_max = t[k].t_pw;
+    if (wstarted) {                        /* diagnostics: the writer's pwrite seconds, and the */
+        r->t_pwrite_sum += w.t_busy;       /* longest a render thread waited for it */
+        if (w.t_busy > r->t_pwrite_max) r->t_pwrite_max = w.t_busy;
+        for (int k = 0; k < nt; ++k)
+            if (t[k].t_pw > r->t_wait_max) r->t_wait_max = t[k].t_pw;
+    } else {                               /* every render thread's own pwrite seconds */
+        for (int k = 0; k < nt; ++k) {
+            r->t_pwrite_sum += t[k].t_pw;
+            if (t[k].t_pw > r->t_pwrite_max) r->t_pwrite_max = t[k].t_pw;
+        }
+    }
     for (int k = 0; k < nt; ++k)
         if (t[k].err) return t[k].err;
     return 0;
@@ -481,8 +489,13 @@ int pipe_render_range(const host_seqs *db, const host_seqs *q, const imsame_read
     rtask *t = calloc((size_t)nt, sizeof *t);
     if (!t) return ENOMEM;
     const int seekable = lseek(fd, 0, SEEK_CUR) >= 0;
+    const uint64_t start = *off;
     const int err = seekable ? render_write_part(t, nt, db, q, res, paths, from, to, fd, off, r)
                              : render_batch(t, nt, db, q, res, paths, from, to, fd, seekable, off, r);
+    if (r) {                                       /* bytes known complete, for a caller that must cut */
+        r->bytes_ok = err ? start : *off;          /* a failed file back to them */
+        if (err && !r->write_errno) r->write_errno = err;
+    }
     for (int k = 0; k < nt; ++k) { free(t[k].text.buf); free(t[k].spare.buf); free(t[k].scratch.buf); }
     free(t);
     return err;
@@ -648,6 +661,7 @@ int pipe_align_render(pipe_dev *d, int G, const host_seqs *db, const host_seqs *
         if (rt && !werr && !rc && hi > pt->from && seekable) {
             /* a file: offsets from the rows, every thread renders and writes */
             werr = render_write_part(rt, nt, db, q, res, pt->paths, pt->from, hi, o->out_fd, &off, r);
+            if (!werr) r->bytes_ok = off;                   /* this part is complete in the file */
         } else if (rt && !werr && !rc && hi > pt->from) {
             /* a pipe: ordered writes.  Set nrend & 1 was last written two
              * parts ago: that writer is joined */
@@ -691,7 +705,11 @@ int pipe_align_render(pipe_dev *d, int G, const host_seqs *db, const host_seqs *
         free(rt);
     }
     free(res);
-    if (werr) { fprintf(stderr, "[imsame] write error: %s\n", strerror(werr)); if (!rc) rc = IMSAME_E_ARG; }
+    if (werr) {
+        fprintf(stderr, "[imsame] write error: %s\n", strerror(werr));
+        r->write_errno = werr;
+        if (!rc) rc = IMSAME_E_ARG;
+    }
     r->rc = rc;
     return rc;
 }

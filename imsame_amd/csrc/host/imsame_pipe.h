@@ -42,7 +42,10 @@ typedef struct {
     double t_render;             /* render threads' busy wall, summed per part */
     double t_write;              /* pwrite wall, summed per part             */
     double t_tail;               /* last part delivered -> output complete   */
-    double t_pwrite_sum, t_pwrite_max;   /* render threads' pwrite seconds: summed, one thread's most */
+    double t_pwrite_sum, t_pwrite_max;   /* seconds in pwrite: summed over threads, one thread's most */
+    double t_wait_max;           /* IMSAME_ONE_WRITER: longest a render thread waited for the writer */
+    uint64_t bytes_ok;           /* a file: bytes [0, bytes_ok) are complete (parts fully written) */
+    int write_errno;             /* the first output write error (0: none)   */
 } pipe_result;
 
 /* parse "-devices" values: "N" (devices 0..N-1) or "d0,d1,..." */

@@ -18,6 +18,7 @@
 #include <math.h>
 #include <limits.h>
 #include <time.h>
+#include <sched.h>
 #include <vector>
 #include <algorithm>
 #include <thread>
@@ -276,6 +277,9 @@ struct imsame_ctx {
     // round 1b (align_one): a second stream and event pair, created on first use
     hipStream_t stream_b = nullptr;
     hipEvent_t evb0 = nullptr, evb1 = nullptr;
+    // wait events (IMSAME_WAIT block / yield, lane_sync): [0] a stream's
+    // queued work, [1] the end of an NW launch; per queue (stream, stream_b)
+    hipEvent_t evw[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
     // database + index
     DBuf db, db_start, off, ent, brk, codes, fill, big;
     uint64_t n_db = 0, db_len = 0, n_ent = 0;
@@ -381,7 +385,8 @@ static inline const uint64_t *dev_qs(const imsame_ctx *c) {
 // counters block layout (u64 slots)
 enum { C_NCAND = 0, C_NCAND2, C_NNEXT, C_NCANDB, C_NCAND2B, C_NNEXT2, C_WORKB,   // (round 1b: B, 2)
        C_WORK, C_WORK2, C_PATHS, C_FLAGS, C_ERR, C_HITS, C_CELLS, C_NACC, C_REDO,
-       C_PROF, C_WIN = C_PROF + 5, C_FBK, C_SWORK, C_DBG = C_SWORK + 3, C_NSLOTS = C_DBG + 8 };
+       C_PROF, C_WIN = C_PROF + 5, C_FBK, C_SWORK, C_DBG = C_SWORK + 3, C_WASTE = C_DBG + 8,
+       C_NSLOTS };
 
 static double now_ms() {
     struct timespec ts; clock_gettime(CLOCK_MONOTONIC, &ts);
@@ -438,6 +443,60 @@ static int hw_queues() {
 #define LANES_DEF 3                 // lanes a call uses by default (align_impl); more are added on demand
 static int lanes_for_queues() { return std::max(1, std::min(LANES_MAX, hw_queues() / 2)); }
 
+// Host threads and waits.  A lane's host thread spends most of a call
+// waiting for its stream (counters of a round, the end of an NW launch);
+// hipStreamSynchronize / hipEventSynchronize on a plain event spin that
+// thread.  A rank of an N-GPU run may have fewer CPUs than its lanes and
+// upload threads (bench.py gives each rank an equal share of the host's
+// usable CPUs): IMSAME_HOST_THREADS caps the threads of the upload's host
+// pass and the lanes of a call (one host thread each), and IMSAME_WAIT=block
+// makes the lanes wait on events created with hipEventBlockingSync (the
+// thread sleeps until the device signals), IMSAME_WAIT=yield poll their event
+// and yield the CPU between polls.
+static int host_threads_cap() {
+    static std::once_flag f;
+    static int n = 8;
+    std::call_once(f, [] { const char *e = getenv("IMSAME_HOST_THREADS"); if (e && atoi(e) > 0) n = std::min(8, atoi(e)); });
+    return n;
+}
+enum { WAIT_SPIN = 0, WAIT_BLOCK, WAIT_YIELD };
+static int wait_mode() {
+    static std::once_flag f;
+    static int m = WAIT_SPIN;
+    std::call_once(f, [] {
+        // yield by default: as fast as HIP's spinning sync with a CPU per
+        // thread, and it keeps a rank whose CPU share is below its threads
+        // from starving the runtime's own threads (C2 1/8 shard on 2 CPUs, 3
+        // lanes: 17.1 vs 18.3 ms; 16 CPUs: 16.38 vs 16.46; C2 106.4 vs 106.2;
+        // profiles/r5d/)
+        const char *e = getenv("IMSAME_WAIT");
+        m = !e ? WAIT_YIELD : !strcmp(e, "block") ? WAIT_BLOCK : !strcmp(e, "spin") ? WAIT_SPIN : WAIT_YIELD;
+    });
+    return m;
+}
+static bool wait_block() { return wait_mode() != WAIT_SPIN; }   // waits go through the evw events
+// wait until event e (recorded) has completed
+static int ev_wait(hipEvent_t e) {
+    if (wait_mode() == WAIT_YIELD) {
+        for (;;) {
+            const hipError_t q = hipEventQuery(e);
+            if (q == hipSuccess) return 0;
+            if (q != hipErrorNotReady) return IMSAME_E_HIP;
+            sched_yield();
+        }
+    }
+    HIPCHK(hipEventSynchronize(e));
+    return 0;
+}
+// wait for everything queued on s (s: the lane's stream or its round-1b stream)
+static int lane_sync(imsame_ctx *c, hipStream_t s) {
+    if (!wait_block()) { HIPCHK(hipStreamSynchronize(s)); return 0; }
+    hipEvent_t e = c->evw[s == c->stream_b ? 1 : 0][0];
+    HIPCHK(hipEventRecord(e, s));
+    return ev_wait(e);
+}
+#define LANE_SYNC(c, s) do { if (int lrc_ = lane_sync((c), (s))) return lrc_; } while (0)
+
 extern "C" int imsame_dev_count(void) {
     int n = 0;
     return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
@@ -488,6 +547,8 @@ static int ctx_create(int device, imsame_ctx **out) {
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(hipEventCreate(&c->ev0));
     HIPCHK(hipEventCreate(&c->ev1));
+    for (int k = 0; k < 2; ++k)
+        HIPCHK(hipEventCreateWithFlags(&c->evw[0][k], hipEventBlockingSync | hipEventDisableTiming));
     if (c->ctr.ensure(C_NSLOTS * 8)) { delete c; return IMSAME_E_OOM; }
     xcc_probe_device(c);
     *out = c;
@@ -537,7 +598,9 @@ extern "C" int imsame_dev_open(int device, imsame_ctx **out) {
     for (size_t k = 0; k <= c->subs.size() && !rc; ++k) {
         imsame_ctx *l = k ? c->subs[k - 1] : c;
         if (hipStreamCreateWithFlags(&l->stream_b, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreate(&l->evb0) != hipSuccess || hipEventCreate(&l->evb1) != hipSuccess)
+            hipEventCreate(&l->evb0) != hipSuccess || hipEventCreate(&l->evb1) != hipSuccess ||
+            hipEventCreateWithFlags(&l->evw[1][0], hipEventBlockingSync | hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&l->evw[1][1], hipEventBlockingSync | hipEventDisableTiming) != hipSuccess)
             rc = IMSAME_E_HIP;
     }
     if (rc) { imsame_dev_close(c); return rc; }
@@ -574,6 +637,8 @@ extern "C" void imsame_dev_close(imsame_ctx *c) {
     (void)hipEventDestroy(c->ev1);
     if (c->evb0) (void)hipEventDestroy(c->evb0);
     if (c->evb1) (void)hipEventDestroy(c->evb1);
+    for (auto &q : c->evw)
+        for (hipEvent_t e : q) if (e) (void)hipEventDestroy(e);
     if (c->stream_b) (void)hipStreamDestroy(c->stream_b);
     if (c->origin && !c->is_sub) (void)hipEventDestroy(c->origin);     // a lane borrows its parent's
     if (!c->is_sub)
@@ -769,7 +834,7 @@ extern "C" int imsame_dev_set_query_range_async(imsame_ctx *c, const uint8_t *q_
         *okp = ok; *multp = mult; *lminp = lmin;
     };
     const uint64_t nblk_r = (m + QB_READS - 1) / QB_READS;
-    const int nt = (int)std::min<uint64_t>(8, (nblk_r + 15) / 16);      // >= 16 blocks per thread
+    const int nt = (int)std::min<uint64_t>(host_threads_cap(), (nblk_r + 15) / 16);   // >= 16 blocks per thread
     bool okv[8] = {true, true, true, true, true, true, true, true}, mv[8] = {true, true, true, true, true, true, true, true};
     uint64_t lminv[8] = {~0ull, ~0ull, ~0ull, ~0ull, ~0ull, ~0ull, ~0ull, ~0ull};
     if (nt <= 1) {
@@ -1111,6 +1176,8 @@ static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, 
 // its interval on the call's common clock
 static int nw_launch_done(imsame_ctx *c, int qi, uint32_t n, double *ms) {
     hipEvent_t e0 = qi ? c->evb0 : c->ev0, e1 = qi ? c->evb1 : c->ev1;
+    if (wait_block())                                              // recorded behind e1 (launch_nw)
+        if (int r = ev_wait(c->evw[qi ? 1 : 0][1])) return r;
     HIPCHK(hipEventSynchronize(e1));
     float f = 0;
     HIPCHK(hipEventElapsedTime(&f, e0, e1));
@@ -1255,6 +1322,7 @@ static int launch_nw(imsame_ctx *c, NwPlan &pl, const uint32_t *cread, const uin
     else if (pl.nstr > 1) nw_kernel<true><<<pl.blocks, 256, pl.lds, s>>>(P);
     else                  nw_kernel<false><<<pl.blocks, 256, pl.lds, s>>>(P);
     HIPCHK(hipEventRecord(e1, s));
+    if (wait_block()) HIPCHK(hipEventRecord(c->evw[qi ? 1 : 0][1], s));
     HIPCHK(hipGetLastError());
     POISON_SYNC(s, pl.pk ? "nw16_kernel" : pl.lp ? "nwp_kernel" : pl.lng ? "nwl_kernel" : "nw_kernel", c);
     return wait ? nw_launch_done(c, qi, n, ms) : 0;
@@ -1496,7 +1564,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
                            c->cur_p.as<uint64_t>(), next,
                            (uint32_t *)(ctr + nnext_slot), (unsigned long long *)(ctr + C_CELLS),
                            (unsigned long long *)(ctr + C_NACC), (unsigned long long *)(ctr + C_ERR),
-                           c->db_start.as<uint64_t>(), ctr + C_FLAGS};
+                           c->db_start.as<uint64_t>(), ctr + C_FLAGS, (unsigned long long *)(ctr + C_WASTE)};
             update_kernel<<<nblk(nc, 256), 256, 0, ss>>>(U);
             POISON_SYNC(ss, "update_kernel", c);
             HIPCHK(hipGetLastError());
@@ -1505,7 +1573,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         if ((rc = seed_launch(S, nact, s, c->ev0, c->ev1))) return rc;
         uint64_t hc[3];
         HIPCHK(hipMemcpyAsync(hc, ctr + C_NCAND, 24, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
+        LANE_SYNC(c, s);
         if ((rc = seed_time(c->ev0, c->ev1, nact))) return rc;
         const uint32_t n1 = (uint32_t)hc[0], n2 = (uint32_t)hc[1];
         if (n1 + n2 + hc[2] == 0) break;                          // no candidates, nobody paused
@@ -1529,6 +1597,8 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
                 HIPCHK(hipStreamCreateWithFlags(&c->stream_b, hipStreamNonBlocking));
                 HIPCHK(hipEventCreate(&c->evb0));
                 HIPCHK(hipEventCreate(&c->evb1));
+                for (int k = 0; k < 2; ++k)
+                    HIPCHK(hipEventCreateWithFlags(&c->evw[1][k], hipEventBlockingSync | hipEventDisableTiming));
             }
             hipStream_t sb = c->stream_b;
             uint32_t *act2 = c->act2.as<uint32_t>();
@@ -1555,7 +1625,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
             }
             uint64_t hb[2];
             HIPCHK(hipMemcpyAsync(hb, ctr + C_NCANDB, 16, hipMemcpyDeviceToHost, sb));
-            HIPCHK(hipStreamSynchronize(sb));                         // the 1b scan only: N1a runs on
+            LANE_SYNC(c, sb);                         // the 1b scan only: N1a runs on
             if ((rc = seed_time(c->evb0, c->evb1, npz))) return rc;
             const uint32_t nb = (uint32_t)hb[0];
             if (hb[1]) return IMSAME_E_STATE;                         // short reads only: cannot happen
@@ -1589,10 +1659,10 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
                 if ((rc = nw_launch_done(c, 1, nb, &msb))) return rc;
                 rec_launch(plb, nb, msb);
             }
-            HIPCHK(hipStreamSynchronize(sb));
+            LANE_SYNC(c, sb);
             uint64_t nn = 0;
             HIPCHK(hipMemcpyAsync(&nn, ctr + C_NNEXT2, 8, hipMemcpyDeviceToHost, s));
-            HIPCHK(hipStreamSynchronize(s));
+            LANE_SYNC(c, s);
             if (getenv("IMSAME_DEBUG_ROUNDS"))
                 fprintf(stderr, "[round 1b] paused=%u spec_weak=%u budget=%u cand=%u+%u next=%llu | a: k%d np%d sw%u tb%llu ck%llu "
                         "mb%u | b: k%d np%d sw%u tb%llu ck%llu mb%u\n", npz, Sb.spec_weak, Sb.budget, n1, nb,
@@ -1621,7 +1691,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         }
         uint64_t nn = 0;
         HIPCHK(hipMemcpyAsync(&nn, ctr + C_NNEXT, 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
+        LANE_SYNC(c, s);
         if (getenv("IMSAME_DEBUG_ROUNDS")) {      // diagnostics: per-round shape + a few candidates
             std::vector<imsame_read_result> o(std::min<uint32_t>(n1, 6));
             std::vector<uint32_t> cr(o.size());
@@ -1648,10 +1718,10 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     }
     uint64_t hc[C_NSLOTS];
     HIPCHK(hipMemcpyAsync(hc, ctr, C_NSLOTS * 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    LANE_SYNC(c, s);
     const double t_d2h = now_ms();
     HIPCHK(hipMemcpyAsync(res, c->res.p, (uint64_t)n * 64, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    LANE_SYNC(c, s);
     st.ms_d2h = now_ms() - t_d2h;
     st.n_hits = hc[C_HITS];
     st.seed_windows = hc[C_SWORK]; st.seed_entries = hc[C_SWORK + 1]; st.seed_ext_chunks = hc[C_SWORK + 2];
@@ -1660,6 +1730,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     st.nw_redo = (uint32_t)hc[C_REDO];
     st.nw_win = (uint32_t)hc[C_WIN];
     st.nw_fallback = (uint32_t)hc[C_FBK];
+    st.nw_spec_waste = hc[C_WASTE];
     if (getenv("IMSAME_NW_PROF")) {           // diagnostics: nw16 phase cycles (summed over waves)
         const double tot = (double)(hc[C_PROF] + hc[C_PROF + 1] + hc[C_PROF + 2] + hc[C_PROF + 3] + hc[C_PROF + 4]);
         fprintf(stderr, "[nwprof] setup %.3f sweep1 %.3f reduce %.3f sweep2 %.3f walk %.3f (fractions of %.4g wave-cycles)\n",
@@ -1793,7 +1864,8 @@ static int align_impl(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint6
     const char *lre = getenv("IMSAME_LANE_READS");
     const uint64_t lane_reads = std::max<uint64_t>(1, lre ? strtoull(lre, nullptr, 10) : LANE_READS);
     int nl = le ? std::max(1, std::min(LANES_MAX, atoi(le)))
-                : (int)std::max<uint64_t>(1, std::min<uint64_t>(std::min(lanes_for_queues(), LANES_DEF), n / lane_reads));
+                : (int)std::max<uint64_t>(1, std::min<uint64_t>(std::min(std::min(lanes_for_queues(), LANES_DEF),
+                                                                          host_threads_cap()), n / lane_reads));
     const char *lme = getenv("IMSAME_LANE_MIN");
     const uint64_t lane_min = lme ? strtoull(lme, nullptr, 10) : LANE_MIN;
     while (nl > 1 && n < (uint64_t)nl * lane_min) --nl;
@@ -1901,7 +1973,7 @@ static int align_impl(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint6
             st.ms_seed += x.ms_seed; st.ms_nw += x.ms_nw; st.nw_bytes += x.nw_bytes; st.n_rewalk += x.n_rewalk;
             st.nw_redo += x.nw_redo; st.nw_win += x.nw_win; st.nw_fallback += x.nw_fallback;
             st.seed_windows += x.seed_windows; st.seed_entries += x.seed_entries;
-            st.seed_ext_chunks += x.seed_ext_chunks;
+            st.seed_ext_chunks += x.seed_ext_chunks; st.nw_spec_waste += x.nw_spec_waste;
             st.ms_setup = std::max(st.ms_setup, x.ms_setup); st.ms_d2h += x.ms_d2h;
         }
         for (uint64_t j = 0; j < std::min<uint64_t>(x.nw_launches, IMSAME_LAUNCH_STATS); ++j) {

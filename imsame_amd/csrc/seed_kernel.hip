@@ -581,13 +581,15 @@ struct UpdLaunch {
     unsigned long long *err;
     const uint64_t *db_start;
     const uint64_t *flags = nullptr;       // NW launch flags (C_FLAGS): bit 2 = a wave ran no task
+    unsigned long long *waste = nullptr;   // candidates computed past a read's accepted one (speculation)
 };
 
 // Per read (run by its first candidate): the first accepted candidate in
 // visiting order is the read's result (NWaligned = 1, :172); rejected ones
 // before it are remembered; none accepted -> a pending size error fires
 // (terror, :155) or the read continues from its cursor next round.
-__device__ __forceinline__ void update_one(const UpdLaunch &U, uint32_t c, uint64_t &cells, uint64_t &acc) {
+__device__ __forceinline__ void update_one(const UpdLaunch &U, uint32_t c, uint64_t &cells, uint64_t &acc,
+                                           uint64_t &waste) {
     const uint32_t r = U.cread[c];
     const uint64_t k = r - U.read_from;
     const imsame_read_result oc = U.out[c];
@@ -602,6 +604,7 @@ __device__ __forceinline__ void update_one(const UpdLaunch &U, uint32_t c, uint6
             U.res[k] = o;
             U.rstat[k] = RS_ACCEPTED;
             acc += 1;
+            waste += cnt - m - 1;                          // speculative NWs past the accepted one
             U.nmemo[k] = (uint8_t)nm;
             return;
         }
@@ -676,12 +679,13 @@ __global__ __launch_bounds__(256) void seed_kernel(SeedLaunch S) {
 
 __global__ void update_kernel(UpdLaunch U) {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    uint64_t cells = 0, acc = 0;
+    uint64_t cells = 0, acc = 0, waste = 0;
     // a non-persistent NW wave that found no arena slot left its candidates'
     // rows unwritten: consume none of them (the host fails the call)
     if (U.flags && (__hip_atomic_load(U.flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 4u)) return;
-    if (c < U.n) update_one(U, c, cells, acc);
+    if (c < U.n) update_one(U, c, cells, acc, waste);
     if (cells) atomicAdd(U.cells, (unsigned long long)cells);
+    if (waste && U.waste) atomicAdd(U.waste, (unsigned long long)waste);
     if (acc) atomicAdd(U.nacc, (unsigned long long)acc);
 }
 

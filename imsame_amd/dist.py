@@ -29,6 +29,89 @@ def hip_runtimes():
     return sorted(seen)
 
 
+KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def _kfd_gpu_nodes(nodes=KFD_NODES, dev_dri="/dev/dri"):
+    """GPU agents of the KFD topology in the order the ROCm runtime numbers
+    them (ascending node id; CPU nodes have simd_count 0), as (node, unique_id)
+    pairs -- only those whose render node this process may open (a container
+    lists every GPU of the host in sysfs but gets only its own /dev/dri
+    devices; opening a render node starts no HIP runtime)."""
+    import os
+    out = []
+    try:
+        ids = sorted(int(d) for d in os.listdir(nodes) if d.isdigit())
+    except OSError:
+        return out
+    for nid in ids:
+        props = {}
+        try:
+            for line in open(os.path.join(nodes, str(nid), "properties")):
+                f = line.split()
+                if len(f) == 2:
+                    props[f[0]] = f[1]
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0") or 0) <= 0:
+            continue
+        minor = props.get("drm_render_minor")
+        if minor is not None and dev_dri is not None:
+            try:
+                os.close(os.open(os.path.join(dev_dri, "renderD%s" % minor), os.O_RDWR | os.O_CLOEXEC))
+            except OSError:
+                continue
+        out.append((nid, props.get("unique_id", "")))
+    return out
+
+
+def _apply_visible(ids, spec, uuid_of=None):
+    """A *_VISIBLE_DEVICES list applied to the devices `ids` (in order): the
+    listed ordinals (or, with uuid_of, GPU-<hex unique id> entries) in list
+    order, up to the first entry that names no device (the runtimes stop
+    there); an empty value hides every device."""
+    if spec is None:
+        return list(ids)
+    out = []
+    for tok in spec.split(","):
+        tok = tok.strip()
+        k = None
+        if tok.isdigit() and int(tok) < len(ids):
+            k = int(tok)
+        elif uuid_of is not None and tok.upper().startswith("GPU-"):
+            try:
+                want = int(tok[4:], 16)
+            except ValueError:
+                want = None
+            k = next((i for i, d in enumerate(ids) if want is not None and uuid_of(d) == want), None)
+        if k is None or ids[k] in out:
+            break
+        out.append(ids[k])
+    return out
+
+
+def visible_gpus(environ=None, nodes=KFD_NODES, dev_dri="/dev/dri"):
+    """GPUs this process may use, counted WITHOUT torch or HIP: the rank
+    launcher (bench.py --gpus N) forks its children afterwards, and a parent
+    that had started the HIP runtime must not fork+exec them.  The KFD
+    topology gives the GPU agents; ROCR_VISIBLE_DEVICES (ordinals or GPU-<uuid>,
+    applied by the ROCm runtime first), then HIP_VISIBLE_DEVICES or
+    CUDA_VISIBLE_DEVICES (ordinals among those) filter them."""
+    import os
+    env = os.environ if environ is None else environ
+    gpus = _kfd_gpu_nodes(nodes, dev_dri)
+    uid = {n: int(u) for n, u in gpus if u.isdigit()}        # KFD: decimal; ROCR: GPU-<hex>
+    ids = _apply_visible([n for n, _ in gpus], env.get("ROCR_VISIBLE_DEVICES"), uuid_of=uid.get)
+    hip = env.get("HIP_VISIBLE_DEVICES", env.get("CUDA_VISIBLE_DEVICES"))
+    return len(_apply_visible(ids, hip))
+
+
+def host_threads_per_rank(usable, world):
+    """Host threads one rank of `world` may keep busy out of the `usable` CPUs
+    of the job: an equal share, at least 2 (a lane thread and the caller)."""
+    return max(2, int(usable) // max(1, int(world)))
+
+
 def shard_range(n_reads, rank, world):
     """Contiguous [from, to) of rank `rank` out of `world`."""
     return (n_reads * rank) // world, (n_reads * (rank + 1)) // world

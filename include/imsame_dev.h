@@ -153,6 +153,13 @@ typedef struct imsame_stats {
                                loaded by ungapped extensions              */
     uint64_t seed_entries;
     uint64_t seed_ext_chunks;
+    uint64_t nw_spec_waste; /* NW work the reference never does: candidates a
+                               read emitted past the one it accepted (speculation,
+                               round_policy.h).  n_nw - nw_spec_waste are the
+                               distinct (read, record) pairs of the reference's
+                               NW calls (alignmentFunctions.c:126-186), which
+                               also repeats a rejected record at each of its
+                               e-value-passing hits                        */
 } imsame_stats;
 
 typedef struct imsame_ctx imsame_ctx;

@@ -610,11 +610,13 @@ int or_align_windows(const uint8_t *dbs, uint64_t db_len, const uint64_t *db_sta
             if (started[w * T + t] == 2) scan_chunk(c);
         }
     int st = 0;
-    uint64_t er = 0;
+    uint64_t er = 0, nn = 0;
     for (uint64_t k = 0; k < nc; k++) {
         if (started[k] == 1) pthread_join(th[k], NULL);
         if (started[k] && ch[k].status && (!st || ch[k].err_read < er)) { st = ch[k].status; er = ch[k].err_read; }
+        nn += ch[k].n_nw;
     }
+    g_last_nw = nn;
     if (err_read) *err_read = er;
     free(ch); free(th); free(started);
     or_free_index(&ix);

@@ -4,9 +4,12 @@
 #
 #  1. ThreadSanitizer and Address+UndefinedBehavior builds of the CLI's host
 #     side (imsame_host.c, imsame_pipe.c) driven by tests/san/pipe_race.c
-#     against a CPU stand-in for the device (tests/san/fake_dev.c): parallel
-#     FASTA parse vs serial, the threaded align/render/write pipeline vs one
-#     thread, pipe_render_range with 5 threads.
+#     against a CPU stand-in for the device (tests/san/fake_dev.c: lanes on
+#     their own threads handing over 3 pieces each, as the library does):
+#     parallel FASTA parse vs serial, the threaded align/render/write pipeline
+#     (per-thread pwrite at computed offsets into fallocate'd ranges) vs one
+#     thread, pipe_render_range with 5 threads, a write that fails part-way;
+#     each build with IMSAME_ONE_WRITER off and on, and one piece per lane.
 #  2. Address+UndefinedBehavior builds of the oracle (lib + CLI binary), the
 #     wave emulator and libimsame_host.so, loaded by the whole CPU test suite
 #     (IMSAME_ORACLE_LIB / IMSAME_ORACLE_BIN / IMSAME_EMU_LIB / IMSAME_LIB_HOST;
@@ -15,7 +18,7 @@
 #   bash scripts/sanitize.sh [OUTDIR] [pytest -k expression]
 set -euo pipefail
 cd "$(dirname "$0")/.."
-OUT=${1:-profiles/r4_sanitize}
+OUT=${1:-profiles/r5_sanitize}
 KEXPR=${2:-}
 B=/tmp/imsame_san
 mkdir -p "$OUT" "$B"
@@ -30,9 +33,17 @@ gcc -O1 $SAN -D_FILE_OFFSET_BITS=64 -Wall -o $B/pipe_race_asan tests/san/pipe_ra
 # and with 4 KiB render pieces: ~1500 hand-offs to each part's writer thread
 gcc -O1 -g -fno-omit-frame-pointer -fsanitize=thread -DRW_PIECE=4096 -D_FILE_OFFSET_BITS=64 -Wall \
     -o $B/pipe_race_tsan_small tests/san/pipe_race.c tests/san/fake_dev.c $HOST -lpthread -lm
-TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1" $B/pipe_race_tsan $B 2>&1 | tee -a "$OUT/pipe_race.log"
-IMSAME_ONE_WRITER=1 TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1" $B/pipe_race_tsan_small $B 2>&1 | tee -a "$OUT/pipe_race.log"
-ASAN_OPTIONS="detect_leaks=1" UBSAN_OPTIONS="print_stacktrace=1" $B/pipe_race_asan $B 2>&1 | tee -a "$OUT/pipe_race.log"
+for ow in 0 1; do
+  for lp in 3 1; do
+    echo "-- IMSAME_ONE_WRITER=$ow IMSAME_LANE_PARTS=$lp" | tee -a "$OUT/pipe_race.log"
+    IMSAME_ONE_WRITER=$ow IMSAME_LANE_PARTS=$lp TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1" \
+        $B/pipe_race_tsan $B 2>&1 | tee -a "$OUT/pipe_race.log"
+    IMSAME_ONE_WRITER=$ow IMSAME_LANE_PARTS=$lp TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1" \
+        $B/pipe_race_tsan_small $B 2>&1 | tee -a "$OUT/pipe_race.log"
+    IMSAME_ONE_WRITER=$ow IMSAME_LANE_PARTS=$lp ASAN_OPTIONS="detect_leaks=1" UBSAN_OPTIONS="print_stacktrace=1" \
+        $B/pipe_race_asan $B 2>&1 | tee -a "$OUT/pipe_race.log"
+  done
+done
 
 echo "== 2. CPU suite with asan+ubsan oracle, emulator, host library" | tee "$OUT/cpu_suite_asan.log"
 gcc -O2 $SAN -D_FILE_OFFSET_BITS=64 -D_LARGEFILE64_SOURCE -Wall -fPIC -shared -o $B/liboracle.so \

@@ -440,7 +440,11 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
             UpdLaunch U = {r, s_, nc_, o, read_from, res, rstat.data(), memo.data(), nmemo.data(),
                            cbase.data(), ccnt.data(), perr.data(), cur_p.data(), next, nnext, &cells, &nacc, &err,
                            dbs.data()};
-            for (uint32_t k = 0; k < nc_; ++k) { uint64_t ce = 0, ac = 0; update_one(U, k, ce, ac); cells += ce; nacc += ac; }
+            for (uint32_t k = 0; k < nc_; ++k) {
+                uint64_t ce = 0, ac = 0, wa = 0;
+                update_one(U, k, ce, ac, wa);
+                cells += ce; nacc += ac; st.nw_spec_waste += wa;
+            }
         };
         run_seed(S, nact);
         if (nc[0] + nc[1] + nc[2] == 0) break;

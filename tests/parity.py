@@ -23,15 +23,28 @@ def windows(lo, hi, n_total, n_threads=16, w=1500):
     return sorted(set((max(lo, a), min(hi, b)) for a, b in out))
 
 
-def check_windows(oracle, ref, rst, q, qs, res, res_lo, wins, n_threads, params=None):
+def check_windows(oracle, ref, rst, q, qs, res, res_lo, wins, n_threads, params=None, count_ref=False):
     """Compare res (rows of reads res_lo, res_lo + 1, ...) with the oracle on
     the windows; the oracle's memo of rejected pairs (identical results, NW is
-    pure: Appendix A Q18) keeps it fast."""
+    pure: Appendix A Q18) keeps it fast.  It also counts the NW calls on the
+    windows: `nw_distinct` with the memo (the distinct (read, record) pairs up
+    to each read's accepted one -- the device computes exactly these plus its
+    speculation) and, with count_ref, `nw_reference` without it (the
+    reference's own count: it re-runs NW at every e-value-passing hit of a
+    rejected record, alignmentFunctions.c:126-186)."""
+    import ctypes as C
+    oracle.lib.or_last_nw.restype = C.c_uint64
     oracle.lib.or_set_memo_rejected(1)
     try:
         rc, exp, er = oracle.align_windows(ref, rst, q, qs, wins, params, n_threads)
+        nw_distinct = int(oracle.lib.or_last_nw())
     finally:
         oracle.lib.or_set_memo_rejected(0)
+    nw_ref = None
+    if count_ref:
+        rc2, exp2, _ = oracle.align_windows(ref, rst, q, qs, wins, params, n_threads)
+        nw_ref = int(oracle.lib.or_last_nw())
+        assert rc2 == rc and all(np.array_equal(a[f], b[f]) for a, b in zip(exp, exp2) for f in PARITY_FIELDS)
     compared = identical = 0
     bad = []
     for (a, b), e in zip(wins, exp):
@@ -42,4 +55,5 @@ def check_windows(oracle, ref, rst, q, qs, res, res_lo, wins, n_threads, params=
         bad += [a + int(i) for i in np.flatnonzero(~same)[:3]]
     return {"reads_compared": compared, "identical": identical, "windows": [list(x) for x in wins],
             "n_threads": n_threads, "oracle_rc": int(rc), "first_mismatches": bad,
-            "accepted_in_windows": int(sum(int((res[a - res_lo:b - res_lo]["status"] == 1).sum()) for a, b in wins))}
+            "accepted_in_windows": int(sum(int((res[a - res_lo:b - res_lo]["status"] == 1).sum()) for a, b in wins)),
+            "oracle_nw_distinct": nw_distinct, "oracle_nw_reference": nw_ref}

@@ -64,7 +64,8 @@ void fake_result(const imsame_ctx *c, uint64_t r, imsame_read_result *o, uint32_
 
 typedef struct {
     imsame_ctx *c;
-    uint64_t a, b;
+    const uint64_t *cut;              /* piece i = reads [cut[i], cut[i+1]) */
+    int k, nl, np;                    /* this lane runs pieces k, k + nl, ... */
     imsame_read_result *res;          /* res[r - base] */
     uint64_t base;
     imsame_part_fn fn;
@@ -74,30 +75,41 @@ typedef struct {
 
 static void *lane_run(void *p) {
     lane *l = p;
-    uint32_t *paths = malloc((l->b - l->a + 1) * sizeof *paths);
-    uint64_t np = 0;
-    for (uint64_t r = l->a; r < l->b; ++r) {
-        imsame_read_result *o = &l->res[r - l->base];
-        fake_result(l->c, r, o, paths + np);
-        if (o->status == 1 && l->want_paths) { o->path_off = (uint32_t)np; np += o->path_len; }
+    for (int i = l->k; i < l->np; i += l->nl) {
+        const uint64_t a = l->cut[i], b = l->cut[i + 1];
+        uint32_t *paths = malloc((b - a + 1) * sizeof *paths);
+        uint64_t np = 0;
+        for (uint64_t r = a; r < b; ++r) {
+            imsame_read_result *o = &l->res[r - l->base];
+            fake_result(l->c, r, o, paths + np);
+            if (o->status == 1 && l->want_paths) { o->path_off = (uint32_t)np; np += o->path_len; }
+        }
+        /* a lane hands over each piece from its own thread, as the library's do */
+        l->fn(l->user, a, b, IMSAME_OK, ~0ull, np ? paths : NULL, np);
+        free(paths);
     }
-    /* a lane hands over its reads from its own thread, as the library's do */
-    l->fn(l->user, l->a, l->b, IMSAME_OK, ~0ull, np ? paths : NULL, np);
-    free(paths);
     return NULL;
 }
 
+/* as imsame_dev.hip:align_impl with a callback: NL lanes on their own
+ * threads, each lane's share cut into IMSAME_LANE_PARTS pieces (3 by
+ * default), piece i on lane i mod NL, handed over as each one ends */
 int imsame_dev_align_parts(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64_t n_threads_semantic,
                            const imsame_params *prm, imsame_read_result *res, imsame_part_fn part, void *user,
                            imsame_stats *stats) {
     (void)n_threads_semantic;
     enum { NL = 3 };
+    const char *pe = getenv("IMSAME_LANE_PARTS");
+    int ns = pe ? atoi(pe) : 3;
+    ns = ns < 1 ? 1 : ns > 16 ? 16 : ns;
+    const int np = NL * ns;
+    uint64_t cut[3 * 16 + 1];
     lane L[NL];
     pthread_t th[NL];
     const uint64_t n = read_to - read_from;
+    for (int i = 0; i <= np; ++i) cut[i] = read_from + n * (uint64_t)i / (uint64_t)np;
     for (int k = 0; k < NL; ++k)
-        L[k] = (lane){c, read_from + n * k / NL, read_from + n * (k + 1) / NL, res, read_from, part, user,
-                      prm->want_paths};
+        L[k] = (lane){c, cut, k, NL, np, res, read_from, part, user, prm->want_paths};
     for (int k = 1; k < NL; ++k) pthread_create(&th[k], NULL, lane_run, &L[k]);
     lane_run(&L[0]);
     for (int k = 1; k < NL; ++k) pthread_join(th[k], NULL);

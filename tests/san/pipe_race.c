@@ -11,7 +11,10 @@
  * The reference's threads share one FILE* (alignmentFunctions.c:165-168);
  * this is the exchange that replaces it.  Exit status 0 = all equal. */
 #define _GNU_SOURCE
+#include <errno.h>
 #include <fcntl.h>
+#include <signal.h>
+#include <sys/resource.h>
 #include <inttypes.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -67,8 +70,15 @@ static char *slurp(const char *path, size_t *len) {
     return b;
 }
 
+static int run_pipe_r(const host_seqs *db, const host_seqs *q, int G, int rt, uint64_t batch, const char *path,
+                      uint64_t *acc, pipe_result *out);
 static int run_pipe(const host_seqs *db, const host_seqs *q, int G, int rt, uint64_t batch, const char *path,
                     uint64_t *acc) {
+    pipe_result r;
+    return run_pipe_r(db, q, G, rt, batch, path, acc, &r);
+}
+static int run_pipe_r(const host_seqs *db, const host_seqs *q, int G, int rt, uint64_t batch, const char *path,
+                      uint64_t *acc, pipe_result *out) {
     pipe_dev d[8];
     int devs[8] = {0};
     if (pipe_open(d, devs, G) || pipe_index(d, G, db) || pipe_set_query(d, G, q)) return 1;
@@ -84,6 +94,7 @@ static int run_pipe(const host_seqs *db, const host_seqs *q, int G, int rt, uint
     close(o.out_fd);
     pipe_close(d, G);
     *acc = r.accepted;
+    *out = r;
     return rc;
 }
 
@@ -156,6 +167,33 @@ int main(int argc, char **argv) {
     close(fd3);
     char *b3 = slurp(p3, &l3);
     if (!b3 || l3 != t.len || memcmp(b3, t.buf, l3)) { fprintf(stderr, "FAIL render_range\n"); fails++; }
+    /* 4. a write that fails part-way (file size limit): the pipeline reports
+     * the error and how many leading bytes are complete -- whole parts, a
+     * prefix of the serial text -- for the CLI to cut the file back to */
+    {
+        char p4[512];
+        snprintf(p4, sizeof p4, "%s/pipe_race_4.align", dir);
+        signal(SIGXFSZ, SIG_IGN);
+        struct rlimit old, lim;
+        getrlimit(RLIMIT_FSIZE, &old);
+        lim = old;
+        lim.rlim_cur = (rlim_t)(l1 * 2 / 3);
+        setrlimit(RLIMIT_FSIZE, &lim);
+        uint64_t a4 = 0;
+        pipe_result r4;
+        const int rc4 = run_pipe_r(&db, &q, 3, 4, 997, p4, &a4, &r4);
+        setrlimit(RLIMIT_FSIZE, &old);
+        size_t l4;
+        char *b4 = slurp(p4, &l4);
+        if (rc4 == 0 || r4.write_errno != EFBIG || r4.bytes_ok == 0 || r4.bytes_ok > (uint64_t)lim.rlim_cur ||
+            !b4 || l4 < r4.bytes_ok || memcmp(b4, b1, r4.bytes_ok)) {
+            fprintf(stderr, "FAIL write error: rc %d errno %d bytes_ok %" PRIu64 " file %zu\n", rc4, r4.write_errno,
+                    r4.bytes_ok, b4 ? l4 : 0);
+            fails++;
+        }
+        free(b4);
+        unlink(p4);
+    }
     printf("pipe_race: %" PRIu64 " reads, %" PRIu64 " accepted, %zu bytes, %s\n", q.n, a1, l1, fails ? "FAIL" : "ok");
     imsame_dev_close(c);
     free(res); free(paths); free(t.buf); free(one.buf); free(b1); free(b2); free(b3); free(fd_); free(fq);

@@ -121,3 +121,63 @@ def test_db_shard_merge_over_gloo(tmp_path):
     exp = merge_shard_results(_fake_parts(world))
     for r in range(world):
         assert np.array_equal(np.load(tmp_path / f"m{r}.npy"), exp)
+
+
+def _fake_kfd(tmp_path, nodes):
+    """A KFD topology tree: nodes = [(simd_count, render_minor, unique_id)]
+    and /dev/dri render nodes for the minors given (None: node not openable)."""
+    root, dri = tmp_path / "nodes", tmp_path / "dri"
+    root.mkdir()
+    dri.mkdir()
+    for k, (simd, minor, uid) in enumerate(nodes):
+        d = root / str(k)
+        d.mkdir()
+        (d / "properties").write_text(f"cpu_cores_count 0\nsimd_count {simd}\ndrm_render_minor {minor or 0}\n"
+                                      f"unique_id {uid}\n")
+        if simd and minor is not None:
+            (dri / f"renderD{minor}").write_text("")
+    return str(root), str(dri)
+
+
+def test_visible_gpus_from_kfd_topology(tmp_path):
+    """bench.py's rank launcher counts GPUs from the KFD topology, never
+    through torch or HIP (a parent that starts the runtime must not fork
+    children): CPU nodes and render nodes this process cannot open do not
+    count; ROCR_VISIBLE_DEVICES (ordinals or GPU-<hex uuid>) applies first,
+    HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES index what it leaves; a list
+    stops at its first entry naming no device."""
+    from imsame_amd.dist import visible_gpus, host_threads_per_rank
+    nodes, dri = _fake_kfd(tmp_path, [(0, None, 0), (304, 128, 1001), (304, 129, 1002), (304, 130, 1003),
+                                      (304, None, 1004)])
+    vg = lambda env: visible_gpus(env, nodes, dri)            # noqa: E731
+    assert vg({}) == 3                                        # the CPU node and the unopenable GPU do not count
+    assert vg({"HIP_VISIBLE_DEVICES": "1"}) == 1
+    assert vg({"HIP_VISIBLE_DEVICES": "0,2"}) == 2
+    assert vg({"HIP_VISIBLE_DEVICES": "0,7,1"}) == 1          # stops at the first bad ordinal
+    assert vg({"HIP_VISIBLE_DEVICES": "1,1"}) == 1            # a repeat ends the list
+    assert vg({"CUDA_VISIBLE_DEVICES": "0,1"}) == 2
+    assert vg({"HIP_VISIBLE_DEVICES": "", "CUDA_VISIBLE_DEVICES": "0,1"}) == 0   # HIP's wins, empty hides all
+    assert vg({"ROCR_VISIBLE_DEVICES": "2"}) == 1
+    assert vg({"ROCR_VISIBLE_DEVICES": "GPU-%x,GPU-%016x" % (1003, 1001)}) == 2
+    assert vg({"ROCR_VISIBLE_DEVICES": "2,0", "HIP_VISIBLE_DEVICES": "1"}) == 1
+    assert vg({"ROCR_VISIBLE_DEVICES": "2", "HIP_VISIBLE_DEVICES": "1"}) == 0
+    assert visible_gpus({}, str(tmp_path / "absent"), dri) == 0
+    assert host_threads_per_rank(16, 8) == 2 and host_threads_per_rank(16, 1) == 16
+    assert host_threads_per_rank(4, 8) == 2 and host_threads_per_rank(128, 8) == 16
+
+
+def test_visible_gpus_starts_no_runtime(tmp_path):
+    """In a fresh interpreter, counting imports neither torch nor a HIP
+    runtime (checked on the GPU box against torch.cuda.device_count() by
+    tests/test_gpu.py:test_device_count_without_hip)."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import json, sys; sys.path.insert(0, %r); from imsame_amd.dist import visible_gpus; n = visible_gpus(); "
+            "print(json.dumps({'n': n, 'hip': 'libamdhip64' in open('/proc/self/maps').read(), "
+            "'torch': 'torch' in sys.modules}))" % repo)
+    p = subprocess.run([sys.executable, "-c", code], stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=120)
+    assert p.returncode == 0, p.stderr.decode(errors="replace")
+    got = json.loads(p.stdout.decode().strip().splitlines()[-1])
+    assert not got["hip"] and not got["torch"], got

@@ -187,6 +187,24 @@ def test_synthetic_c2_shape_vs_oracle_all_T(dev, oracle):
     full, _, _ = dev.align(n_threads=8)
     parts = [dev.align(a, b, n_threads=8)[0] for a, b in ((0, 3001), (3001, 7777), (7777, 12_000))]
     assert not _cmp(np.concatenate(parts), full)
+    # NW accounting (imsame_stats.nw_spec_waste): the device computes the
+    # distinct (read, record) NWs of the reference's visiting order up to each
+    # read's accepted one -- the oracle's count with its memo -- plus the
+    # speculative candidates past it; the reference's own count (no memo)
+    # repeats rejected records and is at least the distinct one
+    import ctypes
+    oracle.lib.or_last_nw.restype = ctypes.c_uint64
+    oracle.lib.or_set_memo_rejected(1)
+    try:
+        oracle.align(ref, rst, q, qs, None, 16)
+        distinct = int(oracle.lib.or_last_nw())
+    finally:
+        oracle.lib.or_set_memo_rejected(0)
+    oracle.align(ref, rst, q, qs, None, 16)
+    reference = int(oracle.lib.or_last_nw())
+    res, _, st = dev.align(n_threads=16)
+    print({"n_nw": st.n_nw, "spec_waste": st.nw_spec_waste, "oracle_distinct": distinct, "reference": reference})
+    assert st.n_nw - st.nw_spec_waste == distinct and reference >= distinct
 
 
 def test_nw16_two_pass_equals_one_pass(dev, oracle):
@@ -914,7 +932,11 @@ def test_short_call_without_shared_arena(oracle, monkeypatch):
 def test_bench_launches_ranks_itself():
     """`bench.py --gpus 2` with no launcher starts its two ranks itself (the
     driver's form of the N-GPU run), here as a gloo rehearsal on one card: the
-    line says n_gpus 2, and the shards' accepted reads sum to a one-rank run's."""
+    line says n_gpus 2, and the shards' accepted reads sum to a one-rank run's.
+    Two forms: the fixed `--device 0` rehearsal, and the driver's own form
+    without --device -- the launcher counts the GPUs without HIP (KFD
+    topology) and, told that 2 are visible, maps rank r onto card r mod the
+    real count."""
     import json
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -922,18 +944,52 @@ def test_bench_launches_ranks_itself():
     base = [sys.executable, "-u", "bench.py", "--steps", "1", "--warmup", "0", "--cpu-sample", "0", "--e2e", "off",
             "--reads", "100000"]
     lines = {}
-    for n in (2, 1):
-        extra = ["--gpus", str(n)] + (["--dist-backend", "gloo", "--device", "0"] if n > 1 else [])
+    for key, extra in (("dev0", ["--gpus", "2", "--dist-backend", "gloo", "--device", "0"]),
+                       ("nodev", ["--gpus", "2", "--dist-backend", "gloo", "--device-count-override", "2"]),
+                       ("one", ["--gpus", "1"])):
         p = subprocess.run(base + extra, cwd=repo, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                            timeout=900)
         assert p.returncode == 0, p.stderr[-3000:].decode(errors="replace")
-        lines[n] = json.loads([x for x in p.stdout.decode().splitlines() if x.startswith("{")][-1])
-    two, one = lines[2], lines[1]
-    print(json.dumps({"two": {k: two[k] for k in ("value", "n_gpus", "ranks")}, "one_value": one["value"]}))
-    assert two["n_gpus"] == 2 and two["ranks"]["world"] == 2 and two["ranks"]["launcher"] == "bench.py"
-    assert two["ranks"]["backend"] == "gloo" and len(two["ranks"]["hip_runtime"]) == 1
-    assert two["detail"]["accepted_reads"] == one["detail"]["accepted_reads"] > 80_000
-    assert two["config"]["reads_per_gpu"] == 50_000
+        lines[key] = json.loads([x for x in p.stdout.decode().splitlines() if x.startswith("{")][-1])
+    one = lines["one"]
+    print(json.dumps({k: {f: lines[k][f] for f in ("value", "n_gpus", "ranks")} for k in lines}))
+    for key in ("dev0", "nodev"):
+        two = lines[key]
+        assert two["n_gpus"] == 2 and two["ranks"]["world"] == 2 and two["ranks"]["launcher"] == "bench.py"
+        assert two["ranks"]["backend"] == "gloo" and len(two["ranks"]["hip_runtime"]) == 1
+        assert two["detail"]["accepted_reads"] == one["detail"]["accepted_reads"] > 80_000
+        assert two["config"]["reads_per_gpu"] == 50_000
+        assert two["ranks"]["host_threads_per_rank"] >= 2
+    assert lines["nodev"]["ranks"]["launcher_visible_gpus"] >= 1 and lines["nodev"]["ranks"]["device"] == 0
+
+
+def test_device_count_without_hip():
+    """The rank launcher counts GPUs before it starts its children, so it must
+    not start the HIP runtime (a parent holding a GPU context must not fork
+    and exec them): imsame_amd.dist.visible_gpus() in a fresh process leaves
+    no libamdhip64 mapped and agrees with torch.cuda.device_count(), also
+    under HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES."""
+    import json
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    count = ("import json, sys; sys.path.insert(0, %r); from imsame_amd.dist import visible_gpus; n = visible_gpus(); "
+             "maps = open('/proc/self/maps').read(); print(json.dumps({'n': n, 'hip': 'libamdhip64' in maps, "
+             "'torch': 'torch' in sys.modules}))" % repo)
+    ref = "import torch; print(torch.cuda.device_count())"
+    base = {k: v for k, v in os.environ.items() if k not in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES",
+                                                             "CUDA_VISIBLE_DEVICES")}
+    for extra in ({}, {"HIP_VISIBLE_DEVICES": "0"}, {"ROCR_VISIBLE_DEVICES": "0"}):
+        env = dict(base, **extra)
+        p = subprocess.run([sys.executable, "-c", count], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                           timeout=120)
+        assert p.returncode == 0, p.stderr.decode(errors="replace")
+        got = json.loads(p.stdout.decode().strip().splitlines()[-1])
+        assert not got["hip"] and not got["torch"], got
+        t = subprocess.run([sys.executable, "-c", ref], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                           timeout=300)
+        assert t.returncode == 0, t.stderr.decode(errors="replace")
+        print(extra, got, "torch:", t.stdout.decode().strip())
+        assert got["n"] == int(t.stdout.decode().strip().splitlines()[-1]) >= 1, (extra, got)
 
 
 def test_rccl_world1_next_to_library():

@@ -562,6 +562,40 @@ def test_emulated_pipeline_seed_budget(emu, oracle, budget, lanes, spec, weak, m
     assert rounds >= 2 or r1b() > 0 or budget == "0", rounds
 
 
+@pytest.mark.parametrize("spec,weak", [("1", "1"), ("8", "8")])
+def test_emulated_nw_accounting(emu, oracle, spec, weak, monkeypatch):
+    """The device's NW work against the reference's (alignmentFunctions.c:
+    126-186: one NW per e-value-passing hit until one is accepted): n_nw minus
+    the speculative candidates past each read's accepted one
+    (imsame_stats.nw_spec_waste, update_one) equals the oracle's count of
+    distinct (read, record) NWs, and the oracle without its memo -- the
+    reference's own count -- is at least that.  Without speculation nothing
+    is wasted."""
+    import ctypes
+    from tests import synth
+    monkeypatch.setenv("IMSAME_SPEC", spec)
+    monkeypatch.setenv("IMSAME_SPEC_WEAK", weak)
+    oracle.lib.or_last_nw.restype = ctypes.c_uint64
+    ref, rst = synth.make_reference_arr(400_000, 2_000, seed=71)
+    q, qs = synth.make_reads_arr(ref, 400, 150, seed=72)
+    rc2, r2, _, st = emu.align(ref, rst, q, qs, oracle.params(), 4)
+    oracle.lib.or_set_memo_rejected(1)
+    try:
+        rc1, r1, _ = oracle.align(ref, rst, q, qs, oracle.params(), 4)
+        distinct = int(oracle.lib.or_last_nw())
+    finally:
+        oracle.lib.or_set_memo_rejected(0)
+    rc0, r0, _ = oracle.align(ref, rst, q, qs, oracle.params(), 4)
+    reference = int(oracle.lib.or_last_nw())
+    assert rc0 == rc1 == rc2 == 0
+    for f in PARITY_FIELDS:
+        assert np.array_equal(r1[f], r2[f]) and np.array_equal(r0[f], r1[f]), f
+    assert st.n_nw - st.nw_spec_waste == distinct, (st.n_nw, st.nw_spec_waste, distinct)
+    assert reference >= distinct > 0
+    if spec == weak == "1":
+        assert st.nw_spec_waste == 0
+
+
 def test_thresholds_match_long_double_tests(emu, oracle):
     """Integer tables (csrc/tables.h) == the reference's long double tests."""
     lib = emu.lib
