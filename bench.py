@@ -546,7 +546,10 @@ def seed_roofline(st, n_reads, read_len):
     if not wins or not ms:
         return None
     survey = n_reads * read_len + 8 * wins + 4 * st["n_hits"] + 32 * ch       # SURVEY 8(d) widths
-    built = n_reads * read_len + 16 * wins + 8 * ents + 32 * ch               # u64 offsets, 8-byte entries
+    # as built: u64 bucket offsets, 8-byte entries, and per 16-base chunk pair
+    # of an extension one packed dword of the database and one of the query
+    # (seed_kernel.hip:ungapped_raw on 2-bit codes)
+    built = n_reads * read_len + 16 * wins + 8 * ents + 8 * ch
     t = ms / 1e3
     return {"bound": "latency (dependent random probes)", "kernel_ms": round(ms, 3),
             "windows": wins, "entries": ents, "hits": st["n_hits"], "ext_chunk_pairs": ch,
@@ -555,7 +558,8 @@ def seed_roofline(st, n_reads, read_len):
             "frac": round(built / t / 1e9 / HBM_PEAK_GBS, 4),
             "probes_per_s": round(wins / t, 1), "entries_per_s": round(ents / t, 1),
             "bytes_per_probe": round(built / wins, 2),
-            "ext_bytes_per_hit": round(32 * ch / max(st["n_hits"], 1), 1)}
+            "ext_bytes_per_hit": round(8 * ch / max(st["n_hits"], 1), 1),
+            "ext_form": "2-bit packed database and query, 16 bases per dword"}
 
 
 # MI355X_MICROARCH.md: a wave issues one VALU instruction over 2 cycles

@@ -28,8 +28,11 @@ from .abi import Params, Stats, RESULT_DTYPE, PARITY_FIELDS  # noqa: F401
 # queues give 4 lanes and 1-2 % more at C2), so a Python host that has not
 # chosen asks for 8 here -- effective only when nothing in this process has
 # started HIP yet (the CLI and bench.py set it at start-up for the same
-# reason).  Results never depend on it.
-if not os.environ.get("GPU_MAX_HW_QUEUES"):
+# reason).  Results never depend on it.  This changes the variable for the
+# whole process (any HIP user started later sees it): IMSAME_NO_HWQ_DEFAULT=1
+# leaves the environment alone (the library then runs the lanes HIP's 4
+# queues allow), see INTEGRATION.md.
+if not os.environ.get("GPU_MAX_HW_QUEUES") and not os.environ.get("IMSAME_NO_HWQ_DEFAULT"):
     os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 HERE = os.path.dirname(os.path.abspath(__file__))

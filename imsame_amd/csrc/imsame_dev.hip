@@ -55,6 +55,13 @@ __global__ void mark_record_starts(const uint64_t *st, uint64_t n, uint64_t L, u
 #define GRID_STRIDE(p, n) \
     for (uint64_t p = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; p < (n); p += (uint64_t)gridDim.x * blockDim.x)
 
+// the 2-bit packed bases (seed_kernel.hip:pk_word): words [w0, w1) of dst
+// (biased: dst[w] holds bases 16w ..) from src (biased: src[p] = base p,
+// valid for lo <= p < hi; other slots 0)
+__global__ void pack2_kernel(const uint8_t *src, int64_t lo, int64_t hi, uint32_t *dst, uint64_t w0, uint64_t w1) {
+    GRID_STRIDE(k, w1 - w0) dst[w0 + k] = pk_word(src, (int64_t)(w0 + k), lo, hi);
+}
+
 // code of the 12-mer ending at base p, or ~0 when a reset lies in (p-11, p]
 __global__ void kmer_code_kernel(const uint8_t *seq, uint64_t L, const uint32_t *brk, uint32_t *codes,
                                  uint32_t *cnt) {
@@ -280,8 +287,8 @@ struct imsame_ctx {
     // wait events (IMSAME_WAIT block / yield, lane_sync): [0] a stream's
     // queued work, [1] the end of an NW launch; per queue (stream, stream_b)
     hipEvent_t evw[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
-    // database + index
-    DBuf db, db_start, off, ent, brk, codes, fill, big;
+    // database + index; dbw: the bases 2-bit packed (seed_kernel.hip:pk_word)
+    DBuf db, db_start, off, ent, brk, codes, fill, big, dbw;
     uint64_t n_db = 0, db_len = 0, n_ent = 0;
     uint32_t max_rec = 0;
     std::vector<uint64_t> h_db_start;
@@ -291,6 +298,8 @@ struct imsame_ctx {
     // the starts of reads q_lo .. q_hi.  Kernels index both with GLOBAL read
     // and base numbers through the biased views dev_q / dev_qs.
     DBuf q, q_start;
+    DBuf qw;                          // the uploaded bases 2-bit packed, from word qw_base = q_base >> 4
+    uint64_t qw_base = 0;
     uint64_t n_q = 0, q_len = 0, q_lo = 0, q_hi = 0, q_base = 0, q_lo_first = 0;
     uint64_t *h_q_start = nullptr;    // starts of reads q_lo .. q_hi, page-locked (the
     uint64_t h_q_cap = 0;             // H2D copy of them runs asynchronously)
@@ -302,6 +311,7 @@ struct imsame_ctx {
     // bases below q_part_end[k] and is complete when q_part_ev[k] fires (the
     // starts go first, with part 0); a lane borrows its parent's events
     std::vector<hipEvent_t> q_part_ev;
+    std::vector<hipEvent_t> q_copy_ev;   // part k's bytes copied (its packing waits for it)
     std::vector<uint64_t> q_part_end;
     bool q_len_mult = false;         // every read length is a multiple of NW16_K
     uint32_t q_len_uni = 0;          // the one read length of the uploaded range (0: lengths differ)
@@ -375,6 +385,9 @@ static uint64_t range_ymax(const imsame_ctx *c, uint64_t a, uint64_t b) {
 }
 // biased views: valid for the uploaded reads (and QPAD bases before them)
 static inline const uint8_t *dev_q(const imsame_ctx *c) { return (const uint8_t *)((uintptr_t)c->q.p - c->q_base); }
+static inline const uint32_t *dev_qw(const imsame_ctx *c) {
+    return (const uint32_t *)((uintptr_t)c->qw.p - c->qw_base * sizeof(uint32_t));
+}
 static inline const uint64_t *dev_qs(const imsame_ctx *c) {
     return (const uint64_t *)((uintptr_t)c->q_start.p - c->q_lo * sizeof(uint64_t));
 }
@@ -612,7 +625,7 @@ extern "C" int imsame_dev_open(int device, imsame_ctx **out) {
 }
 
 static void lane_unalias(imsame_ctx *l) {
-    DBuf *al[] = {&l->db, &l->db_start, &l->off, &l->ent, &l->q, &l->q_start};
+    DBuf *al[] = {&l->db, &l->db_start, &l->off, &l->ent, &l->q, &l->q_start, &l->dbw, &l->qw};
     for (DBuf *b : al) { b->p = nullptr; b->cap = 0; }
     l->q_part_ev.clear(); l->q_part_end.clear();
 }
@@ -621,6 +634,7 @@ extern "C" void imsame_dev_close(imsame_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->ustream) (void)hipStreamSynchronize(c->ustream);    // before the lane that may own it goes
+    if (c->stream_b) (void)hipStreamSynchronize(c->stream_b);
     if (!c->ustream_own) c->ustream = nullptr;
     for (imsame_ctx *l : c->subs) { lane_unalias(l); imsame_dev_close(l); }
     c->subs.clear();
@@ -631,7 +645,7 @@ extern "C" void imsame_dev_close(imsame_ctx *c) {
                     &c->act1, &c->cread, &c->csid, &c->cread2, &c->csid2, &c->cout, &c->cout2, &c->ctr,
                     &c->minraw, &c->minlen, &c->minident, &c->tb, &c->bnd, &c->paths, &c->ck, &c->rc_in, &c->rc_out,
                     &c->rc_a, &c->rc_b, &c->rc_c, &c->cbase, &c->ccnt, &c->perr, &c->wcap, &c->wout, &c->wstart,
-                    &c->crow, &c->cperm, &c->rhist, &c->act2, &c->slotbits, &c->np_tb, &c->np_ck};
+                    &c->crow, &c->cperm, &c->rhist, &c->act2, &c->slotbits, &c->np_tb, &c->np_ck, &c->dbw, &c->qw};
     for (DBuf *b : bufs) b->release();
     (void)hipEventDestroy(c->ev0);
     (void)hipEventDestroy(c->ev1);
@@ -643,6 +657,8 @@ extern "C" void imsame_dev_close(imsame_ctx *c) {
     if (c->origin && !c->is_sub) (void)hipEventDestroy(c->origin);     // a lane borrows its parent's
     if (!c->is_sub)
         for (hipEvent_t e : c->q_part_ev) (void)hipEventDestroy(e);
+    if (!c->is_sub)
+        for (hipEvent_t e : c->q_copy_ev) (void)hipEventDestroy(e);
     if (!c->is_sub && c->h_q_start) (void)hipHostFree(c->h_q_start);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->ustream && c->ustream_own) (void)hipStreamDestroy(c->ustream);
@@ -658,6 +674,7 @@ static int lane_sub(imsame_ctx *c, int k, imsame_ctx **out) {
     }
     imsame_ctx *l = c->subs[k - 1];
     l->db = c->db; l->db_start = c->db_start; l->off = c->off; l->ent = c->ent; l->q = c->q; l->q_start = c->q_start;
+    l->dbw = c->dbw; l->qw = c->qw; l->qw_base = c->qw_base;
     l->n_db = c->n_db; l->db_len = c->db_len; l->n_ent = c->n_ent; l->max_rec = c->max_rec;
     l->have_index = c->have_index;
     l->n_q = c->n_q; l->q_len = c->q_len; l->q_lo = c->q_lo; l->q_hi = c->q_hi; l->q_base = c->q_base;
@@ -707,8 +724,8 @@ extern "C" int imsame_dev_index(imsame_ctx *c, const uint8_t *db_seq, uint64_t d
     for (uint64_t k = 0; k < n_db; ++k) max_rec = std::max<uint64_t>(max_rec, c->h_db_start[k + 1] - c->h_db_start[k]);
     if (max_rec >= 0xFFFFFFF0ull) return IMSAME_E_ARG;           // record-relative u32 entry positions
     c->max_rec = (uint32_t)max_rec;
-    const uint64_t nw = db_len / 32 + 2;
-    if (c->db.ensure(db_len + 64) || c->db_start.ensure((n_db + 1) * 8) || c->brk.ensure(nw * 4) ||
+    const uint64_t nw = db_len / 32 + 2, npw = db_len / 16 + 4;
+    if (c->db.ensure(db_len + 64) || c->dbw.ensure(npw * 4) || c->db_start.ensure((n_db + 1) * 8) || c->brk.ensure(nw * 4) ||
         c->codes.ensure((db_len + 1) * 4) || c->off.ensure(((uint64_t)NBUCKETS + 1) * 8) ||
         c->fill.ensure((uint64_t)NBUCKETS * 4) || c->big.ensure((uint64_t)NBUCKETS * 4))
         return IMSAME_E_OOM;
@@ -718,6 +735,7 @@ extern "C" int imsame_dev_index(imsame_ctx *c, const uint8_t *db_seq, uint64_t d
             if (int rc = b->poison(s)) return rc;
     }
     if (db_len) HIPCHK(hipMemcpyAsync(c->db.p, db_seq, db_len, hipMemcpyHostToDevice, s));
+    pack2_kernel<<<gsblk(npw, 256), 256, 0, s>>>(c->db.as<uint8_t>(), 0, (int64_t)db_len, c->dbw.as<uint32_t>(), 0, npw);
     HIPCHK(hipMemcpyAsync(c->db_start.p, c->h_db_start.data(), (n_db + 1) * 8, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemsetAsync(c->brk.p, 0, nw * 4, s));
     if (db_brk && db_len) HIPCHK(hipMemcpyAsync(c->brk.p, db_brk, (db_len + 7) / 8, hipMemcpyHostToDevice, s));
@@ -794,6 +812,7 @@ extern "C" int imsame_dev_set_query_range_async(imsame_ctx *c, const uint8_t *q_
     if (n_q >= 0xFFFFFFF0ull) return IMSAME_E_ARG;
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->ustream));    // a previous upload may still read h_q_start / fill q
+    if (c->stream_b) HIPCHK(hipStreamSynchronize(c->stream_b));  // ... or pack q
     c->have_query = false;
     auto qs = [&](uint64_t r) { return r < n_q ? q_start[r] : q_len; };
     // one pass over the shard's starts: ascending within the query (else
@@ -865,7 +884,16 @@ extern "C" int imsame_dev_set_query_range_async(imsame_ctx *c, const uint8_t *q_
     const uint64_t nb = b1 - c->q_base, ns = read_to - read_from + 1;
     c->q_len_mult = mult;
     c->q_len_uni = (m > 0 && lmin == lmax && lmax < 0xFFFFFFFFu) ? (uint32_t)lmax : 0u;
-    if (c->q.ensure(nb + 64) || c->q_start.ensure(ns * 8)) return IMSAME_E_OOM;
+    // packed copy: words qw_base .. qw_end of the bases [q_base, q_base + nb + 64)
+    c->qw_base = c->q_base >> 4;
+    const uint64_t qw_end = (c->q_base + nb + 64) / 16 + 2;
+    if (c->q.ensure(nb + 64) || c->q_start.ensure(ns * 8) || c->qw.ensure((qw_end - c->qw_base) * 4))
+        return IMSAME_E_OOM;
+    while (c->q_copy_ev.size() < Q_PARTS) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        c->q_copy_ev.push_back(e);
+    }
     while (c->q_part_ev.size() < Q_PARTS) {
         hipEvent_t e;
         HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -876,16 +904,32 @@ extern "C" int imsame_dev_set_query_range_async(imsame_ctx *c, const uint8_t *q_
     // only for the parts that hold its reads
     HIPCHK(hipMemcpyAsync(c->q_start.p, c->h_q_start, ns * 8, hipMemcpyHostToDevice, c->ustream));
     HIPCHK(hipMemsetAsync((uint8_t *)c->q.p + nb, 0, 64, c->ustream));
+    // The packed copy (seed_kernel.hip:pk_word) is made part by part on a
+    // second stream (this context's round-1b stream, idle between calls), so
+    // the copies run back to back on the upload stream while each part's
+    // packing follows its copy; a part is ready (q_part_ev) once packed.
+    hipStream_t ps = c->stream_b ? c->stream_b : c->ustream;
+    uint64_t wdone = c->qw_base;                         // packed words written so far
     for (uint64_t k = 0, a = 0; k < Q_PARTS; ++k) {      // bases [q_base + a, q_base + b)
         const uint64_t b = nb * (k + 1) / Q_PARTS;
         if (b > a) HIPCHK(hipMemcpyAsync((uint8_t *)c->q.p + a, q_seq + c->q_base + a, b - a, hipMemcpyHostToDevice,
                                          c->ustream));
-        HIPCHK(hipEventRecord(c->q_part_ev[k], c->ustream));
+        HIPCHK(hipEventRecord(c->q_copy_ev[k], c->ustream));
+        if (ps != c->ustream) HIPCHK(hipStreamWaitEvent(ps, c->q_copy_ev[k], 0));
+        // the packed words whose bases are all in HBM now (the last part: all,
+        // with the 64 zero bytes past the range)
+        const uint64_t wend = k + 1 == Q_PARTS ? qw_end : (c->q_base + b) / 16;
+        if (wend > wdone)
+            pack2_kernel<<<gsblk(wend - wdone, 256), 256, 0, ps>>>(
+                dev_q(c), (int64_t)c->q_base, (int64_t)(c->q_base + nb + 64), (uint32_t *)dev_qw(c), wdone, wend);
+        wdone = std::max(wdone, wend);
+        HIPCHK(hipEventRecord(c->q_part_ev[k], ps));
         c->q_part_end[k] = c->q_base + b;
         a = b;
     }
     c->have_query = true;
     POISON_SYNC(c->ustream, "query upload", c);
+    POISON_SYNC(ps, "query packing", c);
     return IMSAME_OK;
 }
 
@@ -903,6 +947,7 @@ extern "C" int imsame_dev_sync(imsame_ctx *c) {
     if (!c) return IMSAME_E_ARG;
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->ustream));
+    if (c->stream_b) HIPCHK(hipStreamSynchronize(c->stream_b));     // the upload's packing
     HIPCHK(hipStreamSynchronize(c->stream));
     return IMSAME_OK;
 }
@@ -1491,6 +1536,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         HIPCHK(hipMemsetAsync(ctr + C_NCAND, 0, 7 * 8, s));     // NCAND, NCAND2, NNEXT, (1b) NCANDB, NCAND2B, NNEXT2, WORKB
         SeedLaunch S;
         S.db = c->db.as<uint8_t>(); S.db_start = c->db_start.as<uint64_t>(); S.n_db = c->n_db; S.db_len = c->db_len;
+        S.dbw = c->dbw.as<uint32_t>(); S.qw = dev_qw(c);
         S.q = qd; S.q_start = qsd; S.n_q = c->n_q; S.q_len = c->q_len;
         S.qs_lo = c->q_lo; S.qs_lo_first = c->q_lo_first;
         S.off = c->off.as<uint64_t>(); S.ent = c->ent.as<uint2>();
@@ -2084,6 +2130,7 @@ extern "C" int imsame_dev_align_windows(imsame_ctx *c, uint64_t read_from, uint6
         SeedLaunch S;
         memset(&S, 0, sizeof S);
         S.db = c->db.as<uint8_t>(); S.db_start = c->db_start.as<uint64_t>(); S.n_db = c->n_db; S.db_len = c->db_len;
+        S.dbw = c->dbw.as<uint32_t>(); S.qw = dev_qw(c);
         S.q = dev_q(c); S.q_start = dev_qs(c); S.n_q = c->n_q; S.q_len = c->q_len;
         S.qs_lo = c->q_lo; S.qs_lo_first = c->q_lo_first;
         S.off = c->off.as<uint64_t>(); S.ent = c->ent.as<uint2>();

@@ -23,6 +23,8 @@ __device__ __forceinline__ uint32_t base2(uint32_t c) { return ((c >> 1) ^ (c >>
 struct SeedLaunch {
     const uint8_t *db; const uint64_t *db_start; uint64_t n_db, db_len;
     const uint8_t *q;  const uint64_t *q_start;  uint64_t n_q, q_len;
+    const uint32_t *dbw, *qw;              // the same bases 2-bit packed (pk_base: word p >> 4 holds base p;
+                                           // qw biased like q)
     const uint64_t *off; const uint2 *ent;        // CSR {pos - record start, record}, buckets in descending pos
     const uint32_t *active; uint32_t n_active;
     uint64_t read_from, rpt, T;
@@ -95,66 +97,124 @@ __device__ __forceinline__ Bytes16 load16(const uint8_t *__restrict__ p, int64_t
     __builtin_memcpy(&r, p + a, 16);
     return r;
 }
-__device__ __forceinline__ bool byte_eq(const Bytes16 &a, const Bytes16 &b, int k) {
-    return ((a.w[k >> 2] ^ b.w[k >> 2]) & (0xFFu << (8 * (k & 3)))) == 0;
+
+// 2-bit packed bases (base2 codes A0 C1 G2 T3), 16 per dword: base p in word
+// p >> 4, bits 2(p & 15).  The ungapped extension and the scan's k-mer codes
+// read the database and the query in this form (imsame_dev.hip:pack2_kernel):
+// 4 bytes per 16 bases instead of 16, so a 500 Mbp database (C3) is 125 MB and
+// stays in the 256 MB Infinity Cache, and a 16-base chunk is a funnel shift of
+// two dwords -- one new dword per chunk as a walk slides.  Both buffers hold
+// only ACGT (the loaders drop every other byte, IMSAME.c:216-221, :340-345),
+// so the codes lose nothing.  Arrays carry >= 2 words past their last base.
+__device__ __forceinline__ uint32_t pk_base(const uint32_t *__restrict__ w, int64_t p) {
+    return (w[p >> 4] >> (2u * (uint32_t)(p & 15))) & 3u;
+}
+// word w of the packed form of src (src[p] = base p, valid for lo <= p < hi;
+// other slots 0): one 16-byte load where the word lies inside, four base2
+// codes per dword gathered by shifts
+__device__ __forceinline__ uint32_t pk_word(const uint8_t *__restrict__ src, int64_t w, int64_t lo, int64_t hi) {
+    const int64_t p0 = w * 16;
+    uint32_t v = 0;
+    if (p0 >= lo && p0 + 16 <= hi) {
+        const Bytes16 b = load16(src, p0);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t t = ((b.w[k] >> 1) ^ (b.w[k] >> 2)) & 0x03030303u;   // base2 of each byte
+            const uint32_t u = t | (t >> 6);                                   // codes 0,1 -> bits 0-3; 2,3 -> 16-19
+            v |= ((u & 0xFu) | ((u >> 12) & 0xF0u)) << (8 * k);
+        }
+    } else {
+        for (int k = 0; k < 16; ++k) {
+            const int64_t p = p0 + k;
+            if (p >= lo && p < hi) v |= base2(src[p]) << (2 * k);
+        }
+    }
+    return v;
+}
+// bit 2k set where slot k of a and b (bases) differ
+__device__ __forceinline__ uint32_t pk_diff(uint32_t a, uint32_t b) {
+    const uint32_t m = a ^ b;
+    return (m | (m >> 1)) & 0x55555555u;
+}
+// the 12-mer code of bases p-11 .. p (first base most significant, as the
+// index's kmer_code_kernel): slots 0..11 of one funnel shift, reversed in
+// 2-bit groups (bit reverse, then swap each pair back)
+__device__ __forceinline__ uint32_t kmer_code_pk(const uint32_t *__restrict__ w, int64_t p) {
+    const int64_t a = p - (IMSAME_FIXED_K - 1);
+    const uint32_t v = wv_alignbit(w[(a >> 4) + 1], w[a >> 4], 2u * (uint32_t)(a & 15));
+    const uint32_t r = wv_bitrev(v);
+    return (((r >> 1) & 0x55555555u) | ((r & 0x55555555u) << 1)) >> (32 - 2 * IMSAME_FIXED_K);
 }
 
 // alignmentFromQuickHits (alignmentFunctions.c:276-387): the raw score in the
 // reference's u64 wrap arithmetic (:373).  Loop bounds fold the reference's
 // per-step tests (:321-322, :344-345) into one limit per direction.  The
-// byte-serial walk of the reference runs over 16-byte chunks (one round of
-// loads per chunk instead of per byte); the first chunk of each direction is
-// fetched before either walk starts.
-// (*nch, when given, counts the 16-byte chunk pairs loaded)
-__device__ __forceinline__ uint64_t ungapped_raw(const uint8_t *__restrict__ db, const uint8_t *__restrict__ q,
+// base-serial walk of the reference runs over 16-base chunks of the packed
+// buffers (one dword load per chunk and side, the mismatches of 16 bases from
+// one xor); the first chunk of each direction is fetched before either walk
+// starts.
+// (*nch, when given, counts the 16-base chunk pairs loaded)
+__device__ __forceinline__ uint64_t ungapped_raw(const uint32_t *__restrict__ db, const uint32_t *__restrict__ q,
                                                  int64_t pd0, int64_t pq0, int64_t xs, int64_t xe, int64_t ys,
                                                  int64_t ye, int64_t dbl, int64_t ql, uint32_t *nch = nullptr) {
     int64_t end_x = pd0 - 1, beg_x = end_x - IMSAME_FIXED_K + 1;
     int sc = IMSAME_FIXED_K * IMSAME_POINT, best_r = sc, best_l = sc;
     uint32_t idents = IMSAME_FIXED_K;
     const int64_t bx0 = pd0 - IMSAME_FIXED_K - 1, by0 = pq0 - IMSAME_FIXED_K - 1;
-    const bool lwin = bx0 >= 15 && by0 >= 15;            // left chunks need 15 bytes below the start
-    Bytes16 rd = load16(db, pd0), rq = load16(q, pq0);
-    Bytes16 ld = rd, lq = rq;
-    if (lwin) { ld = load16(db, bx0 - 15); lq = load16(q, by0 - 15); }
+    const bool lwin = bx0 >= 15 && by0 >= 15;            // left chunks need 15 bases below the start
+    // right walk: chunk = bases x .. x+15, words [x >> 4, (x >> 4) + 1];
+    // word indices are recomputed from the positions (fewer live registers:
+    // the scan kernels stay at 4 waves per SIMD, seed_group_kernel)
+    const int64_t dq = pq0 - pd0;                        // y - x on the right walk
+    const uint32_t dsh = 2u * (uint32_t)(pd0 & 15), qsh = 2u * (uint32_t)(pq0 & 15);
+    uint32_t d0 = db[pd0 >> 4], d1 = db[(pd0 >> 4) + 1], q0 = q[pq0 >> 4], q1 = q[(pq0 >> 4) + 1];
+    // left walk: chunk = bases x-15 .. x (x = bx0 = pd0 - 13 first), walked
+    // downwards (slot 15 first); its shifts are the right walk's + 8 bases
+    uint32_t l0 = 0, l1 = 0, m0 = 0, m1 = 0;
+    const uint32_t lsh = (dsh + 8u) & 31u, lqsh = (qsh + 8u) & 31u;
+    if (lwin) {
+        l0 = db[(bx0 - 15) >> 4]; l1 = db[((bx0 - 15) >> 4) + 1];
+        m0 = q[(by0 - 15) >> 4]; m1 = q[((by0 - 15) >> 4) + 1];
+    }
     uint32_t nc = lwin ? 2 : 1;
     const int64_t fx = min(min(dbl - 1, xe), pd0 + (min(ql - 1, ye) - pq0));
-    for (int64_t x = pd0, y = pq0; sc > 0 && x <= fx;) {
+    for (int64_t x = pd0; sc > 0 && x <= fx;) {
         const int64_t n = min((int64_t)16, fx - x + 1);
+        const uint32_t ne = pk_diff(wv_alignbit(d1, d0, dsh), wv_alignbit(q1, q0, qsh));
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             if (k < n && sc > 0) {
-                const bool eq = byte_eq(rd, rq, k);
+                const bool eq = !((ne >> (2 * k)) & 1u);
                 sc += eq ? IMSAME_POINT : -IMSAME_POINT;
                 idents += eq;
                 if (best_r <= sc) { best_r = sc; end_x = x + k; }
             }
         }
-        x += n; y += n;
-        if (sc > 0 && x <= fx) { rd = load16(db, x); rq = load16(q, y); ++nc; }
+        x += n;                             // n < 16 only for the last chunk (x > fx after it)
+        if (sc > 0 && x <= fx) { d0 = d1; d1 = db[(x >> 4) + 1]; q0 = q1; q1 = q[((x + dq) >> 4) + 1]; ++nc; }
     }
     sc = best_r;                        // left pass restarts from the right max, best_l stays 48 (:339)
     const int64_t lx = max(max((int64_t)0, xs), bx0 - (by0 - max((int64_t)0, ys)));
     int64_t x = bx0, y = by0;
     if (lwin) {
-        // chunk = bytes x-15 .. x, walked downwards (byte 15 first)
         while (sc > 0 && x >= lx && x >= 15 && y >= 15) {
             const int64_t n = min((int64_t)16, x - lx + 1);
+            const uint32_t ne = pk_diff(wv_alignbit(l1, l0, lsh), wv_alignbit(m1, m0, lqsh));
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
                 if (k < n && sc > 0) {
-                    const bool eq = byte_eq(ld, lq, 15 - k);
+                    const bool eq = !((ne >> (2 * (15 - k))) & 1u);
                     sc += eq ? IMSAME_POINT : -IMSAME_POINT;
                     idents += eq;
                     if (best_l <= sc) { best_l = sc; beg_x = x - k; }
                 }
             }
-            x -= n; y -= n;
-            if (sc > 0 && x >= lx && x >= 15 && y >= 15) { ld = load16(db, x - 15); lq = load16(q, y - 15); ++nc; }
+            x -= n; y -= n;                 // n < 16 only when x passes lx (the loop ends)
+            if (sc > 0 && x >= lx && x >= 15 && y >= 15) { l1 = l0; l0 = db[(x - 15) >> 4]; m1 = m0; m0 = q[(y - 15) >> 4]; ++nc; }
         }
     }
-    for (; sc > 0 && x >= lx; --x, --y) {                 // the first 15 bytes of a buffer
-        if (db[x] == q[y]) { sc += IMSAME_POINT; ++idents; } else sc -= IMSAME_POINT;
+    for (; sc > 0 && x >= lx; --x, --y) {                 // the first 15 bases of a buffer
+        if (pk_base(db, x) == pk_base(q, y)) { sc += IMSAME_POINT; ++idents; } else sc -= IMSAME_POINT;
         if (best_l <= sc) { best_l = sc; beg_x = x; }
     }
     if (nch) *nch += nc;
@@ -295,7 +355,7 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, Seed
             const int64_t xs = (int64_t)S.db_start[sid];
             const int64_t xe = (sid == S.n_db - 1) ? (int64_t)S.db_len : (int64_t)S.db_start[sid + 1] - 1;
             ++tl.hits;
-            const uint64_t raw = ungapped_raw(S.db, S.q, xs + ent.x, (int64_t)p + 1, xs, xe, ys, ye,
+            const uint64_t raw = ungapped_raw(S.dbw, S.qw, xs + ent.x, (int64_t)p + 1, xs, xe, ys, ye,
                                               (int64_t)S.db_len, (int64_t)S.q_len, &tl.chunks);
             if (mraw != ~0ull && raw >= mraw) {                      // e < min_e (:139)
                 const uint64_t xlen = S.db_start[sid + 1] - S.db_start[sid];
@@ -367,14 +427,6 @@ __host__ __device__ static inline int seed_lanes(uint32_t nact) {
     return nact >= 2000000u ? 1 : nact >= 750000u ? 4 : 16;
 }
 
-__device__ __forceinline__ uint32_t kmer_code_at(const uint8_t *__restrict__ q, uint64_t p) {
-    const Bytes16 b = load16(q, (int64_t)p - (IMSAME_FIXED_K - 1));     // bases p-11 .. p
-    uint32_t code = 0;
-#pragma unroll
-    for (int t = 0; t < IMSAME_FIXED_K; ++t) code = (code << 2) | base2((b.w[t >> 2] >> (8 * (t & 3))) & 0xFFu);
-    return code;
-}
-
 // emit[] lives in registers, identical in every lane of the group (each lane
 // runs the same merge); statically indexed so it never spills to scratch.
 template <int SM>
@@ -424,7 +476,7 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
         if (!done && pw < up_to) {
             // (a read that may still start speculating lists for it already)
             const uint32_t need = (ne == 0 && nm == 0 && S.spec_weak > spec ? S.spec_weak : spec) - ne;
-            const uint32_t code = kmer_code_at(S.q, pw);
+            const uint32_t code = kmer_code_pk(S.qw, pw);
             const uint64_t wbase = S.off[code], hi = S.off[code + 1];
             ++tl.wins;
             for (uint64_t e = wbase + (wl == 0 ? h : 0u); e < hi; ++e) {
@@ -439,7 +491,7 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
                 ++ev;
                 const int64_t xs = (int64_t)S.db_start[sid];
                 const int64_t xe = (sid == S.n_db - 1) ? (int64_t)S.db_len : (int64_t)S.db_start[sid + 1] - 1;
-                const uint64_t raw = ungapped_raw(S.db, S.q, xs + ent.x, (int64_t)pw + 1, xs, xe, ys, ye,
+                const uint64_t raw = ungapped_raw(S.dbw, S.qw, xs + ent.x, (int64_t)pw + 1, xs, xe, ys, ye,
                                                   (int64_t)S.db_len, (int64_t)S.q_len, &tl.chunks);
                 if (mraw != ~0ull && raw >= mraw) {                      // e < min_e (:139)
                     const uint64_t xlen = S.db_start[sid + 1] - S.db_start[sid];
@@ -524,10 +576,10 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
     if (shortc && S.crow) {
         // the first candidate's hit again: its entry gives the record position
         // and its extension the strength
-        const uint2 ent = S.ent[S.off[kmer_code_at(S.q, rs + e0p)] + e0r];
+        const uint2 ent = S.ent[S.off[kmer_code_pk(S.qw, rs + e0p)] + e0r];
         const int64_t xs = (int64_t)S.db_start[ent.y];
         const int64_t xe = (ent.y == S.n_db - 1) ? (int64_t)S.db_len : (int64_t)S.db_start[ent.y + 1] - 1;
-        const uint64_t raw = ungapped_raw(S.db, S.q, xs + ent.x, (int64_t)(rs + e0p) + 1, xs, xe, ys, ye,
+        const uint64_t raw = ungapped_raw(S.dbw, S.qw, xs + ent.x, (int64_t)(rs + e0p) + 1, xs, xe, ys, ye,
                                           (int64_t)S.db_len, (int64_t)S.q_len);
         S.crow[o] = predicted_row(raw, ylen, ent.x, (int64_t)e0p + 1);
         for (uint32_t m = 1; m < ne; ++m) S.crow[o + m] = INT32_MIN;
@@ -556,11 +608,11 @@ __device__ __forceinline__ void accept_window_one(const SeedLaunch &S, const ims
     const int64_t xe = (sid == S.n_db - 1) ? (int64_t)S.db_len : (int64_t)S.db_start[sid + 1] - 1;
     uint64_t w = ~0ull;
     for (uint64_t p = p0 + IMSAME_FIXED_K - 1; p < up_to && w == ~0ull; ++p) {
-        const uint32_t code = kmer_code_at(S.q, p);
+        const uint32_t code = kmer_code_pk(S.qw, p);
         for (uint64_t e = S.off[code]; e < S.off[code + 1]; ++e) {
             const uint2 ent = S.ent[e];
             if (ent.y != sid) continue;
-            const uint64_t raw = ungapped_raw(S.db, S.q, xs + ent.x, (int64_t)p + 1, xs, xe, ys, ye,
+            const uint64_t raw = ungapped_raw(S.dbw, S.qw, xs + ent.x, (int64_t)p + 1, xs, xe, ys, ye,
                                               (int64_t)S.db_len, (int64_t)S.q_len);
             if (mraw != ~0ull && raw >= mraw) { w = p; break; }
         }
@@ -659,8 +711,19 @@ __global__ void accept_window_kernel(const SeedLaunch S, const imsame_read_resul
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k < n) accept_window_one(S, res, k, wout);
 }
+// <= 128 VGPRs (4 waves per SIMD): the scans of later rounds and of round 1b
+// run beside NW launches, whose 19-column waves hold 256 VGPRs each, so a
+// SIMD with one NW wave has 256 left -- two scan waves at 128, one at 136.  A
+// scan kernel compiled to 135 VGPRs ran round 1b's scans 2.8x longer next to
+// NW (C2 1/8 shard 3.1 -> 8.8 ms, profiles/r5f/).  (The whole-wave groups with
+// SPEC_BIG candidates in registers would spill at 128; they run the small
+// later rounds.)
+#ifndef SEED_WAVES_PER_EU
+#define SEED_WAVES_PER_EU 4
+#endif
 template <int L, int SM = SPEC_MAX>
-__global__ __launch_bounds__(256) void seed_group_kernel(SeedLaunch S) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SM > SPEC_MAX ? 1 : SEED_WAVES_PER_EU)))
+void seed_group_kernel(SeedLaunch S) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x & 63, wl = lane % L;
     uint2 *lst = (uint2 *)smem + threadIdx.x * SM;
@@ -670,7 +733,7 @@ __global__ __launch_bounds__(256) void seed_group_kernel(SeedLaunch S) {
     seed_tally_flush(S, tl);
 }
 
-__global__ __launch_bounds__(256) void seed_kernel(SeedLaunch S) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEED_WAVES_PER_EU))) void seed_kernel(SeedLaunch S) {
     const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
     SeedTally tl;
     if (idx < S.n_active) seed_one(S, idx, tl);

@@ -91,6 +91,9 @@ WV_DEVICE uint32_t wv_bfi(uint32_t m, uint32_t a, uint32_t b) {
 }
 // byte permute of the 8 bytes {hi:lo}: selector byte k picks byte sel_k (0-3 of lo, 4-7 of hi)
 WV_DEVICE uint32_t wv_perm(uint32_t hi, uint32_t lo, uint32_t sel) { return __builtin_amdgcn_perm(hi, lo, sel); }
+// the 32 bits of {hi:lo} from bit s up (s < 32): one v_alignbit_b32
+WV_DEVICE uint32_t wv_alignbit(uint32_t hi, uint32_t lo, uint32_t s) { return __builtin_amdgcn_alignbit(hi, lo, s); }
+WV_DEVICE uint32_t wv_bitrev(uint32_t v) { return __builtin_bitreverse32(v); }        // v_bfrev_b32
 // (w << 1) | c in one v_addc_co_u32 (w + w + carry): the compare's lane mask
 // is the carry-in
 WV_DEVICE uint32_t wv_shift_in(uint32_t w, bool c) {
@@ -209,6 +212,14 @@ inline uint32_t pk_neg_mask(uint32_t a) { return pk_map(a, 0, [](int x, int) { r
 inline uint32_t wv_shift_in(uint32_t w, bool c) { return (w << 1) | (c ? 1u : 0u); }
 inline uint32_t wv_and_or(uint32_t m, uint32_t c, uint32_t w) { return (m & c) | w; }
 inline uint32_t wv_bfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
+inline uint32_t wv_alignbit(uint32_t hi, uint32_t lo, uint32_t s) {
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (s & 31));
+}
+inline uint32_t wv_bitrev(uint32_t v) {
+    uint32_t r = 0;
+    for (int k = 0; k < 32; ++k) r |= ((v >> k) & 1u) << (31 - k);
+    return r;
+}
 inline uint32_t wv_perm(uint32_t hi, uint32_t lo, uint32_t sel) {
     const uint64_t v = ((uint64_t)hi << 32) | lo;
     uint32_t r = 0;

@@ -322,6 +322,13 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
     if (b1 > qbase) memcpy((uint8_t *)qpad.data() + qbase, q + qbase, b1 - qbase);
     memset((uint8_t *)qpad.data() + b1, 0, std::min<uint64_t>(64, qpad.size() * 4 - b1));
     q = (const uint8_t *)qpad.data();
+    // the packed bases (imsame_dev.hip:pack2_kernel): the whole database, and
+    // the query's words over [qbase, b1 + 64) as the upload packs them; other
+    // words POISON
+    std::vector<uint32_t> dbw(db_len / 16 + 4), qw(q_len / 16 + 8, 0xEEEEEEEEu);
+    for (uint64_t w = 0; w < dbw.size(); ++w) dbw[w] = pk_word(db, (int64_t)w, 0, (int64_t)db_len);
+    for (uint64_t w = qbase >> 4; w < std::min<uint64_t>(qw.size(), (b1 + 64) / 16 + 2); ++w)
+        qw[w] = pk_word(q, (int64_t)w, (int64_t)qbase, (int64_t)std::min<uint64_t>(b1 + 64, qpad.size() * 4));
     std::vector<uint64_t> qsv(qs.size(), 0xDEADBEEFDEADBEEFull);
     for (uint64_t r = read_from; r <= read_to; ++r) qsv[r] = qs[r];
     uint64_t qlo_first = read_from;
@@ -376,6 +383,7 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
         SeedLaunch S;
         S.db = db; S.db_start = dbs.data(); S.n_db = n_db; S.db_len = db_len;
         S.q = q; S.q_start = qsv.data(); S.n_q = n_q; S.q_len = q_len;
+        S.dbw = dbw.data(); S.qw = qw.data();
         S.qs_lo = read_from; S.qs_lo_first = qlo_first;
         S.off = off.data(); S.ent = ent.data(); S.wcap = nullptr; S.wstart = nullptr;
         S.active = act.data(); S.n_active = nact;
@@ -495,14 +503,14 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
 extern "C" uint64_t emu_ungapped(const uint8_t *db, uint64_t db_len, const uint64_t *db_start, uint64_t n_db,
                                  const uint8_t *q, uint64_t q_len, const uint64_t *q_start, uint64_t n_q,
                                  uint64_t pd0, uint64_t pq0, uint64_t read, uint64_t sid) {
-    std::vector<uint32_t> dbpad(db_len / 4 + 17, 0), qpad(q_len / 4 + 17, 0);
-    if (db_len) memcpy(dbpad.data(), db, db_len);
-    if (q_len) memcpy(qpad.data(), q, q_len);
+    std::vector<uint32_t> dbw(db_len / 16 + 4), qw(q_len / 16 + 4);
+    for (uint64_t w = 0; w < dbw.size(); ++w) dbw[w] = pk_word(db, (int64_t)w, 0, (int64_t)db_len);
+    for (uint64_t w = 0; w < qw.size(); ++w) qw[w] = pk_word(q, (int64_t)w, 0, (int64_t)q_len);
     const int64_t xs = (int64_t)db_start[sid];
     const int64_t xe = (sid == n_db - 1) ? (int64_t)db_len : (int64_t)db_start[sid + 1] - 1;
     const int64_t ys = (int64_t)q_start[read];
     const int64_t ye = (read == n_q - 1) ? (int64_t)q_len : (int64_t)q_start[read + 1] - 1;
-    return ungapped_raw((const uint8_t *)dbpad.data(), (const uint8_t *)qpad.data(), (int64_t)pd0, (int64_t)pq0,
+    return ungapped_raw(dbw.data(), qw.data(), (int64_t)pd0, (int64_t)pq0,
                         xs, xe, ys, ye, (int64_t)db_len, (int64_t)q_len);
 }
 
