@@ -586,6 +586,20 @@ def valu_roofline(path, kernel, config, cells_per_s, read_len=150, record_bp=200
            "unit": "G wave-instr/s", "frac": round(rate / VALU_ISSUE_PEAK, 4), "source": os.path.relpath(path, REPO),
            "note": "peak = 2 cycles per wave instruction at 2.4 GHz; v_pk_*_i16 / v_perm issue at ~4 "
                    "(profiles/r06_valu_rate.txt)"}
+    # the shader clock under this config's NW load (profiles/nw_clock.json:
+    # s_memtime / s_memrealtime in the bench's own launches) and the issue
+    # fraction at that clock instead of the 2.4 GHz peak
+    kp = os.path.join(REPO, "profiles", "nw_clock.json")
+    if os.path.exists(kp):
+        try:
+            kj = json.load(open(kp))
+            if kj.get("kernel") == kernel and config in kj:
+                ghz = kj[config]["shader_clock_ghz"]
+                out.update({"shader_clock_ghz": ghz,
+                            "frac_at_measured_clock": round(rate / (VALU_ISSUE_PEAK * ghz / 2.4), 4),
+                            "clock_source": os.path.relpath(kp, REPO)})
+        except Exception:
+            pass
     # the measured ceiling of this instruction mix: the first-sweep loop
     # alone on a full chip (scripts/micro/nw16_loop.py), cycles per VALU per
     # SIMD -> a fraction of the same 2-cycle peak

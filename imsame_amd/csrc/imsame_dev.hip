@@ -398,7 +398,7 @@ static inline const uint64_t *dev_qs(const imsame_ctx *c) {
 // counters block layout (u64 slots)
 enum { C_NCAND = 0, C_NCAND2, C_NNEXT, C_NCANDB, C_NCAND2B, C_NNEXT2, C_WORKB,   // (round 1b: B, 2)
        C_WORK, C_WORK2, C_PATHS, C_FLAGS, C_ERR, C_HITS, C_CELLS, C_NACC, C_REDO,
-       C_PROF, C_WIN = C_PROF + 5, C_FBK, C_SWORK, C_DBG = C_SWORK + 3, C_WASTE = C_DBG + 8,
+       C_PROF, C_WIN = C_PROF + 6, C_FBK, C_SWORK, C_DBG = C_SWORK + 3, C_WASTE = C_DBG + 8,
        C_NSLOTS };
 
 static double now_ms() {
@@ -1779,8 +1779,11 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     st.nw_spec_waste = hc[C_WASTE];
     if (getenv("IMSAME_NW_PROF")) {           // diagnostics: nw16 phase cycles (summed over waves)
         const double tot = (double)(hc[C_PROF] + hc[C_PROF + 1] + hc[C_PROF + 2] + hc[C_PROF + 3] + hc[C_PROF + 4]);
-        fprintf(stderr, "[nwprof] setup %.3f sweep1 %.3f reduce %.3f sweep2 %.3f walk %.3f (fractions of %.4g wave-cycles)\n",
-                hc[C_PROF] / tot, hc[C_PROF + 1] / tot, hc[C_PROF + 2] / tot, hc[C_PROF + 3] / tot, hc[C_PROF + 4] / tot, tot);
+        // shader clock under this load: the waves' cycles over their 100 MHz real time
+        const double ghz = hc[C_PROF + 5] ? tot / (double)hc[C_PROF + 5] * 0.1 : 0.0;
+        fprintf(stderr, "[nwprof] setup %.3f sweep1 %.3f reduce %.3f sweep2 %.3f walk %.3f (fractions of %.4g wave-cycles) "
+                "clock_ghz %.3f\n", hc[C_PROF] / tot, hc[C_PROF + 1] / tot, hc[C_PROF + 2] / tot, hc[C_PROF + 3] / tot,
+                hc[C_PROF + 4] / tot, tot, ghz);
     }
     st.nw_launch_ms = st.nw_launches ? st.ms_nw / st.nw_launches : 0;
     st.nw_bytes = 2 * st.nw_cells;       // 2 B/cell traceback floor; bench.py adds xlen + ylen per NW
@@ -2323,9 +2326,10 @@ extern "C" int imsame_dev_nw_pairs(imsame_ctx *c, const uint8_t *xs, const uint6
     HIPCHK(hipStreamSynchronize(s));
     if (getenv("IMSAME_NW_PROF") && pl.pk) {  // diagnostics (scripts/micro/nw16_loop.py): raw phase wave-cycles
         fprintf(stderr, "[nwprof-raw] blocks %u G %d GPW %d k %d steps %d cand %llu setup %llu sweep1 %llu reduce %llu "
-                "sweep2 %llu walk %llu ms %.4f\n", pl.blocks, pl.G, pl.GPW, pl.k, pl.steps, (unsigned long long)npairs,
-                (unsigned long long)hc[C_PROF], (unsigned long long)hc[C_PROF + 1], (unsigned long long)hc[C_PROF + 2],
-                (unsigned long long)hc[C_PROF + 3], (unsigned long long)hc[C_PROF + 4], ms);
+                "sweep2 %llu walk %llu rt %llu ms %.4f\n", pl.blocks, pl.G, pl.GPW, pl.k, pl.steps,
+                (unsigned long long)npairs, (unsigned long long)hc[C_PROF], (unsigned long long)hc[C_PROF + 1],
+                (unsigned long long)hc[C_PROF + 2], (unsigned long long)hc[C_PROF + 3], (unsigned long long)hc[C_PROF + 4],
+                (unsigned long long)hc[C_PROF + 5], ms);
     }
     if (getenv("IMSAME_NW_PROF") && pl.lng)   // diagnostics: which long-read kernel, waves that fell back
         fprintf(stderr, "[nwprof-long] kernel %s blocks %u cand %llu fallback %llu ms %.4f\n",

@@ -228,7 +228,8 @@ __device__ __forceinline__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const
 
     // phase profile (P.prof): 0 fetch + staging + setup, 1 first sweep, 2 best-cell
     // reduction, 3 second sweep(s) incl. restore, 4 walks + results
-    unsigned long long ph[5] = {0, 0, 0, 0, 0}, tq = P.prof ? wv_clock() : 0;
+    // (and the wave's 100 MHz real time beside its cycles: the shader clock under this load)
+    unsigned long long ph[5] = {0, 0, 0, 0, 0}, tq = P.prof ? wv_clock() : 0, rt0 = P.prof ? wv_realtime() : 0;
     auto mark = [&](const int k) {
         if (P.prof) { const unsigned long long n = wv_clock(); ph[k] += n - tq; tq = n; }
     };
@@ -678,8 +679,10 @@ __device__ __forceinline__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const
         }
         wv_lds_sync();
     }
-    if (P.prof && lane == 0)
+    if (P.prof && lane == 0) {
         for (int k = 0; k < 5; ++k) wv_atomic_add64(P.prof + k, ph[k]);
+        wv_atomic_add64(P.prof + 5, wv_realtime() - rt0);
+    }
 }
 
 // Launch shape: G lanes per group, GPW groups (2*GPW candidates) per wave,

@@ -39,6 +39,8 @@ WV_DEVICE void wv_atomic_min64(unsigned long long *p, unsigned long long v) { at
 WV_DEVICE void wv_atomic_add64(unsigned long long *p, unsigned long long v) { atomicAdd(p, v); }
 // shader clock (phase profiling only)
 WV_DEVICE unsigned long long wv_clock() { return (unsigned long long)clock64(); }
+// the constant 100 MHz counter (s_memrealtime): with wv_clock it gives the shader clock
+WV_DEVICE unsigned long long wv_realtime() { return (unsigned long long)__builtin_amdgcn_s_memrealtime(); }
 // LDS written by some lanes, read by others of the SAME wave
 WV_DEVICE void wv_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -190,6 +192,7 @@ inline void wv_atomic_min64(unsigned long long *p, unsigned long long v) {
 }
 inline void wv_atomic_add64(unsigned long long *p, unsigned long long v) { __atomic_fetch_add(p, v, __ATOMIC_SEQ_CST); }
 inline unsigned long long wv_clock() { return 0; }
+inline unsigned long long wv_realtime() { return 0; }
 inline void wv_lds_sync() { wvemu::sync(); }
 inline void wv_mem_sync() { wvemu::sync(); }
 

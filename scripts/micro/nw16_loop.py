@@ -85,15 +85,22 @@ def main():
         a.waves_per_simd = min(r["blocks"] * 4, tasks) / 1024.0
     rate = a.waves_per_simd * a.valu / cyc_iter           # wave-instructions per SIMD cycle
     tot_cyc = sum(r[k] for k in ("setup", "sweep1", "reduce", "sweep2", "walk"))
-    ghz = tot_cyc / (r["blocks"] * 4) / (r["ms"] * 1e-3) / 1e9     # s_memtime ticks per second
+    # shader clock: the waves' s_memtime cycles over their s_memrealtime ticks
+    # (100 MHz), MI355X_MICROARCH.md's in-kernel clock (round 4 divided by the
+    # launch's duration x its waves, which assumed every wave ran the whole
+    # launch: 1.94 GHz, too low)
+    ghz = tot_cyc / r["rt"] * 0.1 if r.get("rt") else None
     out = {"kernel": "nw16_kernel", "form": int(r["k"]), "what": "first-sweep fast loop, chip full, kernel alone",
            "pairs": int(r["cand"]), "xlen": a.xlen, "ylen": a.ylen, "G": G, "GPW": GPW, "tasks": tasks,
            "valu_per_iteration": a.valu, "waves_per_simd": a.waves_per_simd,
            "cycles_per_iteration_per_wave": round(cyc_iter, 1),
            "cycles_per_valu_per_simd": round(cyc_iter / (a.waves_per_simd * a.valu), 3),
            "simd_valu_rate": round(rate, 4), "mix_ceiling_frac": round(rate / 0.5, 4),
-           "sweep1_share": round(r["sweep1"] / tot, 4), "kernel_ms": r["ms"], "memtime_ghz": round(ghz, 3),
-           "cells_per_s": round(a.pairs * a.xlen * a.ylen / (r["ms"] / 1e3), 1),
+           "sweep1_share": round(r["sweep1"] / tot, 4), "kernel_ms": r["ms"],
+           "shader_clock_ghz": round(ghz, 3) if ghz else None,
+           # not comparable with the bench's cells/s: the micro's candidates
+           # carry no predicted window, so every one takes a second sweep
+           "micro_cells_per_s_no_windows": round(a.pairs * a.xlen * a.ylen / (r["ms"] / 1e3), 1),
            "raw": runs}
     s = json.dumps(out, indent=1)
     print(s)
