@@ -320,6 +320,7 @@ struct imsame_ctx {
     // candidates
     DBuf cread, csid, cread2, csid2, cout, cout2;
     DBuf crow, cperm, rhist;          // predicted rows of class-0 candidates, their launch order
+    DBuf cperm_b, rhist_b;            // ... of round 1b's launch (it runs beside round 1's)
     // scalars (one block of u64 counters)
     DBuf ctr;
     // tables (and the inputs they were built for)
@@ -398,7 +399,7 @@ static inline const uint64_t *dev_qs(const imsame_ctx *c) {
 // counters block layout (u64 slots)
 enum { C_NCAND = 0, C_NCAND2, C_NNEXT, C_NCANDB, C_NCAND2B, C_NNEXT2, C_WORKB,   // (round 1b: B, 2)
        C_WORK, C_WORK2, C_PATHS, C_FLAGS, C_ERR, C_HITS, C_CELLS, C_NACC, C_REDO,
-       C_PROF, C_WIN = C_PROF + 6, C_FBK, C_SWORK, C_DBG = C_SWORK + 3, C_WASTE = C_DBG + 8,
+       C_PROF, C_WIN = C_PROF + 12, C_FBK, C_SWORK, C_DBG = C_SWORK + 3, C_WASTE = C_DBG + 8,
        C_NSLOTS };
 
 static double now_ms() {
@@ -645,7 +646,8 @@ extern "C" void imsame_dev_close(imsame_ctx *c) {
                     &c->act1, &c->cread, &c->csid, &c->cread2, &c->csid2, &c->cout, &c->cout2, &c->ctr,
                     &c->minraw, &c->minlen, &c->minident, &c->tb, &c->bnd, &c->paths, &c->ck, &c->rc_in, &c->rc_out,
                     &c->rc_a, &c->rc_b, &c->rc_c, &c->cbase, &c->ccnt, &c->perr, &c->wcap, &c->wout, &c->wstart,
-                    &c->crow, &c->cperm, &c->rhist, &c->act2, &c->slotbits, &c->np_tb, &c->np_ck, &c->dbw, &c->qw};
+                    &c->crow, &c->cperm, &c->rhist, &c->act2, &c->slotbits, &c->np_tb, &c->np_ck, &c->dbw, &c->qw,
+                    &c->cperm_b, &c->rhist_b};
     for (DBuf *b : bufs) b->release();
     (void)hipEventDestroy(c->ev0);
     (void)hipEventDestroy(c->ev1);
@@ -1332,14 +1334,15 @@ static int launch_nw(imsame_ctx *c, NwPlan &pl, const uint32_t *cread, const uin
     if (crow && pl.two && n >= 64) {
         // queue order by predicted row (first-sweep traceback windows)
         const uint32_t nb = ((uint32_t)pl.xcap + 512) / 8 + 2;
-        if (c->cperm.ensure((uint64_t)n * 4) || c->rhist.ensure((uint64_t)nb * 8)) return IMSAME_E_OOM;
-        uint32_t *hist = c->rhist.as<uint32_t>(), *cur = hist + nb;
+        DBuf &cperm = qi ? c->cperm_b : c->cperm, &rhist = qi ? c->rhist_b : c->rhist;
+        if (cperm.ensure((uint64_t)n * 4) || rhist.ensure((uint64_t)nb * 8)) return IMSAME_E_OOM;
+        uint32_t *hist = rhist.as<uint32_t>(), *cur = hist + nb;
         HIPCHK(hipMemsetAsync(hist, 0, (size_t)nb * 4, s));
         row_hist_kernel<<<nblk(n, 256), 256, 0, s>>>(crow, n, nb, hist);
         row_scan_kernel<<<1, 1024, 0, s>>>(hist, nb, cur);
-        row_scatter_kernel<<<nblk(n, 256), 256, 0, s>>>(crow, n, nb, cur, c->cperm.as<uint32_t>());
+        row_scatter_kernel<<<nblk(n, 256), 256, 0, s>>>(crow, n, nb, cur, cperm.as<uint32_t>());
         HIPCHK(hipGetLastError());
-        P.perm = c->cperm.as<uint32_t>(); P.cand_row = crow;
+        P.perm = cperm.as<uint32_t>(); P.cand_row = crow;
         const char *wu = getenv("IMSAME_NW_WIN_UP"), *wd = getenv("IMSAME_NW_WIN_DOWN");
         P.win_up = wu ? atoi(wu) : NW16_WIN_UP; P.win_down = wd ? atoi(wd) : NW16_WIN_DOWN;
         const char *wb = getenv("IMSAME_NW_WIN_BOTTOM");
@@ -1504,7 +1507,8 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     if (poison_on()) {                        // this call's scratch holds nothing it may read
         const DBuf *scr[] = {&c->res, &c->cur_p, &c->cur_h, &c->memo, &c->nmemo, &c->rstat, &c->act0, &c->act1, &c->act2,
                              &c->cread, &c->csid, &c->cread2, &c->csid2, &c->cout, &c->cout2, &c->cbase, &c->ccnt,
-                             &c->perr, &c->crow, &c->cperm, &c->rhist, &c->paths, &c->tb, &c->ck, &c->bnd};
+                             &c->perr, &c->crow, &c->cperm, &c->rhist, &c->cperm_b, &c->rhist_b, &c->paths, &c->tb,
+                             &c->ck, &c->bnd};
         for (const DBuf *b : scr)
             if ((rc = b->poison(s))) return rc;
     }
@@ -1555,7 +1559,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         S.next = nxt; S.nnext = (uint32_t *)(ctr + C_NNEXT);
         S.cbase = c->cbase.as<uint32_t>(); S.ccnt = c->ccnt.as<uint32_t>(); S.perr = c->perr.as<uint32_t>();
         S.cread = c->cread.as<uint32_t>(); S.csid = c->csid.as<uint32_t>(); S.ncand = (uint32_t *)(ctr + C_NCAND);
-        S.crow = crow;
+        S.crow = crow; S.weak_rows = RP.weak_rows;
         S.cread2 = c->cread2.as<uint32_t>(); S.csid2 = c->csid2.as<uint32_t>(); S.ncand2 = (uint32_t *)(ctr + C_NCAND2);
         S.err = (unsigned long long *)(ctr + C_ERR); S.nhits = (unsigned long long *)(ctr + C_HITS);
         S.nwork = (unsigned long long *)(ctr + C_SWORK);
@@ -1656,7 +1660,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
             Sb.budget = RP.r1b_budget();
             Sb.next = act2; Sb.nnext = (uint32_t *)(ctr + C_NNEXT2);
             Sb.cread = c->cread.as<uint32_t>() + n1; Sb.csid = c->csid.as<uint32_t>() + n1;
-            Sb.ncand = (uint32_t *)(ctr + C_NCANDB); Sb.crow = nullptr;
+            Sb.ncand = (uint32_t *)(ctr + C_NCANDB); Sb.crow = crow && RP.r1b_rows ? crow + n1 : nullptr;
             Sb.ncand2 = (uint32_t *)(ctr + C_NCAND2B);
             Sb.dbg = nullptr;
             if ((rc = seed_launch(Sb, npz, sb, c->evb0, c->evb1))) return rc;
@@ -1692,7 +1696,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
                 rc = launch_nw(c, plb, c->cread.as<uint32_t>() + n1, c->csid.as<uint32_t>() + n1, nb,
                                c->cout.as<imsame_read_result>() + n1, p->igap, p->egap, p, ymax, xcap,
                                (uint32_t *)(ctr + C_WORKB), c->db.as<uint8_t>(), c->db_start.as<uint64_t>(), qd, qsd,
-                               pcap, &msb, nullptr, 1, false);
+                               pcap, &msb, Sb.crow, 1, false);
                 if (rc) return rc;
                 if ((rc = upd_launch(c->cread.as<uint32_t>() + n1, c->csid.as<uint32_t>() + n1, nb,
                                      c->cout.as<imsame_read_result>() + n1, act2, C_NNEXT2, sb))) return rc;
@@ -1782,8 +1786,11 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         // shader clock under this load: the waves' cycles over their 100 MHz real time
         const double ghz = hc[C_PROF + 5] ? tot / (double)hc[C_PROF + 5] * 0.1 : 0.0;
         fprintf(stderr, "[nwprof] setup %.3f sweep1 %.3f reduce %.3f sweep2 %.3f walk %.3f (fractions of %.4g wave-cycles) "
-                "clock_ghz %.3f\n", hc[C_PROF] / tot, hc[C_PROF + 1] / tot, hc[C_PROF + 2] / tot, hc[C_PROF + 3] / tot,
-                hc[C_PROF + 4] / tot, tot, ghz);
+                "clock_ghz %.3f best_cells(weak: last_row last_col<=40 <=200 higher | predicted: in out) "
+                "%llu %llu %llu %llu | %llu %llu\n", hc[C_PROF] / tot, hc[C_PROF + 1] / tot, hc[C_PROF + 2] / tot,
+                hc[C_PROF + 3] / tot, hc[C_PROF + 4] / tot, tot, ghz, (unsigned long long)hc[C_PROF + 6],
+                (unsigned long long)hc[C_PROF + 7], (unsigned long long)hc[C_PROF + 8], (unsigned long long)hc[C_PROF + 9],
+                (unsigned long long)hc[C_PROF + 10], (unsigned long long)hc[C_PROF + 11]);
     }
     st.nw_launch_ms = st.nw_launches ? st.ms_nw / st.nw_launches : 0;
     st.nw_bytes = 2 * st.nw_cells;       // 2 B/cell traceback floor; bench.py adds xlen + ylen per NW

@@ -552,6 +552,22 @@ __device__ __forceinline__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const
             else          { bscore[h] = bC; bx[h] = bCi; by[h] = yl[h] - 1; }
         }
         wv_lds_sync();
+        // diagnostics (P.prof): where the best cells lie -- unpredicted (weak)
+        // candidates: [6] last row, [7] last column within 40 rows of the
+        // bottom (the window), [8] within 200, [9] higher; predicted ones:
+        // [10] inside their window, [11] outside
+        if (P.prof && in_group && gl == 0)
+            for (int h = 0; h < 2; ++h) {
+                if (!valid[h]) continue;
+                int b;
+                if (prow[h] == NW16_NOROW) {
+                    const int up = xl[h] - 1 - bx[h];
+                    b = up == 0 ? 6 : up <= 40 ? 7 : up <= 200 ? 8 : 9;
+                } else {
+                    b = (bx[h] >= prow[h] - P.win_up && bx[h] <= prow[h] + yl[h] - 1 + P.win_down) ? 10 : 11;
+                }
+                wv_atomic_add64(P.prof + b, 1ull);
+            }
         mark(2);
         if (!TWO) {
             for (int h = 0; h < 2; ++h) {

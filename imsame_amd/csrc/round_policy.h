@@ -24,6 +24,8 @@ struct RoundPolicy {
     int nlanes = 1;                  // lanes of the call: the device scans nlanes x na reads at once
     bool r1b_on = true;              // round 1b (short reads only)
     bool window = true;              // predicted traceback windows of the packed NW kernel
+    bool weak_rows = false;          // ... predicted from weak hits too (IMSAME_NW_WEAK_ROWS)
+    bool r1b_rows = false;           // ... for round 1b's candidates (IMSAME_NW_R1B_ROWS)
 
     // A lane's call of n reads whose longest is ycap (short reads: <= short_y).
     // Environment overrides (A/B runs, tests): IMSAME_SPEC_WEAK, IMSAME_CCAP_MULT,
@@ -68,6 +70,9 @@ struct RoundPolicy {
         // 1b they take C2's NW busy time from 113.4 to 107.4 ms, profiles/r4d/)
         const char *wi = getenv("IMSAME_NW_WINDOW");
         r.window = !(wi && !atoi(wi));
+        const char *wr = getenv("IMSAME_NW_WEAK_ROWS"), *br = getenv("IMSAME_NW_R1B_ROWS");
+        r.weak_rows = wr && atoi(wr);
+        r.r1b_rows = br && atoi(br);
         return r;
     }
     // lanes per read of round `round`'s scan of na reads: from the reads the

@@ -49,6 +49,7 @@ struct SeedLaunch {
     uint32_t *cread, *csid, *ncand;        // class 0: ylen <= short_ylen
     int32_t *crow;                         // class 0: the record row of the read's first base by the
                                            // hit that made the candidate (INT32_MIN: none; NULL: off)
+    bool weak_rows = false;                // ... for weak hits too (predicted_row)
     uint32_t *cread2, *csid2, *ncand2;     // class 1: longer reads
     unsigned long long *err;               // min (read << 32 | record)
     unsigned long long *nhits;
@@ -274,8 +275,9 @@ __device__ __forceinline__ bool read_irrelevant(const SeedLaunch &S, uint64_t yl
 // Appendix A Q6).  A weak hit gets no prediction: its NW takes the second
 // sweep, and it does not widen the window of the true hits' wave.
 __device__ __forceinline__ bool weak_hit(uint64_t raw, uint64_t ylen) { return 3 * raw < 7 * ylen; }
-__device__ __forceinline__ int32_t predicted_row(uint64_t raw, uint64_t ylen, int64_t rec_pos, int64_t read_pos) {
-    return weak_hit(raw, ylen) ? INT32_MIN : (int32_t)(rec_pos - read_pos);
+__device__ __forceinline__ int32_t predicted_row(uint64_t raw, uint64_t ylen, int64_t rec_pos, int64_t read_pos,
+                                                bool weak_rows = false) {
+    return (!weak_rows && weak_hit(raw, ylen)) ? INT32_MIN : (int32_t)(rec_pos - read_pos);
 }
 // Speculation from the first candidate on: a read whose first e-value pass is
 // weak (a random read's, by the idents quirk) will most likely see it
@@ -366,7 +368,7 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, Seed
                 }
                 if (nw_cannot_accept(S, xlen, ylen)) continue;       // NW would reject it
                 if (ne == 0) {
-                    row0 = predicted_row(raw, ylen, ent.x, (int64_t)(p + 1 - rs));
+                    row0 = predicted_row(raw, ylen, ent.x, (int64_t)(p + 1 - rs), S.weak_rows);
                     spec = spec_after_first(S, spec, nm, raw, ylen);
                 }
                 emit[ne++] = sid;
@@ -581,7 +583,7 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
         const int64_t xe = (ent.y == S.n_db - 1) ? (int64_t)S.db_len : (int64_t)S.db_start[ent.y + 1] - 1;
         const uint64_t raw = ungapped_raw(S.dbw, S.qw, xs + ent.x, (int64_t)(rs + e0p) + 1, xs, xe, ys, ye,
                                           (int64_t)S.db_len, (int64_t)S.q_len);
-        S.crow[o] = predicted_row(raw, ylen, ent.x, (int64_t)e0p + 1);
+        S.crow[o] = predicted_row(raw, ylen, ent.x, (int64_t)e0p + 1, S.weak_rows);
         for (uint32_t m = 1; m < ne; ++m) S.crow[o + m] = INT32_MIN;
     }
     S.cbase[k] = o; S.ccnt[k] = ne;

@@ -401,7 +401,7 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
         S.budget = RP.budget(rnd);
         S.next = nxt.data(); S.nnext = &nc[2];
         S.cbase = cbase.data(); S.ccnt = ccnt.data(); S.perr = perr.data();
-        S.cread = cr.data(); S.csid = cs.data(); S.ncand = &nc[0]; S.crow = crowp;
+        S.cread = cr.data(); S.csid = cs.data(); S.ncand = &nc[0]; S.crow = crowp; S.weak_rows = RP.weak_rows;
         S.cread2 = cr2.data(); S.csid2 = cs2.data(); S.ncand2 = &nc[1];
         S.err = &err; S.nhits = &nhits;
         auto run_seed = [&](const SeedLaunch &SL, uint32_t na) {
@@ -467,12 +467,13 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
             Sb.spec_weak = RP.r1b_spec_weak(n1, npz);
             Sb.budget = RP.r1b_budget();
             Sb.next = act2.data(); Sb.nnext = &nb[2];
-            Sb.cread = cr.data() + n1; Sb.csid = cs.data() + n1; Sb.ncand = &nb[0]; Sb.crow = nullptr;
+            Sb.cread = cr.data() + n1; Sb.csid = cs.data() + n1; Sb.ncand = &nb[0];
+            Sb.crow = crowp && RP.r1b_rows ? crowp + n1 : nullptr;
             Sb.ncand2 = &nb[1];
             run_seed(Sb, npz);
             if (nb[1]) return IMSAME_E_STATE;
             if (n1) nw_upd(cr.data(), cs.data(), n1, o1.data(), short_y, crowp, act2.data(), &nb[2]);
-            if (nb[0]) nw_upd(cr.data() + n1, cs.data() + n1, nb[0], o1.data() + n1, short_y, nullptr, act2.data(), &nb[2]);
+            if (nb[0]) nw_upd(cr.data() + n1, cs.data() + n1, nb[0], o1.data() + n1, short_y, Sb.crow, act2.data(), &nb[2]);
             g_r1b += npz;
             if (getenv("IMSAME_DEBUG_ROUNDS"))
                 fprintf(stderr, "[emu round 1b] paused=%u cand=%u+%u next=%u\n", npz, n1, nb[0], nb[2]);

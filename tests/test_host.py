@@ -241,8 +241,8 @@ def test_emulated_k19_form(emu, oracle, band, monkeypatch):
                 assert paths[res[k]["path_off"]:res[k]["path_off"] + res[k]["path_len"]].tolist() == want, (key, k)
 
 
-@pytest.mark.parametrize("seed_l", ["1", "4"])
-def test_emulated_predicted_traceback_window(emu, oracle, seed_l, monkeypatch):
+@pytest.mark.parametrize("seed_l,weak_rows", [("1", "0"), ("4", "0"), ("1", "1"), ("4", "1")])
+def test_emulated_predicted_traceback_window(emu, oracle, seed_l, weak_rows, monkeypatch):
     """nw16_kernel.hip's predicted window (emulated pipeline): the strong seed
     hit's diagonal (seed_one, or seed_group's re-derivation) orders the queue
     (8-row buckets) and the first sweep writes the traceback of each wave's
@@ -254,6 +254,7 @@ def test_emulated_predicted_traceback_window(emu, oracle, seed_l, monkeypatch):
     from tests import synth
     monkeypatch.setenv("IMSAME_SEED_L", seed_l)
     monkeypatch.setenv("IMSAME_NW_WINDOW", "1")       # (imsame_dev.hip: on by default)
+    monkeypatch.setenv("IMSAME_NW_WEAK_ROWS", weak_rows)   # weak hits predict rows too
     win = emu.lib.emu_win_count
     win.restype = C.c_uint32
     ref, rst = synth.make_reference_arr(240_000, 700, seed=61)
@@ -275,8 +276,9 @@ def test_emulated_predicted_traceback_window(emu, oracle, seed_l, monkeypatch):
         assert np.array_equal(got0[f], exp[f]), f
 
 
-@pytest.mark.parametrize("r1b,seed_l", [("1", ""), ("0", ""), ("1", "64"), ("0", "64")])
-def test_emulated_round1b(emu, oracle, r1b, seed_l, monkeypatch):
+@pytest.mark.parametrize("r1b,seed_l,rows", [("1", "", "0"), ("0", "", "0"), ("1", "64", "0"), ("0", "64", "0"),
+                                             ("1", "", "1"), ("1", "64", "1")])
+def test_emulated_round1b(emu, oracle, r1b, seed_l, rows, monkeypatch):
     """Round 1b (imsame_dev.hip:align_one): reads that round 1 paused without
     a candidate (random reads against a 20 Mbp database spend the 32-hit
     budget) scan on at once with weak-first speculation, before round 1's
@@ -286,6 +288,8 @@ def test_emulated_round1b(emu, oracle, r1b, seed_l, monkeypatch):
     up to SPEC_BIG candidates per read in the later rounds."""
     from tests import synth
     monkeypatch.setenv("IMSAME_ROUND1B", r1b)
+    monkeypatch.setenv("IMSAME_NW_R1B_ROWS", rows)        # round 1b's launch ordered by predicted rows,
+    monkeypatch.setenv("IMSAME_NW_WEAK_ROWS", rows)       # weak hits predicting them too
     if seed_l:          # whole-wave groups, which emit up to SPEC_BIG per read after round 1
         monkeypatch.setenv("IMSAME_SEED_L", seed_l)
         monkeypatch.delenv("IMSAME_SPEC", raising=False)
