@@ -1968,7 +1968,7 @@ static int align_impl(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint6
     // moment and leave the chip idle together; x = 0.4 for 8 lanes (C2: +0.7 %
     // over four alternating pairs, profiles/r2ap_*, r2aq_*), IMSAME_LANE_SKEW
     const char *ske = getenv("IMSAME_LANE_SKEW");
-    const double skew = ske ? std::max(0.0, std::min(0.9, atof(ske))) : (nl >= 8 ? 0.4 : 0.0);
+    const double skew = ske ? std::max(-0.9, std::min(0.9, atof(ske))) : (nl >= 8 ? 0.4 : 0.0);
     {
         std::vector<double> w(np), acc(np + 1, 0.0);
         for (int i = 0; i < np; ++i) w[i] = 1.0 + skew * (nl > 1 ? 2.0 * (i % nl) / (nl - 1) - 1.0 : 0.0);
