@@ -74,9 +74,14 @@ __device__ __forceinline__ void seed_outcome(const SeedLaunch &S, uint32_t ne, b
 // so a random read with more than SPEC_MAX live e-value passes needs no
 // extra round of one read (its NW alone is ~0.6 ms of a 2000-row record)
 #define SPEC_BIG 32
-// speculation width from a weak first candidate on (spec_after_first); 1 = off
+// speculation width from a weak first candidate on (spec_after_first); 1 = off.
+// 8: a read whose first e-value pass is weak (a random read's, by the idents
+// quirk) emits up to 8 in round 1 instead of one -- C3 400.1 -> 393.6 ms (6
+// rounds instead of 7, 2.85 NW per read instead of 2.88), C2 1/8 and 1/4
+// shards 16.60 -> 16.34 and 30.08 -> 29.73 ms, C2 106.3 ms either way
+// (profiles/r5q/, r5r/)
 #ifndef SPEC_WEAK
-#define SPEC_WEAK 1
+#define SPEC_WEAK 8
 #endif
 // Hit budget per read and round: round 1 lets a read run SEED_BUDGET1
 // ungapped extensions (true reads accept within a few), each later round 8x
