@@ -457,7 +457,7 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "reads/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": a.scaling, "vs_baseline": None,
-            "dtype": "int16" if kernel == "nw16_kernel" else "int32", "data": "synthetic",
+            "dtype": "int16" if kernel in ("nw16_kernel", "nwp_kernel") else "int32", "data": "synthetic",
             "config": {"workload": cfg["workload"] + (f"; {a.reads} reads total over {world} GPU(s), contiguous "
                                                       f"shards" if strong else f"; {a.reads} reads per GPU")
                        + (f"; database searched in {n_slices} slices of <= {a.slice_bases} bases"

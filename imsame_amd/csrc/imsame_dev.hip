@@ -298,8 +298,9 @@ struct imsame_ctx {
     // the starts of reads q_lo .. q_hi.  Kernels index both with GLOBAL read
     // and base numbers through the biased views dev_q / dev_qs.
     DBuf q, q_start;
-    DBuf qw;                          // the uploaded bases 2-bit packed, from word qw_base = q_base >> 4
-    uint64_t qw_base = 0;
+    DBuf qw;                          // the uploaded bases 2-bit packed, words [qw_base, qw_end) (each
+    uint64_t qw_base = 0, qw_end = 0; // lane packs the words its reads use, align_one)
+    uint64_t qb_end = 0;              // end of the uploaded bytes (the 64 zero bytes included)
     uint64_t n_q = 0, q_len = 0, q_lo = 0, q_hi = 0, q_base = 0, q_lo_first = 0;
     uint64_t *h_q_start = nullptr;    // starts of reads q_lo .. q_hi, page-locked (the
     uint64_t h_q_cap = 0;             // H2D copy of them runs asynchronously)
@@ -311,7 +312,6 @@ struct imsame_ctx {
     // bases below q_part_end[k] and is complete when q_part_ev[k] fires (the
     // starts go first, with part 0); a lane borrows its parent's events
     std::vector<hipEvent_t> q_part_ev;
-    std::vector<hipEvent_t> q_copy_ev;   // part k's bytes copied (its packing waits for it)
     std::vector<uint64_t> q_part_end;
     bool q_len_mult = false;         // every read length is a multiple of NW16_K
     uint32_t q_len_uni = 0;          // the one read length of the uploaded range (0: lengths differ)
@@ -635,7 +635,6 @@ extern "C" void imsame_dev_close(imsame_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->ustream) (void)hipStreamSynchronize(c->ustream);    // before the lane that may own it goes
-    if (c->stream_b) (void)hipStreamSynchronize(c->stream_b);
     if (!c->ustream_own) c->ustream = nullptr;
     for (imsame_ctx *l : c->subs) { lane_unalias(l); imsame_dev_close(l); }
     c->subs.clear();
@@ -659,8 +658,6 @@ extern "C" void imsame_dev_close(imsame_ctx *c) {
     if (c->origin && !c->is_sub) (void)hipEventDestroy(c->origin);     // a lane borrows its parent's
     if (!c->is_sub)
         for (hipEvent_t e : c->q_part_ev) (void)hipEventDestroy(e);
-    if (!c->is_sub)
-        for (hipEvent_t e : c->q_copy_ev) (void)hipEventDestroy(e);
     if (!c->is_sub && c->h_q_start) (void)hipHostFree(c->h_q_start);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->ustream && c->ustream_own) (void)hipStreamDestroy(c->ustream);
@@ -676,7 +673,7 @@ static int lane_sub(imsame_ctx *c, int k, imsame_ctx **out) {
     }
     imsame_ctx *l = c->subs[k - 1];
     l->db = c->db; l->db_start = c->db_start; l->off = c->off; l->ent = c->ent; l->q = c->q; l->q_start = c->q_start;
-    l->dbw = c->dbw; l->qw = c->qw; l->qw_base = c->qw_base;
+    l->dbw = c->dbw; l->qw = c->qw; l->qw_base = c->qw_base; l->qw_end = c->qw_end; l->qb_end = c->qb_end;
     l->n_db = c->n_db; l->db_len = c->db_len; l->n_ent = c->n_ent; l->max_rec = c->max_rec;
     l->have_index = c->have_index;
     l->n_q = c->n_q; l->q_len = c->q_len; l->q_lo = c->q_lo; l->q_hi = c->q_hi; l->q_base = c->q_base;
@@ -814,7 +811,6 @@ extern "C" int imsame_dev_set_query_range_async(imsame_ctx *c, const uint8_t *q_
     if (n_q >= 0xFFFFFFF0ull) return IMSAME_E_ARG;
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->ustream));    // a previous upload may still read h_q_start / fill q
-    if (c->stream_b) HIPCHK(hipStreamSynchronize(c->stream_b));  // ... or pack q
     c->have_query = false;
     auto qs = [&](uint64_t r) { return r < n_q ? q_start[r] : q_len; };
     // one pass over the shard's starts: ascending within the query (else
@@ -891,11 +887,6 @@ extern "C" int imsame_dev_set_query_range_async(imsame_ctx *c, const uint8_t *q_
     const uint64_t qw_end = (c->q_base + nb + 64) / 16 + 2;
     if (c->q.ensure(nb + 64) || c->q_start.ensure(ns * 8) || c->qw.ensure((qw_end - c->qw_base) * 4))
         return IMSAME_E_OOM;
-    while (c->q_copy_ev.size() < Q_PARTS) {
-        hipEvent_t e;
-        HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        c->q_copy_ev.push_back(e);
-    }
     while (c->q_part_ev.size() < Q_PARTS) {
         hipEvent_t e;
         HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -906,32 +897,19 @@ extern "C" int imsame_dev_set_query_range_async(imsame_ctx *c, const uint8_t *q_
     // only for the parts that hold its reads
     HIPCHK(hipMemcpyAsync(c->q_start.p, c->h_q_start, ns * 8, hipMemcpyHostToDevice, c->ustream));
     HIPCHK(hipMemsetAsync((uint8_t *)c->q.p + nb, 0, 64, c->ustream));
-    // The packed copy (seed_kernel.hip:pk_word) is made part by part on a
-    // second stream (this context's round-1b stream, idle between calls), so
-    // the copies run back to back on the upload stream while each part's
-    // packing follows its copy; a part is ready (q_part_ev) once packed.
-    hipStream_t ps = c->stream_b ? c->stream_b : c->ustream;
-    uint64_t wdone = c->qw_base;                         // packed words written so far
+    // (the packed copy the seed scan reads, qw, is made by each lane over its
+    // own reads once their parts are in HBM: align_one)
+    c->qw_end = qw_end; c->qb_end = c->q_base + nb + 64;
     for (uint64_t k = 0, a = 0; k < Q_PARTS; ++k) {      // bases [q_base + a, q_base + b)
         const uint64_t b = nb * (k + 1) / Q_PARTS;
         if (b > a) HIPCHK(hipMemcpyAsync((uint8_t *)c->q.p + a, q_seq + c->q_base + a, b - a, hipMemcpyHostToDevice,
                                          c->ustream));
-        HIPCHK(hipEventRecord(c->q_copy_ev[k], c->ustream));
-        if (ps != c->ustream) HIPCHK(hipStreamWaitEvent(ps, c->q_copy_ev[k], 0));
-        // the packed words whose bases are all in HBM now (the last part: all,
-        // with the 64 zero bytes past the range)
-        const uint64_t wend = k + 1 == Q_PARTS ? qw_end : (c->q_base + b) / 16;
-        if (wend > wdone)
-            pack2_kernel<<<gsblk(wend - wdone, 256), 256, 0, ps>>>(
-                dev_q(c), (int64_t)c->q_base, (int64_t)(c->q_base + nb + 64), (uint32_t *)dev_qw(c), wdone, wend);
-        wdone = std::max(wdone, wend);
-        HIPCHK(hipEventRecord(c->q_part_ev[k], ps));
+        HIPCHK(hipEventRecord(c->q_part_ev[k], c->ustream));
         c->q_part_end[k] = c->q_base + b;
         a = b;
     }
     c->have_query = true;
     POISON_SYNC(c->ustream, "query upload", c);
-    POISON_SYNC(ps, "query packing", c);
     return IMSAME_OK;
 }
 
@@ -949,7 +927,6 @@ extern "C" int imsame_dev_sync(imsame_ctx *c) {
     if (!c) return IMSAME_E_ARG;
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->ustream));
-    if (c->stream_b) HIPCHK(hipStreamSynchronize(c->stream_b));     // the upload's packing
     HIPCHK(hipStreamSynchronize(c->stream));
     return IMSAME_OK;
 }
@@ -1468,6 +1445,27 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     const uint32_t n = (uint32_t)(read_to - read_from);
     // this lane's bases (and the 16-byte chunk loads' reach past its last read)
     if (int rq = query_wait(c, s, hqs(c, read_to) + 64)) return rq;
+    // ... and their packed copy (seed_kernel.hip:pk_word): the words from QPAD
+    // bases before its first read to the end of its last part.  Each lane
+    // packs its own on its stream as its parts arrive (packing in the upload
+    // delayed every lane: the upload's kernels waited for free CUs behind NW
+    // waves, profiles/r5t/); neighbouring lanes both write the few words where
+    // their reaches meet, with the same values.
+    // Words are packed only where all 16 of their bytes are in HBM (below the
+    // end of the part waited for): a word at the edge of a part that is still
+    // copying would get garbage in the slots a neighbouring lane reads.
+    {
+        const uint64_t b0 = hqs(c, read_from), b1 = hqs(c, read_to) + 64;
+        uint64_t pe = c->qb_end;                          // end of the part query_wait waited for
+        for (size_t k = 0; k + 1 < c->q_part_end.size(); ++k)
+            if (c->q_part_end[k] >= b1) { pe = c->q_part_end[k]; break; }
+        const uint64_t w0 = std::max(c->qw_base, (b0 > QPAD ? b0 - QPAD : 0) / 16);
+        const uint64_t w1 = pe == c->qb_end ? c->qw_end : std::min(c->qw_end, pe / 16);
+        if (w1 > w0)
+            pack2_kernel<<<gsblk(w1 - w0, 256), 256, 0, s>>>(dev_q(c), (int64_t)c->q_base, (int64_t)c->qb_end,
+                                                             (uint32_t *)dev_qw(c), w0, w1);
+        HIPCHK(hipGetLastError());
+    }
     imsame_stats st;
     memset(&st, 0, sizeof st);
     st.n_reads = n;
