@@ -44,6 +44,8 @@ run_step() {   # $1 = step, $2 = output suffix
     # C3 with the oracle as the checker on 3 windows (parity + NW accounting) and the port as CPU baseline
     c3p) timeout -k 10 1100 python -u bench.py --config c3 --steps 2 --e2e off --cpu-kind port > $O/bench_c3p_${TAG}$X.json \
            2> $O/bench_c3p_${TAG}$X.err; ok_or_stop $? c3p$X ;;
+    c5) timeout -k 10 900 python -u bench.py --config c5 --steps 2 --warmup 1 > $O/bench_c5_${TAG}$X.json \
+           2> $O/bench_c5_${TAG}$X.err; ok_or_stop $? c5$X ;;
     c5w) timeout -k 10 900 python -u bench.py --config c5w --steps 1 --warmup 0 > $O/bench_c5w_${TAG}$X.json \
            2> $O/bench_c5w_${TAG}$X.err; ok_or_stop $? c5w$X ;;
     shard*) SH=${s#shard}; timeout -k 10 600 ${PINCMD:-} python -u bench.py $BQ --shard ${SH/_//} --steps 10 --warmup 2 \
