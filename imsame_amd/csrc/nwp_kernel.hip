@@ -58,6 +58,29 @@
 #define NWP_G    (4 * 64 + 64)            // how far a T moves within a 64-step block (+4 per step; column 0: +-44)
 #define NWP_S2   2308                     // nwp_fits: the T spread it budgets
 
+#ifdef IMSAME_WAVE_EMU
+// Emulator only: the block-start bound above is a proof about the steps
+// inside a block; the emulator checks its conclusion at every step.  Each
+// packed operation whose result a live cell uses (rows [1, xlen), columns
+// [1, ylen) of that half) is checked for int16 wrap in that half:
+// tests/emu/wave_emu.cpp counts the violations (emu_nwp_range_violations).
+extern std::atomic<uint64_t> g_nwp_viol;
+static inline void nwp_chk(unsigned live, int kind, uint32_t a, uint32_t b) {
+    for (int h = 0; h < 2; ++h) {
+        if (!(live >> h & 1u)) continue;
+        const int ua = (int)(h ? a >> 16 : a & 0xFFFFu), ub = (int)(h ? b >> 16 : b & 0xFFFFu);
+        bool bad;
+        if (kind == 0) { const int s = ua + (int)(int16_t)ub; bad = s < 0 || s > 0xFFFF; }   // pk_add, b signed
+        else if (kind == 1) { const int d = ua - ub; bad = d < -32768 || d > 32767; }        // pk_sub -> sign
+        else bad = ua < ub;                                                                  // biased decrement
+        if (bad) g_nwp_viol.fetch_add(1, std::memory_order_relaxed);
+    }
+}
+#define NWP_CHK(live, kind, a, b) nwp_chk(live, kind, a, b)
+#else
+#define NWP_CHK(live, kind, a, b) ((void)0)
+#endif
+
 // |ig| + |eg| (L + 64): the drift bound of the launch (NwLaunch::rlim)
 __host__ static inline int64_t nwp_rlim(int64_t ig, int64_t eg, uint64_t xcap, uint64_t ymax) {
     return -ig + -eg * (int64_t)(std::max<uint64_t>(xcap, ymax) + 64);
@@ -266,6 +289,25 @@ __device__ void nwp_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const 
             const uint32_t sN = pk_add((uint32_t)wv_shr1_fill((int)outT, (int)R0), dl);
             const uint32_t mS = pk_add((uint32_t)wv_shr1_fill((int)outMS, (int)R1), dl);
             const uint32_t mL0 = pk_add((uint32_t)wv_shr1_fill((int)outL, (int)R2), dl);
+#ifdef IMSAME_WAVE_EMU
+            // the halves whose cell (i, j0 + s) is live
+            auto live = [&](int s) {
+                unsigned m = 0;
+                for (int h = 0; h < 2; ++h) {
+                    const int j = st * NWP_W + lane * K + s;
+                    const int ii = t - lane;
+                    m |= (unsigned)(ii >= 1 && ii < xl[h] && j >= 1 && j < yl[h]) << h;
+                }
+                return m;
+            };
+            {   // (the exchanges are lock-step: every lane makes them)
+                const uint32_t sT = (uint32_t)wv_shr1_fill((int)outT, (int)R0),
+                               sM = (uint32_t)wv_shr1_fill((int)outMS, (int)R1),
+                               sL = (uint32_t)wv_shr1_fill((int)outL, (int)R2);
+                const unsigned l0m = live(0), l1m = (st == 0 && lane == 1) ? 0u : l0m;  // column 1: column 0's sentinels
+                NWP_CHK(l0m, 0, sT, dl); NWP_CHK(l1m, 0, sM, dl); NWP_CHK(l1m, 0, sL, dl);
+            }
+#endif
             R0 = R0n; R1 = R1n; R2 = R2n;
             const uint32_t xqn = (uint32_t)wv_shl1((int)xq);
             xs = (uint32_t)wv_shr1_fill((int)xs, (int)xq);
@@ -282,6 +324,18 @@ __device__ void nwp_wave(const NwLaunch &P, uint8_t *wsm, const int lane, const 
                 const uint32_t sc = wv_perm(NW16_TBL_HI, NW16_TBL_LO, xs ^ yreg[s]);
                 const uint32_t up = row1 ? NBIG : u0[s];
                 const uint32_t lu = pk_maxu(l0, up), m = pk_maxu(d0, lu);
+#ifdef IMSAME_WAVE_EMU
+                {
+                    const unsigned lv = live(s), lv2 = (i >= 2) ? lv : 0u;
+                    NWP_CHK(lv, 0, m, sc);
+                    if (TB) { NWP_CHK(lv, 1, l0, lu); NWP_CHK(lv, 1, d0, m); }
+                    NWP_CHK(lv2, 1, mcS[s], dI[s]);
+                    NWP_CHK(lv2, 2, wv_bfi(pk_neg_mask(pk_sub(mcS[s], dI[s])), dI[s], u0[s]), EGN);
+                    NWP_CHK(lv, 1, tl, mfS);
+                    NWP_CHK(lv, 2, d0, IGEN);
+                    if (!(s == 0 && leadc0)) NWP_CHK(lv, 2, l0, EGN);
+                }
+#endif
                 uint32_t v = pk_add(m, sc);
                 if (s == 0 && leadc0) v = sc ^ H;                        // column 0 (:426)
                 cur[s] = pre ? own[s] : v;

@@ -11,6 +11,7 @@
 // tests/emu/build/libwave_emu.so.
 #define IMSAME_WAVE_EMU 1
 #include <algorithm>
+#include <atomic>
 #include <functional>
 #include <memory>
 #include <thread>
@@ -130,6 +131,21 @@ extern "C" uint32_t emu_k19_count(void) { const uint32_t r = g_k19; g_k19 = 0; r
 // long-read launches that ran the packed kernel (nwp_fits), and its waves that
 // fell back to the int32 path, since the last emu_nwp_count()
 static uint32_t g_nwp, g_fbk;
+// int16 wraps the emulated nwp_kernel met in live cells (nwp_kernel.hip:nwp_chk)
+std::atomic<uint64_t> g_nwp_viol{0};
+extern "C" uint64_t emu_nwp_range_violations(void) { return g_nwp_viol.exchange(0); }
+// nwp_chk on wraps of each kind (two adds, a sign, a decrement) and on the same operations in range: 4
+extern "C" uint32_t emu_nwp_chk_selftest(void) {
+    const uint64_t before = g_nwp_viol.exchange(0);
+    nwp_chk(1u, 0, 0x0000FFF0u, 0x00000020u);      // low half: 0xFFF0 + 32 > 0xFFFF
+    nwp_chk(2u, 0, 0xFFF0FFF0u, 0x0020FFE0u);      // high half: wraps; low: 0xFFF0 - 32 (not checked)
+    nwp_chk(1u, 1, 0x00009000u, 0x00001000u);      // 0x8000 apart: the sign wraps
+    nwp_chk(3u, 1, 0x80008000u, 0x00010001u);      // 0x7FFF apart: in range
+    nwp_chk(2u, 2, 0x00010005u, 0x00020002u);      // high half 1 < 2: underflow
+    nwp_chk(3u, 2, 0x00020002u, 0x00020002u);      // equal: in range
+    const uint64_t n = g_nwp_viol.exchange(before);
+    return (uint32_t)n;
+}
 extern "C" uint32_t emu_nwp_count(uint32_t *fallbacks) {
     const uint32_t r = g_nwp;
     if (fallbacks) *fallbacks = g_fbk;

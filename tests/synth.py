@@ -150,3 +150,32 @@ def make_metagenome_arr(pool, abundance, n, L, seed, sub=0.01, ins=0.0005, dele=
         s[flip] = lut[s[flip]]
         out[rows] = s
     return out.reshape(-1), np.arange(0, n * L, L, dtype=np.uint64)
+
+
+def adversarial_long_pairs():
+    """Long pairs near the packed long kernel's size limit (nwp_fits: records
+    and reads up to ~13.9 kbp at igap 5, egap 2) where its int16 frames are
+    stressed most: scores climbing 4 per row over 12 kbp, tandem and
+    dinucleotide repeats (long runs of equal maxima, ties in every column
+    max), a 3 kbp deletion, homopolymer runs, a random pair (scores falling),
+    and a read longer than its record."""
+    rng = np.random.default_rng(77)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    rnd = lambda n: acgt[rng.integers(0, 4, n)]           # noqa: E731
+    unit = rnd(37)
+    x1 = rnd(13_900)
+    rep = np.tile(unit, 376)[:13_900]
+    ac = np.tile(np.frombuffer(b"AC", dtype=np.uint8), 6950)
+    x4 = rnd(13_900)
+    hp = np.concatenate([np.full(4000, ord("A"), np.uint8), rnd(5000), np.full(4900, ord("A"), np.uint8)])
+    y7 = rnd(13_500)
+    pairs = [
+        (x1, x1[500:13_000]),                                             # identical 12.5 kbp
+        (rep, rep[11:11 + 13_000]),                                       # tandem repeat, shifted
+        (ac, np.concatenate([ac[:5000], rnd(1500), ac[:5000]])),          # dinucleotide + insertion
+        (x4, np.concatenate([x4[:5000], x4[8000:]])),                     # 3 kbp deletion
+        (hp, np.concatenate([np.full(3000, ord("A"), np.uint8), hp[4000:9000], np.full(3000, ord("A"), np.uint8)])),
+        (rnd(13_900), rnd(12_000)),                                       # random: falling scores
+        (y7[3000:9000].copy(), y7),                                       # read longer than its record
+    ]
+    return [x.tobytes() for x, _ in pairs], [y.tobytes() for _, y in pairs]

@@ -344,44 +344,15 @@ def test_packed_long_nw_kernels(dev, oracle, mode, monkeypatch, capfd):
         assert txt == o["text"], k
 
 
-def _adversarial_long_pairs():
-    """Long pairs near the packed long kernel's size limit (nwp_fits: records
-    and reads up to ~13.9 kbp at igap 5, egap 2) where its int16 frames are
-    stressed most: scores climbing 4 per row over 12 kbp, tandem and
-    dinucleotide repeats (long runs of equal maxima, ties in every column
-    max), a 3 kbp deletion, homopolymer runs, a random pair (scores falling),
-    and a read longer than its record."""
-    rng = np.random.default_rng(77)
-    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
-    rnd = lambda n: acgt[rng.integers(0, 4, n)]           # noqa: E731
-    unit = rnd(37)
-    x1 = rnd(13_900)
-    rep = np.tile(unit, 376)[:13_900]
-    ac = np.tile(np.frombuffer(b"AC", dtype=np.uint8), 6950)
-    x4 = rnd(13_900)
-    hp = np.concatenate([np.full(4000, ord("A"), np.uint8), rnd(5000), np.full(4900, ord("A"), np.uint8)])
-    y7 = rnd(13_500)
-    pairs = [
-        (x1, x1[500:13_000]),                                             # identical 12.5 kbp
-        (rep, rep[11:11 + 13_000]),                                       # tandem repeat, shifted
-        (ac, np.concatenate([ac[:5000], rnd(1500), ac[:5000]])),          # dinucleotide + insertion
-        (x4, np.concatenate([x4[:5000], x4[8000:]])),                     # 3 kbp deletion
-        (hp, np.concatenate([np.full(3000, ord("A"), np.uint8), hp[4000:9000], np.full(3000, ord("A"), np.uint8)])),
-        (rnd(13_900), rnd(12_000)),                                       # random: falling scores
-        (y7[3000:9000].copy(), y7),                                       # read longer than its record
-    ]
-    return [x.tobytes() for x, _ in pairs], [y.tobytes() for _, y in pairs]
-
-
 def test_packed_long_nw_adversarial_near_limit(dev, oracle, monkeypatch, capfd):
     """nwp_kernel.hip's range proof is checked per 64-step block from the
     wave's actual extremes; inside a block it relies on drift
     bounds.  Pairs at the largest sizes nwp_fits admits, built to stress it
-    (_adversarial_long_pairs), give every field of the oracle's NW -- whether
+    (synth.adversarial_long_pairs), give every field of the oracle's NW -- whether
     a wave stayed packed or fell back to the int32 body (both counted) -- and
     the same rows as the int32 kernel (IMSAME_NWP=0)."""
     monkeypatch.setenv("IMSAME_NW_PROF", "1")
-    X, Y = _adversarial_long_pairs()
+    X, Y = synth.adversarial_long_pairs()
     p = dev.params(igap=-5, egap=-2, min_coverage=1e-9, min_identity=1e-9, max_read_size=14_000)
     capfd.readouterr()
     res, _, _ = dev.nw_pairs(X, Y, p, want_paths=True)

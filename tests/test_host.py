@@ -11,6 +11,7 @@ import imsame_amd
 from imsame_amd import abi, fasta
 from imsame_amd import PARITY_FIELDS
 from tests import golden_io as G
+from tests import synth
 from tests.emu_bind import Emu
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -386,12 +387,57 @@ def test_emulated_packed_long_nw(emu, oracle, mode, monkeypatch):
     assert rc == 0 and fl == 0
     assert cnt(C.byref(fb)) == 1
     assert (fb.value == 0) if mode == "nwp" else (fb.value == 3), fb.value
+    assert _nwp_violations(emu) == 0
     for k in range(len(X)):
         o = oracle.nw(X[k], Y[k], igap=-5, egap=-2, text=True)
         for f in ("score", "bx", "by", "length", "identities", "igaps", "egaps", "head_x", "head_y"):
             assert int(res[k][f]) == int(o[f]), (f, k)
         txt, _ = imsame_amd.render(X[k], Y[k], res[k], paths[res[k]["path_off"]:res[k]["path_off"] + res[k]["path_len"]])
         assert txt == o["text"], k
+
+
+def _nwp_violations(emu):
+    f = emu.lib.emu_nwp_range_violations
+    f.restype = C.c_uint64
+    return f()
+
+
+@pytest.mark.parametrize("size", ["short", "full"])
+def test_emulated_packed_long_nw_adversarial(emu, oracle, size):
+    """nwp_kernel's int16 range proof runs at 64-step block starts
+    and relies on drift bounds inside a block.  The emulator checks the
+    conclusion at EVERY step (nwp_kernel.hip:nwp_chk: each packed add, sign
+    difference and biased decrement a live cell uses must not wrap in its
+    half) on pairs built to stress the frames (synth.adversarial_long_pairs:
+    12.5 kbp identical, tandem and dinucleotide repeats, a 3 kbp deletion,
+    homopolymers, random, a read longer than its record): no violation, and
+    every field equal to the oracle's.  "full" runs all of them at the largest
+    sizes nwp_fits admits (~7 min of emulation: IMSAME_EMU_FULL=1, log in
+    profiles/r5_sanitize/); the default suite runs the repeat pairs cut to 3 kbp."""
+    X, Y = synth.adversarial_long_pairs()
+    if size == "full":
+        if not os.environ.get("IMSAME_EMU_FULL"):
+            pytest.skip("IMSAME_EMU_FULL=1: all pairs at full size")
+    else:
+        X, Y = [X[k][:3000] for k in (1, 2, 4)], [Y[k][:2800] for k in (1, 2, 4)]
+    assert emu.lib.emu_nwp_chk_selftest() == 4            # the check sees a wrap of each kind
+    cnt = emu.lib.emu_nwp_count
+    cnt.restype = C.c_uint32
+    cnt.argtypes = [C.POINTER(C.c_uint32)]
+    fb = C.c_uint32(0)
+    cnt(C.byref(fb))
+    _nwp_violations(emu)
+    p = oracle.params(igap=-5, egap=-2, min_coverage=1e-9, min_identity=1e-9, max_read_size=14_000)
+    rc, res, _, fl = emu.nw_pairs(X, Y, p)
+    assert rc == 0 and fl == 0
+    assert cnt(C.byref(fb)) == 1
+    viol = _nwp_violations(emu)
+    print(f"pairs {len(X)}, waves fallen back {fb.value}, wraps {viol}")
+    assert viol == 0, (viol, fb.value)
+    for k in range(len(X)):
+        o = oracle.nw(X[k], Y[k], igap=-5, egap=-2)
+        for f in ("score", "bx", "by", "length", "identities", "igaps", "egaps", "head_x", "head_y"):
+            assert int(res[k][f]) == int(o[f]), (f, k, fb.value)
 
 
 def test_emulated_packed_long_seams_equal_int32(emu, oracle, monkeypatch, tmp_path):
