@@ -81,6 +81,9 @@ run_step() {   # $1 = step, $2 = output suffix
     micro) timeout -k 10 600 python -u scripts/micro/nw16_loop.py --valu ${MICRO_VALU:-351} \
              ${MICRO_WPS:+--waves-per-simd $MICRO_WPS} --out $O/micro_${TAG}$X.json > $O/micro_${TAG}$X.log 2>&1
            ok_or_stop $? micro$X ;;
+    # small NW launches per form (scripts/micro/nw_small.py)
+    nwsmall) IMSAME_NW_PROF=1 timeout -k 10 600 python -u scripts/micro/nw_small.py ${NWS_ARGS:-} --out $O/nwsmall_${TAG}$X.json \
+             > $O/nwsmall_${TAG}$X.log 2>&1; ok_or_stop $? nwsmall$X ;;
     benchab) local Y=$X k=1; while [ -e $O/benchab_${TAG}$Y.json ]; do k=$((k+1)); Y=${X}_$k; done
            timeout -k 10 600 python -u bench.py $BQ --steps 10 --warmup 2 > $O/benchab_${TAG}$Y.json \
            2> $O/benchab_${TAG}$Y.err; ok_or_stop $? benchab$Y ;;
