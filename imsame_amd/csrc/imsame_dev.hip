@@ -1061,14 +1061,20 @@ static int nw16_np_part_cu(imsame_ctx *c) {
 // the columns per step) and doubles their number, for ~8 % more
 // instructions per cell.  Chosen when the launch holds fewer than
 // k5_fill x (the chip's K = 10 slots / the lanes running) tasks.
-// IMSAME_NW_K=5|10 forces one; IMSAME_NW_K5_FILL sets k5_fill, 0 by default:
-// at k5_fill 2 the C2 1/8 shard ran 21.3-21.5 ms against 20.5-20.6 with
-// K = 10 everywhere (profiles/r3o_*: the small launches are not wave-latency
-// bound but share the chip with the other lanes' large ones).
+// IMSAME_NW_K=5|10 forces one; IMSAME_NW_K5_FILL sets k5_fill.  Round 3
+// measured k5_fill 2 slower (the C2 1/8 shard 21.3-21.5 ms against
+// 20.5-20.6, profiles/r3o_*: launches of ~10k candidates share the chip with
+// the other lanes' large ones).  Round 5: at 0.3 (below ~3.3k candidates with
+// 3 lanes) K = 5 replaces the int32 kernel that ran those launches (plan_nw's
+// `small`): alone on the chip a 2000 x 150 launch takes 0.59 / 0.63 / 0.74 ms
+// at 128 / 1400 / 4096 candidates against 0.68 / 0.71 / 1.17 (int32) and
+// 1.69 / 1.72 / 1.79 (K = 19) (profiles/r5y/nwsmall_r5y.json); the 1/4 shard's
+// round-2 launches (~2.9k candidates) went 1.1-1.9 -> 0.8-1.4 ms and the
+// shard 29.7 -> 28.8 ms, C2 and the 1/8 shard unchanged (profiles/r5z/).
 static int nw16_k(imsame_ctx *c, uint32_t ncand, bool rounds) {
     const char *e = getenv("IMSAME_NW_K"), *fe = getenv("IMSAME_NW_K5_FILL");
     const int force = e ? atoi(e) : 0;
-    const double fill = fe ? atof(fe) : 0.0;      // off: measured slower (profiles/r3o_*)
+    const double fill = fe ? atof(fe) : 0.3;
     if (force == NW16_K5 || force == NW16_K) return force;
     if (!rounds) return NW16_K;
     const double slots = (double)c->ncu * 4.0 * 4.0 / std::max(1, c->nlanes);
@@ -1082,13 +1088,14 @@ static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, 
                    bool ylen_mult, NwPlan *pl, bool rounds = true, uint32_t ylen_uni = 0) {
     const int wpb = 4;
     // Small launches (the last rounds; every round of a small shard) are
-    // latency-bound: one packed task is 8 candidates x all rows with 10
-    // columns per lane (~1.1 ms alone on a SIMD), while the int32 kernel puts
-    // 5 columns on a lane (about a third of the per-row issue) and 2
-    // candidates in a wave.  Results are identical (tests run both kernels).
-    // (IMSAME_FLAG_NW16 and the unit-level nw_pairs keep the packed kernel.)
+    // latency-bound: one 19-column task is 16 candidates x all rows (~1.6 ms
+    // alone on a SIMD).  Rounds 3-4 ran launches below 3000 candidates on the
+    // int32 kernel (5 columns per lane, 2 candidates per wave); since round 5
+    // the packed kernel's 5-column form takes them (nw16_k: faster alone at
+    // every size, profiles/r5y/).  IMSAME_NW_SMALL=N: the int32 kernel below N
+    // candidates again.  Results are identical (tests run every kernel).
     const char *se = getenv("IMSAME_NW_SMALL");
-    const uint32_t small = (p->flags & IMSAME_FLAG_NW16) || !rounds ? 0u : se ? (uint32_t)atoi(se) : 3000u;
+    const uint32_t small = (p->flags & IMSAME_FLAG_NW16) || !rounds ? 0u : se ? (uint32_t)atoi(se) : 0u;
     pl->pk = !(p->flags & IMSAME_FLAG_NW32) && ncand >= small && nw16_fits(p->igap, p->egap, xcap, ymax);
     pl->last4 = pl->pk && ylen_mult;
     const char *op = getenv("IMSAME_NW_ONEPASS");
