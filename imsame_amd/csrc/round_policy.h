@@ -50,7 +50,10 @@ struct RoundPolicy {
         r.spec_set = sp != nullptr;
         r.spec_later = sp ? (uint32_t)std::max(1, std::min(SPEC_MAX, atoi(sp))) : (uint32_t)SPEC_MAX;
         const char *bu = getenv("IMSAME_SEED_BUDGET");
-        r.budget1 = bu ? (uint32_t)std::max(0, atoi(bu)) : SEED_BUDGET1;
+        // (2 x SEED_BUDGET1 for lanes of >= 200k reads -- C2 and C3's lanes:
+        // C3 392.4 -> 383.8 ms, C2 106.2 -> 105.8-105.9 ms per step; a lane of
+        // the 1/4 shard's 83k reads ran 29.8 ms against 28.6, profiles/r5zg/)
+        r.budget1 = bu ? (uint32_t)std::max(0, atoi(bu)) : (n >= 200000 ? 2 * SEED_BUDGET1 : SEED_BUDGET1);
         // budget growth per round: 8x; a lane of < 100k reads (an 8-GPU shard
         // of C2) 64x, so its third round finishes the random reads' scans
         // instead of leaving a latency-bound fourth round of tiny launches (C2
