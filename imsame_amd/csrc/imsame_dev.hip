@@ -1625,6 +1625,107 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
             HIPCHK(hipGetLastError());
             return 0;
         };
+        // Split rounds (rounds >= 2 of many reads, short reads only).  A lane
+        // alternates scan and NW round by round, and where every lane scans at
+        // once the chip runs no NW (C3: ~39 ms of a 385 ms step,
+        // profiles/r5zb/).  The round's active reads are scanned in two
+        // halves, the second on stream_b, and each half's NW launch starts as
+        // soon as its own scan is done: the first half's NW runs while the
+        // second half scans.  The halves hold different reads, so each read
+        // sees the same scan and the same NW results in the same order as in
+        // one launch (tests).  IMSAME_SPLIT_ROUNDS=0 turns it off;
+        // IMSAME_SPLIT_MIN sets the reads below which a round stays whole.
+        if (RP.split(rnd, nact)) {
+            if (!c->stream_b) {
+                HIPCHK(hipStreamCreateWithFlags(&c->stream_b, hipStreamNonBlocking));
+                HIPCHK(hipEventCreate(&c->evb0));
+                HIPCHK(hipEventCreate(&c->evb1));
+                for (int k = 0; k < 2; ++k)
+                    HIPCHK(hipEventCreateWithFlags(&c->evw[1][k], hipEventBlockingSync | hipEventDisableTiming));
+            }
+            hipStream_t sb = c->stream_b;
+            const char *sf = getenv("IMSAME_SPLIT_FRAC");            // the first half's share
+            const double fa = sf ? std::max(0.05, std::min(0.95, atof(sf))) : 0.5;
+            const uint32_t nA = std::max<uint32_t>(1, (uint32_t)(nact * fa)), nB = nact - nA;
+            const uint64_t offB = (uint64_t)S.spec * nA;               // the first half's list room
+            // stream_b starts behind what stream s has queued (the counters' reset)
+            HIPCHK(hipEventRecord(c->evb0, s));
+            HIPCHK(hipStreamWaitEvent(sb, c->evb0, 0));
+            S.n_active = nA;
+            SeedLaunch Sb = S;
+            Sb.active = act + nA; Sb.n_active = nB;
+            Sb.cread = c->cread.as<uint32_t>() + offB; Sb.csid = c->csid.as<uint32_t>() + offB;
+            Sb.ncand = (uint32_t *)(ctr + C_NCANDB); Sb.ncand2 = (uint32_t *)(ctr + C_NCAND2B);
+            Sb.crow = crow ? crow + offB : nullptr;
+            Sb.dbg = nullptr;
+            if ((rc = seed_launch(S, nA, s, c->ev0, c->ev1))) return rc;
+            // the second half scans after the first (beside its NW launch): two
+            // scans at once would end together and start both launches late
+            // (IMSAME_SPLIT_SEQ=0: at once)
+            const char *sq = getenv("IMSAME_SPLIT_SEQ");
+            if (!(sq && !atoi(sq))) HIPCHK(hipStreamWaitEvent(sb, c->ev1, 0));
+            if ((rc = seed_launch(Sb, nB, sb, c->evb0, c->evb1))) return rc;
+            uint64_t ha[2], hb[2];
+            HIPCHK(hipMemcpyAsync(ha, ctr + C_NCAND, 16, hipMemcpyDeviceToHost, s));
+            LANE_SYNC(c, s);
+            if ((rc = seed_time(c->ev0, c->ev1, nA))) return rc;
+            if (ha[1]) return IMSAME_E_STATE;                         // short reads only: cannot happen
+            const uint32_t na1 = (uint32_t)ha[0];
+            NwPlan pla = {}, plb = {};
+            double msa = 0, msb = 0;
+            if (na1) {
+                if ((rc = plan_nw(c, short_y, xcap, na1, p, c->q_len_mult, &pla, true, c->q_len_uni))) return rc;
+                rc = launch_nw(c, pla, c->cread.as<uint32_t>(), c->csid.as<uint32_t>(), na1, c->cout.as<imsame_read_result>(),
+                               p->igap, p->egap, p, ymax, xcap, (uint32_t *)(ctr + C_WORK), c->db.as<uint8_t>(),
+                               c->db_start.as<uint64_t>(), qd, qsd, pcap, &msa, crow, 0, false);
+                if (rc) return rc;
+                if ((rc = upd_launch(c->cread.as<uint32_t>(), c->csid.as<uint32_t>(), na1, c->cout.as<imsame_read_result>(),
+                                     nxt, C_NNEXT, s))) return rc;
+            }
+            HIPCHK(hipMemcpyAsync(hb, ctr + C_NCANDB, 16, hipMemcpyDeviceToHost, sb));
+            LANE_SYNC(c, sb);
+            if ((rc = seed_time(c->evb0, c->evb1, nB))) return rc;
+            if (hb[1]) return IMSAME_E_STATE;
+            const uint32_t nb1 = (uint32_t)hb[0];
+            bool a_done = na1 == 0;
+            if (nb1) {
+                if ((rc = plan_nw(c, short_y, xcap, nb1, p, c->q_len_mult, &plb, true, c->q_len_uni))) return rc;
+                // both launches share the arena only as non-persistent launches of one
+                // slot layout; otherwise the second waits for the first (as round 1b)
+                const bool same = pla.np && plb.np && plb.slot_words == pla.slot_words && plb.tb_dw == pla.tb_dw &&
+                                  plb.ck_dw == pla.ck_dw && plb.bnd_dw == pla.bnd_dw && plb.max_blocks == pla.max_blocks;
+                if (!same && !a_done) {
+                    if ((rc = nw_launch_done(c, 0, na1, &msa))) return rc;
+                    rec_launch(pla, na1, msa);
+                    a_done = true;
+                }
+                rc = launch_nw(c, plb, Sb.cread, Sb.csid, nb1, c->cout.as<imsame_read_result>() + offB, p->igap, p->egap,
+                               p, ymax, xcap, (uint32_t *)(ctr + C_WORKB), c->db.as<uint8_t>(), c->db_start.as<uint64_t>(),
+                               qd, qsd, pcap, &msb, Sb.crow, 1, false);
+                if (rc) return rc;
+                if ((rc = upd_launch(Sb.cread, Sb.csid, nb1, c->cout.as<imsame_read_result>() + offB, nxt, C_NNEXT, sb)))
+                    return rc;
+            }
+            if (!a_done) {
+                if ((rc = nw_launch_done(c, 0, na1, &msa))) return rc;
+                rec_launch(pla, na1, msa);
+            }
+            if (nb1) {
+                if ((rc = nw_launch_done(c, 1, nb1, &msb))) return rc;
+                rec_launch(plb, nb1, msb);
+            }
+            LANE_SYNC(c, sb);
+            uint64_t nn = 0;
+            HIPCHK(hipMemcpyAsync(&nn, ctr + C_NNEXT, 8, hipMemcpyDeviceToHost, s));
+            LANE_SYNC(c, s);
+            if (getenv("IMSAME_DEBUG_ROUNDS"))
+                fprintf(stderr, "[round %llu split] active=%u+%u spec=%u budget=%u cand=%u+%u next=%llu\n",
+                        (unsigned long long)st.rounds, nA, nB, S.spec, S.budget, na1, nb1, (unsigned long long)nn);
+            if (na1 + nb1 == 0 && nn == 0) break;
+            nact = (uint32_t)nn;
+            std::swap(act, nxt);
+            continue;
+        }
         if ((rc = seed_launch(S, nact, s, c->ev0, c->ev1))) return rc;
         uint64_t hc[3];
         HIPCHK(hipMemcpyAsync(hc, ctr + C_NCAND, 24, hipMemcpyDeviceToHost, s));

@@ -23,6 +23,8 @@ struct RoundPolicy {
     uint64_t l64_below = 8192;       // reads (over all lanes) below which a whole wave scans a read
     int nlanes = 1;                  // lanes of the call: the device scans nlanes x na reads at once
     bool r1b_on = true;              // round 1b (short reads only)
+    bool split_on = true;            // split rounds (imsame_dev.hip:align_one; short reads only)
+    uint32_t split_min = 16384;      // ... of at least this many active reads
     bool window = true;              // predicted traceback windows of the packed NW kernel
     bool weak_rows = false;          // ... predicted from weak hits too (IMSAME_NW_WEAK_ROWS)
     bool r1b_rows = false;           // ... for round 1b's candidates (IMSAME_NW_R1B_ROWS)
@@ -68,6 +70,9 @@ struct RoundPolicy {
         r.l64_below = l64 ? strtoull(l64, nullptr, 10) : 8192;
         const char *rb = getenv("IMSAME_ROUND1B");
         r.r1b_on = !(rb && !atoi(rb)) && ycap <= short_y;
+        const char *sr = getenv("IMSAME_SPLIT_ROUNDS"), *sm = getenv("IMSAME_SPLIT_MIN");
+        r.split_on = !(sr && !atoi(sr)) && ycap <= short_y;
+        if (sm) r.split_min = (uint32_t)std::max(2, atoi(sm));
         // (round 2 measured the windows 1-3 % slower -- the window steps spilled
         // at 4 waves per SIMD, round 1b off; at 3 waves per SIMD and with round
         // 1b they take C2's NW busy time from 113.4 to 107.4 ms, profiles/r4d/)
@@ -114,4 +119,9 @@ struct RoundPolicy {
         return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(w, (ccap - n1) / std::max<uint32_t>(paused, 1)));
     }
     uint32_t r1b_budget() const { return seed_budget(budget1, 2, grow); }
+    // Split rounds: a round >= 2 of at least split_min active reads scans
+    // them in two halves, each half's NW launch starting after its own scan
+    bool split(uint32_t round, uint32_t nact) const {
+        return round >= 2 && split_on && nact >= split_min;
+    }
 };

@@ -413,6 +413,52 @@ def test_full_c2_reference_properties(dev, oracle):
     assert sum(b - a for a, b in wins) >= 4_500
 
 
+@pytest.mark.timeout(300)
+def test_split_rounds_equal(dev, oracle, monkeypatch, capfd):
+    """Split rounds (imsame_dev.hip:align_one): a later round's active reads
+    scanned in two halves, the second on stream_b after (or beside) the
+    first, each half's NW launch after its own scan.  With a low threshold
+    (IMSAME_SPLIT_MIN) every later round splits: the per-read results equal
+    the unsplit run's for the default halves, a 0.3 / 0.7 cut and two scans
+    at once, and the default run equals the oracle on three windows.  A
+    third of the reads are random (many rounds of many reads)."""
+    ref, rst = synth.make_reference_arr(8_000_000, 2_000, seed=81)
+    q, qs = synth.make_reads_arr(ref, 150_000, 150, seed=82, frac_true=0.67)
+    dev.index(ref, rst)
+    dev.set_query(q, qs)
+    monkeypatch.setenv("IMSAME_SPLIT_ROUNDS", "0")
+    base, pb, sb = dev.align(n_threads=16, want_paths=True)
+    monkeypatch.delenv("IMSAME_SPLIT_ROUNDS")
+    monkeypatch.setenv("IMSAME_SPLIT_MIN", "64")
+    monkeypatch.setenv("IMSAME_DEBUG_ROUNDS", "1")      # split rounds print "[round k split]"
+    res = None
+    for env in [{}, {"IMSAME_SPLIT_FRAC": "0.3"}, {"IMSAME_SPLIT_SEQ": "0"}]:
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        capfd.readouterr()
+        r, pp, st = dev.align(n_threads=16, want_paths=True)
+        err = capfd.readouterr().err
+        for k in env:
+            monkeypatch.delenv(k)
+        assert " split] " in err, (env, err[-1500:])
+        assert not _cmp(r, base), (env, _cmp(r, base))
+        assert st.n_nw == sb.n_nw and st.rounds >= 2, (env, st.n_nw, sb.n_nw, st.rounds)
+        for k in np.flatnonzero(base["status"] == 1)[::211]:
+            s_ = int(base[k]["db_seq"])
+            X = ref[int(rst[s_]):int(rst[s_]) + 2_000].tobytes()
+            Y = q[int(qs[k]):int(qs[k]) + 150].tobytes()
+            t1, _ = render(X, Y, r[k], pp[r[k]["path_off"]:r[k]["path_off"] + r[k]["path_len"]])
+            t0, _ = render(X, Y, base[k], pb[base[k]["path_off"]:base[k]["path_off"] + base[k]["path_len"]])
+            assert t1 == t0, (env, k)
+        if res is None:
+            res = r
+    wins = _windows(len(qs))
+    rc, exp, _ = oracle.align_windows(ref, rst, q, qs, wins, None, 16)
+    assert rc == 0
+    for (a, b), e in zip(wins, exp):
+        assert not _cmp(res[a:b], e), ((a, b), _cmp(res[a:b], e))
+
+
 @pytest.mark.timeout(900)
 def test_headline_mode_parity():
     """The benchmark's own execution mode: 1M x 150 bp vs the 50 Mbp C2
