@@ -1072,9 +1072,15 @@ static int nw16_np_part_cu(imsame_ctx *c) {
 // round-2 launches (~2.9k candidates) went 1.1-1.9 -> 0.8-1.4 ms and the
 // shard 29.7 -> 28.8 ms, C2 and the 1/8 shard unchanged (profiles/r5z/).
 static int nw16_k(imsame_ctx *c, uint32_t ncand, bool rounds) {
-    const char *e = getenv("IMSAME_NW_K"), *fe = getenv("IMSAME_NW_K5_FILL");
+    const char *e = getenv("IMSAME_NW_K"), *fe = getenv("IMSAME_NW_K5_FILL"), *f2 = getenv("IMSAME_NW_K5_FILL2");
     const int force = e ? atoi(e) : 0;
-    const double fill = fe ? atof(fe) : 0.3;
+    // a lane's launches of rounds >= 2 (IMSAME_NW_K5_FILL2, 1.5: below ~16k
+    // candidates with 3 lanes): C2's round-2 launches of ~15.5k candidates
+    // run one or two 19-column waves per SIMD, latency-bound; the 5-column
+    // form took C2 from 105.8-105.9 to 105.2-105.3 ms per step, the 1/8 shard
+    // and C3 unchanged (profiles/r5zt/; 1.5 for every launch, round 1b's
+    // included, slowed the 1/8 shard and C3: r5zs/)
+    const double fill = c->cur_round >= 2 ? (f2 ? atof(f2) : 1.5) : fe ? atof(fe) : 0.3;
     if (force == NW16_K5 || force == NW16_K) return force;
     if (!rounds) return NW16_K;
     const double slots = (double)c->ncu * 4.0 * 4.0 / std::max(1, c->nlanes);
