@@ -345,12 +345,14 @@ def main():
     h2d.clear()
     barrier()
     stats = []
+    cpu0 = time.process_time()                      # this rank's host CPU seconds (all its threads)
     t0 = time.perf_counter()
     for _ in range(a.steps):
         res, _, st = step()
         stats.append(st.as_dict())
     barrier()
     elapsed = time.perf_counter() - t0
+    host_cpu_s = (time.process_time() - cpu0) / a.steps
     accepted = int((res["status"] == 1).sum())
     res = res.copy()
     if dist is not None:
@@ -408,8 +410,8 @@ def main():
     tp = nw16_min_bytes_per_cell(a.read_len, a.record_bp) if kernel == "nw16_kernel" else None
     hbm = {"basis": "CONTRACT figure: algorithmic bytes of SURVEY 8(d) (xlen + ylen + 2 B/cell traceback floor per "
                     "NW) / NW busy time -- the kernel stores 4 bits per cell of a band, not 2 B per cell",
-           "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "frac": round(achieved / HBM_PEAK_GBS, 4),
+           "contract_achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "contract_frac": round(achieved / HBM_PEAK_GBS, 4),
            "two_pass_min": tp,
            "measured_bytes_per_cell": bpc,
            "measured_over_two_pass_min": round(bpc / tp["bytes_per_cell"], 3) if bpc and tp else None,
@@ -435,8 +437,8 @@ def main():
         roofline = dict({"bound": "valu", "achieved": valu["achieved"], "peak": valu["issue_peak"],
                          "unit": valu["unit"], "frac": valu["frac"]}, **common, valu=valu, hbm=hbm)
     else:
-        roofline = dict({"bound": "hbm", "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": hbm["frac"]}, **common, valu=None, hbm=hbm)
+        roofline = dict({"bound": "hbm", "achieved": hbm["contract_achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": hbm["contract_frac"]}, **common, valu=None, hbm=hbm)
 
     cpu = parity = None
     if rank == 0 and world == 1 and a.cpu_sample > 0:
@@ -477,6 +479,10 @@ def main():
             "ranks": {"world": world, "backend": ("rccl" if backend == "nccl" else backend),
                       "device": gpu, "host_cpus_usable": hc["usable"],
                       "host_threads_per_rank": int(os.environ["IMSAME_HOST_THREADS"]),
+                      "host_cpu_s_per_step": round(host_cpu_s, 5),
+                      "host_cpu_s_per_step_basis": "rank 0's process CPU time (user + system, every thread: the "
+                                                   "lanes' host threads, the upload pass, waits) over the timed "
+                                                   "steps / steps",
                       "lane_wait": os.environ.get("IMSAME_WAIT", "yield"),
                       "launcher_visible_gpus": (int(os.environ["IMSAME_BENCH_VISIBLE"])
                                                 if "IMSAME_BENCH_VISIBLE" in os.environ else None),
@@ -729,16 +735,54 @@ def cpu_baseline(dev, ref, rst, q, qs, a, params):
         return port
     r = run_reference(ref_bin, ref, rst, qv, qs[:n], a.cpu_threads)
     gpu_acc = int((got["status"] == 1).sum())
+    # the reference's own records vs the GPU rows (a second run with -out,
+    # outside the timed one above)
+    rows = reference_rows(ref_bin, ref, rst, qv, qs[:n], a.cpu_threads, got)
     return {"value": round(n / r["align_s"], 1), "unit": "reads/s", "cores": a.cpu_threads, "kind": "reference",
             "sample": f"first {n} reads of the rank-0 shard as their own query vs the same database, "
                       f"IMSAME compiled from the reference sources (oracle/Makefile ref, gcc -O3) -n_threads "
                       f"{a.cpu_threads}; alignment phase = process wall {r['wall_s']:.2f} s minus its single-threaded "
                       f"setup phases {r['setup_s']:.2f} s = {r['align_s']:.2f} s",
-            "reference_accepted": r["accepted"], "gpu_accepted": gpu_acc, "host": host,
+            "reference_accepted": r["accepted"], "gpu_accepted": gpu_acc,
+            "reference_rows_identical": rows["identical"], "reference_rows_compared": rows["compared"],
+            "reference_rows": rows, "host": host,
             "port": port}
 
 
-def run_reference(ref_bin, ref, rst, q, qs, threads):
+def reference_rows(ref_bin, ref, rst, q, qs, threads, got):
+    """Row-level parity with the compiled reference itself on the CPU-baseline
+    sample: its `-out` file holds one record per accepted read, headed
+    "(read, record) : id% cov% ylen" (alignmentFunctions.c:167; each header is
+    one fprintf, so it survives the -n_threads interleave).  A read is
+    identical when the reference accepted it and the GPU row has status 1,
+    the same record, min(100, 100*identities/length) and min(100,
+    100*length/ylen) in the reference's integer arithmetic, and the same ylen
+    -- or when neither accepted it."""
+    import re
+    n = len(qs)
+    ref_rows = {}
+    dup = 0
+    for m in re.finditer(rb"^\((\d+), (\d+)\) : (\d+)% (\d+)% (\d+)\n \$\$\$\$\$\$\$ $",
+                         run_reference(ref_bin, ref, rst, q, qs, threads, want_out=True)["out"], re.M):
+        k = int(m.group(1))
+        dup += k in ref_rows
+        ref_rows[k] = tuple(int(x) for x in m.groups()[1:])
+    acc = got["status"] == 1
+    ln = got["length"].astype(np.uint64)
+    idp = np.minimum(100, (100 * got["identities"].astype(np.uint64)) // np.maximum(ln, 1))
+    cov = np.minimum(100, (100 * ln) // np.maximum(got["ylen"].astype(np.uint64), 1))
+    same = ~acc.copy()                                  # neither accepted ...
+    for k, (sid, i_, c_, y_) in ref_rows.items():
+        same[k] = bool(acc[k]) and (int(got["db_seq"][k]), int(idp[k]), int(cov[k]), int(got["ylen"][k])) == \
+            (sid, i_, c_, y_)
+    bad = np.flatnonzero(~same)
+    return {"identical": int(same.sum()), "compared": n, "reference_records": len(ref_rows),
+            "duplicate_headers": dup, "first_mismatches": [int(x) for x in bad[:5]],
+            "fields": "read, record, id%, cov%, ylen of every '(read, record) : id% cov% ylen' header "
+                      "(alignmentFunctions.c:167) vs the GPU row; reads without a header must have status != 1"}
+
+
+def run_reference(ref_bin, ref, rst, q, qs, threads, want_out=False):
     """Run the compiled reference on FASTA files of the sample (test
     infrastructure: the CPU baseline only).  Its timing lines use clock() --
     CPU time summed over threads -- so the alignment phase is the process's
@@ -761,16 +805,20 @@ def run_reference(ref_bin, ref, rst, q, qs, threads):
         qe = qs[1:].tolist() + [len(q)]
         with open(qf, "wb") as f:
             f.write(b"".join(b">read_%d\n" % i + b[s0:s1] + b"\n" for i, (s0, s1) in enumerate(zip(qs.tolist(), qe))))
+        outf = os.path.join(td, "out.align")
         t0 = time.monotonic()
-        p = subprocess.run([ref_bin, "-db", dbf, "-query", qf, "-n_threads", str(threads)],
+        p = subprocess.run([ref_bin, "-db", dbf, "-query", qf, "-n_threads", str(threads)]
+                           + (["-out", outf] if want_out else []),
                            stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=600)
         wall = time.monotonic() - t0
+        body = open(outf, "rb").read() if want_out and p.returncode == 0 else None
     out = p.stdout.decode(errors="replace")
     setup = [float(x) for x in re.findall(r"(?:Initialization took|building took|Took) ([0-9.eE+-]+) seconds", out)]
     acc = re.search(r"\[INFO\] (\d+) reads \(", out)
     if p.returncode != 0 or len(setup) != 3 or acc is None:
         raise RuntimeError(f"reference run failed (rc {p.returncode}): {out[-500:]}")
-    return {"align_s": wall - sum(setup), "wall_s": wall, "setup_s": sum(setup), "accepted": int(acc.group(1))}
+    return {"align_s": wall - sum(setup), "wall_s": wall, "setup_s": sum(setup), "accepted": int(acc.group(1)),
+            "out": body}
 
 
 if __name__ == "__main__":

@@ -58,8 +58,26 @@ __global__ void mark_record_starts(const uint64_t *st, uint64_t n, uint64_t L, u
 // the 2-bit packed bases (seed_kernel.hip:pk_word): words [w0, w1) of dst
 // (biased: dst[w] holds bases 16w ..) from src (biased: src[p] = base p,
 // valid for lo <= p < hi; other slots 0)
-__global__ void pack2_kernel(const uint8_t *src, int64_t lo, int64_t hi, uint32_t *dst, uint64_t w0, uint64_t w1) {
-    GRID_STRIDE(k, w1 - w0) dst[w0 + k] = pk_word(src, (int64_t)(w0 + k), lo, hi);
+// ... and, where `bad` is given, bit 0 of *bad set if a byte of [lo, hi) in
+// these words is not 'A', 'C', 'G' or 'T': the 2-bit codes (and nw16's
+// base_code) alias every other byte to one of them, so the bases must be what
+// IMSAME's loaders keep (IMSAME.c:216-221, :340-345; include/imsame_dev.h)
+__device__ __forceinline__ bool acgt_word_bad(const uint8_t *src, int64_t w, int64_t lo, int64_t hi) {
+    bool bad = false;
+    for (int64_t p = max(w * 16, lo), e = min(w * 16 + 16, hi); p < e; ++p) {
+        const uint8_t b = src[p];
+        bad |= b != 'A' && b != 'C' && b != 'G' && b != 'T';
+    }
+    return bad;
+}
+__global__ void pack2_kernel(const uint8_t *src, int64_t lo, int64_t hi, uint32_t *dst, uint64_t w0, uint64_t w1,
+                             unsigned long long *bad = nullptr) {
+    bool b = false;
+    GRID_STRIDE(k, w1 - w0) {
+        dst[w0 + k] = pk_word(src, (int64_t)(w0 + k), lo, hi);
+        if (bad) b |= acgt_word_bad(src, (int64_t)(w0 + k), lo, hi);
+    }
+    if (b) atomicOr(bad, 8ull);
 }
 
 // code of the 12-mer ending at base p, or ~0 when a reset lies in (p-11, p]
@@ -734,7 +752,10 @@ extern "C" int imsame_dev_index(imsame_ctx *c, const uint8_t *db_seq, uint64_t d
             if (int rc = b->poison(s)) return rc;
     }
     if (db_len) HIPCHK(hipMemcpyAsync(c->db.p, db_seq, db_len, hipMemcpyHostToDevice, s));
-    pack2_kernel<<<gsblk(npw, 256), 256, 0, s>>>(c->db.as<uint8_t>(), 0, (int64_t)db_len, c->dbw.as<uint32_t>(), 0, npw);
+    uint64_t *badf = c->ctr.as<uint64_t>() + C_FLAGS;  // bit 3: a byte that is not ACGT (no align runs now)
+    HIPCHK(hipMemsetAsync(badf, 0, 8, s));
+    pack2_kernel<<<gsblk(npw, 256), 256, 0, s>>>(c->db.as<uint8_t>(), 0, (int64_t)db_len, c->dbw.as<uint32_t>(), 0, npw,
+                                                 (unsigned long long *)badf);
     HIPCHK(hipMemcpyAsync(c->db_start.p, c->h_db_start.data(), (n_db + 1) * 8, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemsetAsync(c->brk.p, 0, nw * 4, s));
     if (db_brk && db_len) HIPCHK(hipMemcpyAsync(c->brk.p, db_brk, (db_len + 7) / 8, hipMemcpyHostToDevice, s));
@@ -754,8 +775,11 @@ extern "C" int imsame_dev_index(imsame_ctx *c, const uint8_t *db_seq, uint64_t d
         int rc = dev_scan<uint32_t, uint64_t>(s, cnt.as<uint32_t>(), c->off.as<uint64_t>(), (uint64_t)NBUCKETS + 1);
         if (rc) return rc;
         HIPCHK(hipMemcpyAsync(&total, c->off.as<uint64_t>() + NBUCKETS, 8, hipMemcpyDeviceToHost, s));
+        uint64_t hbad = 0;
+        HIPCHK(hipMemcpyAsync(&hbad, badf, 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         cnt.release();
+        if (hbad) return IMSAME_E_ARG;                 // not an ACGT-filtered database (the header)
     }
     c->n_ent = total;
     if (c->ent.ensure((total + 1) * 8)) return IMSAME_E_OOM;
@@ -1449,6 +1473,20 @@ static int rewalk_lost(imsame_ctx *c, const imsame_params *p, uint64_t read_from
 }
 
 // one lane's alignment of reads [read_from, read_to) (arguments checked)
+// Blocks of an update launch (update_kernel strides over the candidates):
+// few waves, so a launch queued while other lanes' NW waves hold the chip
+// starts as soon as a handful of slots free up.  IMSAME_UPD_BLOCKS overrides.
+static unsigned upd_blocks() {
+    static unsigned v = [] { const char *e = getenv("IMSAME_UPD_BLOCKS"); return e ? std::max(1, atoi(e)) : 64; }();
+    return v;
+}
+// ... and of a seed launch (the scan kernels stride over the reads' groups):
+// unlimited unless IMSAME_SEED_BLOCKS is set
+static unsigned seed_blocks() {
+    static unsigned v = [] { const char *e = getenv("IMSAME_SEED_BLOCKS"); return e ? std::max(1, atoi(e)) : 1u << 30; }();
+    return v;
+}
+
 static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64_t n_threads_semantic,
                      const imsame_params *p, imsame_read_result *res, uint32_t *paths, uint64_t paths_cap,
                      uint64_t *paths_used, imsame_stats *stats) {
@@ -1458,27 +1496,6 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     const uint32_t n = (uint32_t)(read_to - read_from);
     // this lane's bases (and the 16-byte chunk loads' reach past its last read)
     if (int rq = query_wait(c, s, hqs(c, read_to) + 64)) return rq;
-    // ... and their packed copy (seed_kernel.hip:pk_word): the words from QPAD
-    // bases before its first read to the end of its last part.  Each lane
-    // packs its own on its stream as its parts arrive (packing in the upload
-    // delayed every lane: the upload's kernels waited for free CUs behind NW
-    // waves, profiles/r5t/); neighbouring lanes both write the few words where
-    // their reaches meet, with the same values.
-    // Words are packed only where all 16 of their bytes are in HBM (below the
-    // end of the part waited for): a word at the edge of a part that is still
-    // copying would get garbage in the slots a neighbouring lane reads.
-    {
-        const uint64_t b0 = hqs(c, read_from), b1 = hqs(c, read_to) + 64;
-        uint64_t pe = c->qb_end;                          // end of the part query_wait waited for
-        for (size_t k = 0; k + 1 < c->q_part_end.size(); ++k)
-            if (c->q_part_end[k] >= b1) { pe = c->q_part_end[k]; break; }
-        const uint64_t w0 = std::max(c->qw_base, (b0 > QPAD ? b0 - QPAD : 0) / 16);
-        const uint64_t w1 = pe == c->qb_end ? c->qw_end : std::min(c->qw_end, pe / 16);
-        if (w1 > w0)
-            pack2_kernel<<<gsblk(w1 - w0, 256), 256, 0, s>>>(dev_q(c), (int64_t)c->q_base, (int64_t)c->qb_end,
-                                                             (uint32_t *)dev_qw(c), w0, w1);
-        HIPCHK(hipGetLastError());
-    }
     imsame_stats st;
     memset(&st, 0, sizeof st);
     st.n_reads = n;
@@ -1510,10 +1527,13 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     if (c->res.ensure((uint64_t)n * 64) || c->cur_p.ensure((uint64_t)n * 8) || c->cur_h.ensure((uint64_t)n * 4) ||
         c->memo.ensure((uint64_t)n * 4 * MEMO) || c->nmemo.ensure(n) || c->rstat.ensure(n) ||
         c->act0.ensure((uint64_t)n * 4) || c->act1.ensure((uint64_t)n * 4) || c->act2.ensure((uint64_t)n * 4) ||
-        c->cread.ensure(ccap * 4) ||
-        c->csid.ensure(ccap * 4) || c->cread2.ensure(ccap * 4) || c->csid2.ensure(ccap * 4) ||
-        c->cout.ensure(ccap * 64) || c->cout2.ensure(ccap * 64) || c->cbase.ensure((uint64_t)n * 4) ||
+        c->cread.ensure(ccap * 4) || c->csid.ensure(ccap * 4) ||
+        c->cout.ensure(ccap * 64) || c->cbase.ensure((uint64_t)n * 4) ||
         c->ccnt.ensure((uint64_t)n * 4) || c->perr.ensure((uint64_t)n * 4) || c->crow.ensure(ccap * 4))
+        return IMSAME_E_OOM;
+    // the long-read class (ylen > short_y) only where this call has such reads
+    // (72 B per list entry: ~1.3 KB per read of a short-read lane otherwise)
+    if (ycap > short_y && (c->cread2.ensure(ccap * 4) || c->csid2.ensure(ccap * 4) || c->cout2.ensure(ccap * 64)))
         return IMSAME_E_OOM;
     if (poison_on()) {                        // this call's scratch holds nothing it may read
         const DBuf *scr[] = {&c->res, &c->cur_p, &c->cur_h, &c->memo, &c->nmemo, &c->rstat, &c->act0, &c->act1, &c->act2,
@@ -1531,6 +1551,30 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     HIPCHK(hipMemsetAsync(ctr, 0, C_NSLOTS * 8, s));
     const unsigned long long errinit = ~0ull;
     HIPCHK(hipMemcpyAsync(ctr + C_ERR, &errinit, 8, hipMemcpyHostToDevice, s));
+    // This lane's packed query words (seed_kernel.hip:pk_word; queued after
+    // the counters' reset: the packing flags a byte that is not ACGT in
+    // C_FLAGS): the words from QPAD bases before its first read to the end of
+    // its last part.  Each lane
+    // packs its own on its stream as its parts arrive (packing in the upload
+    // delayed every lane: the upload's kernels waited for free CUs behind NW
+    // waves, profiles/r5t/); neighbouring lanes both write the few words where
+    // their reaches meet, with the same values.
+    // Words are packed only where all 16 of their bytes are in HBM (below the
+    // end of the part waited for): a word at the edge of a part that is still
+    // copying would get garbage in the slots a neighbouring lane reads.
+    {
+        const uint64_t b0 = hqs(c, read_from), b1 = hqs(c, read_to) + 64;
+        uint64_t pe = c->qb_end;                          // end of the part query_wait waited for
+        for (size_t k = 0; k + 1 < c->q_part_end.size(); ++k)
+            if (c->q_part_end[k] >= b1) { pe = c->q_part_end[k]; break; }
+        const uint64_t w0 = std::max(c->qw_base, (b0 > QPAD ? b0 - QPAD : 0) / 16);
+        const uint64_t w1 = pe == c->qb_end ? c->qw_end : std::min(c->qw_end, pe / 16);
+        if (w1 > w0)
+            pack2_kernel<<<gsblk(w1 - w0, 256), 256, 0, s>>>(dev_q(c), (int64_t)c->q_base, (int64_t)c->qb_end,
+                                                             (uint32_t *)dev_qw(c), w0, w1,
+                                                             (unsigned long long *)(ctr + C_FLAGS));
+        HIPCHK(hipGetLastError());
+    }
     InitLaunch I = {qsd, read_from, n, c->res.as<imsame_read_result>(), c->cur_p.as<uint64_t>(),
                     c->cur_h.as<uint32_t>(), c->nmemo.as<uint8_t>(), c->rstat.as<uint8_t>(), c->act0.as<uint32_t>()};
     init_kernel<<<nblk(n, 256), 256, 0, s>>>(I);
@@ -1583,12 +1627,14 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         auto seed_launch = [&](const SeedLaunch &SL, uint32_t na, hipStream_t ss, hipEvent_t e0, hipEvent_t e1) -> int {
             const int L = RP.pick_L(rnd, na);
             const size_t slds = 256 * SEED_LDS_PER_LANE;
+            // (IMSAME_SEED_BLOCKS: at most this many blocks, the kernels stride)
+            auto sb = [&](uint64_t lanes) { return std::min<unsigned>(nblk(lanes, 256), seed_blocks()); };
             HIPCHK(hipEventRecord(e0, ss));
-            if (L >= 64)      seed_group_kernel<64, SPEC_BIG><<<nblk((uint64_t)na * 64, 256), 256, 256 * SPEC_BIG * 8, ss>>>(SL);
-            else if (L >= 16) seed_group_kernel<16><<<nblk((uint64_t)na * 16, 256), 256, slds, ss>>>(SL);
-            else if (L >= 4) seed_group_kernel<4><<<nblk((uint64_t)na * 4, 256), 256, slds, ss>>>(SL);
-            else if (L >= 2) seed_group_kernel<2><<<nblk((uint64_t)na * 2, 256), 256, slds, ss>>>(SL);
-            else             seed_kernel<<<nblk(na, 256), 256, 0, ss>>>(SL);
+            if (L >= 64)      seed_group_kernel<64, SPEC_BIG><<<sb((uint64_t)na * 64), 256, 256 * SPEC_BIG * 8, ss>>>(SL);
+            else if (L >= 16) seed_group_kernel<16><<<sb((uint64_t)na * 16), 256, slds, ss>>>(SL);
+            else if (L >= 4) seed_group_kernel<4><<<sb((uint64_t)na * 4), 256, slds, ss>>>(SL);
+            else if (L >= 2) seed_group_kernel<2><<<sb((uint64_t)na * 2), 256, slds, ss>>>(SL);
+            else             seed_kernel<<<sb(na), 256, 0, ss>>>(SL);
             POISON_SYNC(ss, "seed kernel", c);
             HIPCHK(hipEventRecord(e1, ss));
             HIPCHK(hipGetLastError());
@@ -1626,7 +1672,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
                            (uint32_t *)(ctr + nnext_slot), (unsigned long long *)(ctr + C_CELLS),
                            (unsigned long long *)(ctr + C_NACC), (unsigned long long *)(ctr + C_ERR),
                            c->db_start.as<uint64_t>(), ctr + C_FLAGS, (unsigned long long *)(ctr + C_WASTE)};
-            update_kernel<<<nblk(nc, 256), 256, 0, ss>>>(U);
+            update_kernel<<<std::min<unsigned>(nblk(nc, 256), upd_blocks()), 256, 0, ss>>>(U);
             POISON_SYNC(ss, "update_kernel", c);
             HIPCHK(hipGetLastError());
             return 0;
@@ -1653,7 +1699,10 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
             const char *sf = getenv("IMSAME_SPLIT_FRAC");            // the first half's share
             const double fa = sf ? std::max(0.05, std::min(0.95, atof(sf))) : 0.5;
             const uint32_t nA = std::max<uint32_t>(1, (uint32_t)(nact * fa)), nB = nact - nA;
-            const uint64_t offB = (uint64_t)S.spec * nA;               // the first half's list room
+            // the first half's list room: a read with no rejection yet may emit
+            // up to spec_weak (spec_after_first), more than spec when IMSAME_SPEC
+            // is set below it; nact x max(spec, spec_weak) <= ccap (RoundPolicy)
+            const uint64_t offB = (uint64_t)std::max(S.spec, S.spec_weak) * nA;
             // stream_b starts behind what stream s has queued (the counters' reset)
             HIPCHK(hipEventRecord(c->evb0, s));
             HIPCHK(hipStreamWaitEvent(sb, c->evb0, 0));
@@ -1908,6 +1957,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     st.nw_bytes = 2 * st.nw_cells;       // 2 B/cell traceback floor; bench.py adds xlen + ylen per NW
     int ret = IMSAME_OK;
     if (hc[C_FLAGS] & 4) return IMSAME_E_HIP;     // a non-persistent NW wave found no arena slot (never)
+    if (hc[C_FLAGS] & 8) return IMSAME_E_ARG;     // a query byte that is not ACGT (pack2_kernel)
     if (hc[C_ERR] != ~0ull) {
         st.err_read = hc[C_ERR] >> 32; st.err_dbseq = hc[C_ERR] & 0xFFFFFFFFull;
         ret = IMSAME_E_READ_TOO_LONG;

@@ -728,32 +728,43 @@ __global__ void accept_window_kernel(const SeedLaunch S, const imsame_read_resul
 #ifndef SEED_WAVES_PER_EU
 #define SEED_WAVES_PER_EU 4
 #endif
+// Wave-stride over the groups (a launch may hold fewer waves than groups,
+// imsame_dev.hip:seed_blocks; a wave's groups are consecutive, so the loop's
+// exit is wave-uniform)
 template <int L, int SM = SPEC_MAX>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SM > SPEC_MAX ? 1 : SEED_WAVES_PER_EU)))
 void seed_group_kernel(SeedLaunch S) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x & 63, wl = lane % L;
     uint2 *lst = (uint2 *)smem + threadIdx.x * SM;
-    const uint32_t gidx = (blockIdx.x * blockDim.x + threadIdx.x) / L;
+    constexpr uint32_t GPW = 64 / L;                       // groups per wave
+    const uint32_t nwv = gridDim.x * (blockDim.x >> 6);
     SeedTally tl;
-    seed_group<L, SM>(S, gidx, wl, lane, lst, tl);
+    for (uint32_t wv = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); (uint64_t)wv * GPW < S.n_active; wv += nwv)
+        seed_group<L, SM>(S, wv * GPW + (uint32_t)lane / L, wl, lane, lst, tl);
     seed_tally_flush(S, tl);
 }
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEED_WAVES_PER_EU))) void seed_kernel(SeedLaunch S) {
-    const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
     SeedTally tl;
-    if (idx < S.n_active) seed_one(S, idx, tl);
+    for (uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x; idx < S.n_active; idx += gridDim.x * blockDim.x)
+        seed_one(S, idx, tl);
     seed_tally_flush(S, tl);
 }
 
+// Grid-stride over the candidates: the host launches few waves (imsame_dev.hip:
+// upd_blocks).  A round's update is queued behind its NW launch while other
+// lanes' NW waves hold the chip; every wave it launches must win a slot
+// freed by one of those waves (each runs ~ms), so one wave per 64 candidates
+// -- 4.6k waves at C2's round 1 -- waited ~10 ms (profiles/r5end4/ C2
+// timeline: lane 2's round 1 ended at 79.8 ms, its round-2 scan began 90.7).
 __global__ void update_kernel(UpdLaunch U) {
-    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t cells = 0, acc = 0, waste = 0;
     // a non-persistent NW wave that found no arena slot left its candidates'
     // rows unwritten: consume none of them (the host fails the call)
     if (U.flags && (__hip_atomic_load(U.flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 4u)) return;
-    if (c < U.n) update_one(U, c, cells, acc, waste);
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < U.n; c += gridDim.x * blockDim.x)
+        update_one(U, c, cells, acc, waste);
     if (cells) atomicAdd(U.cells, (unsigned long long)cells);
     if (waste && U.waste) atomicAdd(U.waste, (unsigned long long)waste);
     if (acc) atomicAdd(U.nacc, (unsigned long long)acc);

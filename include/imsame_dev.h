@@ -191,7 +191,13 @@ const char *imsame_strerror(int code);
  * Sizes: db_len is u64 (databases past 4 Gbases index with 8-byte entries
  * {pos - record start, record}); n_db and each record's length must be
  * below 2^32 - 16 (IMSAME_E_ARG).  HBM: db_len x 5 B during the build,
- * plus 8 B per k-mer and 128 MB of bucket offsets. */
+ * plus 8 B per k-mer and 128 MB of bucket offsets.
+ * Bases: db_seq (and every query below) holds only the bytes 'A', 'C', 'G',
+ * 'T' -- what IMSAME's loaders keep (toupper, then drop the rest).  The seed
+ * stage compares 2-bit codes, which alias every other byte to one of them, so
+ * the build checks every byte and returns IMSAME_E_ARG on any other one;
+ * imsame_dev_align* do the same for the bytes of the reads they align (the
+ * check runs inside the query's 2-bit packing kernel). */
 int imsame_dev_index(imsame_ctx *ctx, const uint8_t *db_seq, uint64_t db_len,
                      const uint64_t *db_start, uint64_t n_db, const uint8_t *db_brk);
 

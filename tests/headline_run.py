@@ -7,6 +7,9 @@ the call runs 4 lanes, two streams each, on 8 hardware queues -- then read-for-r
 with the oracle on the start, middle (a chunk head) and end windows.
 
     python -m tests.headline_run        -> one JSON line on stdout
+    python -m tests.headline_run --all  -> ... with EVERY one of the 1M rows
+                                           compared (the oracle on the host's
+                                           usable CPUs, ~2 min at 16)
 
 Run as a subprocess by tests/test_gpu.py::test_headline_mode_parity (the
 pytest process's HIP runtime has already read its own GPU_MAX_HW_QUEUES).
@@ -39,7 +42,16 @@ def main():
         res, _, st = dev.align(n_threads=16)
         res = res.copy()
         pin.free()
-    out = parity.check_windows(Oracle.load(), ref, rst, q, qs, res, 0, parity.windows(0, len(qs), len(qs), 16), 16)
+    if "--all" in sys.argv:
+        # every row: 4 oracle calls of one thread per -n_threads chunk, a
+        # progress line on stderr after each (a run of ~2 min that prints)
+        def progress(k, n, tot):
+            print(f"[headline_run] oracle part {k}/{n}: {tot['identical']}/{tot['reads_compared']} identical, "
+                  f"{time.time() - t0:.0f} s", file=sys.stderr, flush=True)
+        out = parity.check_all(Oracle.load(), ref, rst, q, qs, res, 16, parts=4, progress=progress)
+    else:
+        out = parity.check_windows(Oracle.load(), ref, rst, q, qs, res, 0, parity.windows(0, len(qs), len(qs), 16),
+                                   16)
     out.update({"lanes": int(st.lanes), "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                 "reads": len(qs), "accepted": int((res["status"] == 1).sum()), "n_nw": int(st.n_nw),
                 "ms_align": round(st.ms_total, 3), "wall_s": round(time.time() - t0, 1)})

@@ -57,3 +57,39 @@ def check_windows(oracle, ref, rst, q, qs, res, res_lo, wins, n_threads, params=
             "n_threads": n_threads, "oracle_rc": int(rc), "first_mismatches": bad,
             "accepted_in_windows": int(sum(int((res[a - res_lo:b - res_lo]["status"] == 1).sum()) for a, b in wins)),
             "oracle_nw_distinct": nw_distinct, "oracle_nw_reference": nw_ref}
+
+
+def chunk_slices(n_total, n_threads, parts):
+    """Every read of an n_total-read query, as `parts` calls of n_threads
+    windows each: call p holds the p-th of `parts` slices of every -n_threads
+    chunk [t*floor(n/T), (t+1)*floor(n/T)) (the last chunk runs to the end), so
+    each oracle call keeps one thread per chunk busy (IMSAME.c:414,430-452)."""
+    T = max(n_threads, 1)
+    rpt = n_total // T
+    bounds = [(t * rpt, n_total if t == T - 1 else (t + 1) * rpt) for t in range(T)] if rpt else [(0, n_total)]
+    calls = []
+    for p in range(parts):
+        wins = []
+        for f, e in bounds:
+            a, b = f + (e - f) * p // parts, f + (e - f) * (p + 1) // parts
+            if b > a:
+                wins.append((a, b))
+        calls.append(wins)
+    return calls
+
+
+def check_all(oracle, ref, rst, q, qs, res, n_threads, parts=4, params=None, progress=None):
+    """EVERY read of the query against the oracle (its memo of rejected
+    pairs on, as check_windows): `parts` oracle calls of n_threads windows
+    (chunk_slices), each followed by a progress callback."""
+    tot = {"reads_compared": 0, "identical": 0, "first_mismatches": [], "oracle_rc": 0, "parts": parts,
+           "n_threads": n_threads}
+    for k, wins in enumerate(chunk_slices(len(qs), n_threads, parts)):
+        out = check_windows(oracle, ref, rst, q, qs, res, 0, wins, n_threads, params)
+        tot["reads_compared"] += out["reads_compared"]
+        tot["identical"] += out["identical"]
+        tot["first_mismatches"] += out["first_mismatches"][:3]
+        tot["oracle_rc"] = tot["oracle_rc"] or out["oracle_rc"]
+        if progress:
+            progress(k + 1, parts, tot)
+    return tot
