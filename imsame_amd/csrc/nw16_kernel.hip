@@ -135,10 +135,72 @@ WV_DEVICE int pk_half(uint32_t v, int h) { return (int)(int16_t)(h ? (v >> 16) :
 WV_DEVICE int pk_score(uint32_t v, int h) { return (int)(h ? (v >> 16) : (v & 0xFFFFu)) - 32768; }
 WV_DEVICE uint32_t base_code(uint8_t b) { return (b >> 1) & 3u; }          // A0 C1 T2 G3: distinct
 
-// score table for v_perm: selector byte d = xcode ^ ycode picks the low byte
-// (d in 0..3) and, with bit 2 set, the high byte (4..7) of s = d ? -4 : +4
+// The substitution score of a cell pair.  NW16_ROWTAB (the default, round
+// 6): each step builds two ROW tables from the row's record codes -- tlo =
+// 8 << 8*xA (byte xA of A's table is 8, the others 0) and thi = 8 << 8*xB --
+// and each column keeps a constant selector ysel = [yA, 0x0C, 4 + yB, 0x0C],
+// so one v_perm gives [8*(xA==yA), 0, 8*(xB==yB), 0] and one v_add3_u32 adds
+// it with the -4 of a mismatch folded in (max + s8 - 0x00040004; biased
+// halves never carry across).  Per cell pair: perm + add3 instead of xor +
+// perm + pk_add -- one instruction fewer, for 4 per step to build the tables
+// (3 before: the xor selector).  The LDS record byte of a row pair is xA << 3
+// | xB << 5, so tlo is one v_lshlrev (the shift uses the low 5 bits).
+// Otherwise (NW16_ROWTAB=0): a constant table indexed by xcode ^ ycode.
+#ifndef NW16_ROWTAB
+#define NW16_ROWTAB 1
+#endif
 #define NW16_TBL_LO 0xFCFCFC04u
 #define NW16_TBL_HI 0xFFFFFF00u
+#if NW16_ROWTAB
+#define NW16_XSH_A 3              // bit of A's record code in the LDS row byte
+#define NW16_XSH_B 5              // ... and of B's
+#else
+#define NW16_XSH_A 0
+#define NW16_XSH_B 2
+#endif
+#define NW16_XM_A (3u << NW16_XSH_A)
+#define NW16_XM_B (3u << NW16_XSH_B)
+// a row pair's table (ROWTAB: tlo, thi; else the xor selector in lo)
+struct Nw16Row { uint32_t lo, hi; };
+WV_DEVICE Nw16Row nw16_row(uint32_t xb) {
+#if NW16_ROWTAB
+    return {8u << (xb & 31u), 8u << ((xb >> 2) & 0x18u)};
+#else
+    return {wv_perm(xb >> 2, xb & 3u, 0x04040000u), 0u};
+#endif
+}
+// a column's constant operand for the codes ya, yb of its two halves
+WV_DEVICE uint32_t nw16_ycol(uint32_t ya, uint32_t yb) {
+#if NW16_ROWTAB
+    return ya | (0x0Cu << 8) | ((yb + 4u) << 16) | (0x0Cu << 24);
+#else
+    return ya | ((ya | 4u) << 8) | (yb << 16) | ((yb | 4u) << 24);
+#endif
+}
+// the cell pair's score term (ROWTAB: 0 / 8 per half; else +-4 as int16)
+WV_DEVICE uint32_t nw16_sc(const Nw16Row &r, uint32_t ycol) {
+#if NW16_ROWTAB
+    return wv_perm(r.hi, r.lo, ycol);
+#else
+    return wv_perm(NW16_TBL_HI, NW16_TBL_LO, r.lo ^ ycol);
+#endif
+}
+// T = max + score (biased halves)
+WV_DEVICE uint32_t nw16_add_sc(uint32_t m, uint32_t sc) {
+#if NW16_ROWTAB
+    return m + sc + 0xFFFBFFFCu;                  // + s8 - 0x00040004: one v_add3_u32
+#else
+    return pk_add(m, sc);
+#endif
+}
+// the biased score itself (row 0, column 0: T = score)
+WV_DEVICE uint32_t nw16_sc_biased(uint32_t sc) {
+#if NW16_ROWTAB
+    return sc + 0x7FFC7FFCu;                      // s8 - 4 + 2^15 per half
+#else
+    return sc ^ 0x80008000u;
+#endif
+}
 
 // cell s of half h in one lane's traceback words of a step (layout above) ->
 // nw_kernel.hip's nibble: move (0 diag, 1 up, 2 left) | U << 2 | L << 3
@@ -173,7 +235,9 @@ struct TbAcc16 {
         const int l = (j + OFF) / K, s = (j + OFF) - l * K;
         return tb16_nib<K>(tb + ((uint32_t)(i + l - t0) * 64u + (uint32_t)(g * G + l)) * (uint32_t)nw16_nrec(K), s, h);
     }
-    __device__ bool match(int i, int j) const { return ((X[i] >> (2 * h)) & 3u) == base_code(Y[j]); }
+    __device__ bool match(int i, int j) const {
+        return ((X[i] >> (h ? NW16_XSH_B : NW16_XSH_A)) & 3u) == base_code(Y[j]);
+    }
 };
 
 // one lane's traceback words of one step (layout above), built cell by cell
@@ -291,8 +355,9 @@ __device__ __forceinline__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const
                 }
                 uint32_t o[4];
 #pragma unroll
-                for (int q = 0; q < 4; ++q)   // base_code per byte: (b >> 1) & 3; B's code at bits 2-3
-                    o[q] = ((w[0][q] >> 1) & 0x03030303u) | ((w[1][q] << 1) & 0x0C0C0C0Cu);
+                for (int q = 0; q < 4; ++q)   // base_code per byte: (b >> 1) & 3, A's at NW16_XSH_A, B's at _B
+                    o[q] = (((w[0][q] >> 1) << NW16_XSH_A) & (NW16_XM_A * 0x01010101u)) |
+                           (((w[1][q] >> 1) << NW16_XSH_B) & (NW16_XM_B * 0x01010101u));
                 __builtin_memcpy(X8 + k0, o, 16);
             }
         }
@@ -354,21 +419,19 @@ __device__ __forceinline__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const
             const int j = j0 + s;
             const uint32_t ya = (valid[0] && j >= 0 && j < yl[0]) ? base_code(Yp[0][j]) : 0u;
             const uint32_t yb = (valid[0] && j >= 0 && j < yl[1]) ? base_code(Yp[1][j]) : 0u;
-            yreg[s] = ya | ((ya | 4u) << 8) | (yb << 16) | ((yb | 4u) << 24);
+            yreg[s] = nw16_ycol(ya, yb);
             lastm[s] = ((ownC[0] && yl[0] - 1 - j0 == s) ? 0x0000FFFFu : 0u) |
                        ((ownC[1] && yl[1] - 1 - j0 == s) ? 0xFFFF0000u : 0u);
         }
-        // [xA, xA, xB, xB] selector bytes of an LDS row byte
-        auto xsel_of = [](uint32_t xb) { return wv_perm(xb >> 2, xb & 3u, 0x04040000u); };
         // row 0 (:404-413)
         uint32_t xrow = valid[0] ? X8[0] : 0u;
-        const uint32_t xsel0 = xsel_of(xrow);
-        uint32_t yprev = 0;
+        const Nw16Row xr0 = nw16_row(xrow);
+        uint32_t yprev = nw16_ycol(0u, 0u);
         if (valid[0] && j0 > 0) {
             const uint32_t ya = base_code(Yp[0][min(j0 - 1, yl[0] - 1)]), yb = base_code(Yp[1][min(j0 - 1, yl[1] - 1)]);
-            yprev = ya | ((ya | 4u) << 8) | (yb << 16) | ((yb | 4u) << 24);
+            yprev = nw16_ycol(ya, yb);
         }
-        const uint32_t t0prev = wv_perm(NW16_TBL_HI, NW16_TBL_LO, xsel0 ^ yprev) ^ NW16_H;
+        const uint32_t t0prev = nw16_sc_biased(nw16_sc(xr0, yprev));
         // The column state keeps mc's score in a frame shifted by ig + eg: dI[s]
         // = T[i-2][j-1] + ig + eg is the previous row's d0 + ig + eg of this
         // slot (the left take computes it anyway), so the column max compares
@@ -377,7 +440,7 @@ __device__ __forceinline__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const
         uint32_t A[K], B[K], dI[K], mcS[K], u0[K];
 #pragma unroll
         for (int s = 0; s < K; ++s) {
-            A[s] = wv_perm(NW16_TBL_HI, NW16_TBL_LO, xsel0 ^ yreg[s]) ^ NW16_H;
+            A[s] = nw16_sc_biased(nw16_sc(xr0, yreg[s]));
             B[s] = A[s];
         }
 #pragma unroll
@@ -402,7 +465,7 @@ __device__ __forceinline__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const
             const uint32_t sN = (uint32_t)wv_shr1((int)outT), mS = (uint32_t)wv_shr1((int)outMS),
                            mL0 = (uint32_t)wv_shr1((int)outL);
             const int i = t - gl;
-            const uint32_t xsel = xsel_of(xrow);
+            const Nw16Row xr = nw16_row(xrow);
             xrow = CAREFUL ? X8[min(max(i + 1, 0), xcl)] : X8[i + 1];          // next row, read ahead
             const bool pre = PRE && i < 1;
             const bool row1 = CAREFUL && i <= 1;                     // up invalid, mc frozen (:449, :476)
@@ -412,11 +475,11 @@ __device__ __forceinline__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const
             for (int s = 0; s < K; ++s) {
                 const uint32_t d0 = (s == 0) ? in1 : own[s - 1];     // T[i-1][j-1]
                 const uint32_t tl = (s == 0) ? sN : cur[s - 1];      // T[i][j-1]
-                const uint32_t sc = wv_perm(NW16_TBL_HI, NW16_TBL_LO, xsel ^ yreg[s]);
+                const uint32_t sc = nw16_sc(xr, yreg[s]);
                 const uint32_t up = row1 ? NBIG : u0[s];
                 const uint32_t lu = pk_maxu(l0, up);
-                uint32_t v = pk_add(pk_maxu(d0, lu), sc);
-                if (s == OFF) v = leadc0 ? (sc ^ NW16_H) : v;                    // column 0 (:426)
+                uint32_t v = nw16_add_sc(pk_maxu(d0, lu), sc);
+                if (s == OFF) v = leadc0 ? nw16_sc_biased(sc) : v;               // column 0 (:426)
                 cur[s] = pre ? own[s] : v;
                 // move bits: signs of (d0 - lu) [not diagonal] and (l0 - up) [up > left] (:457-472)
                 // (sign-replicating selectors 8-11: bytes 0xFF / 0x00, no shift before packing)
@@ -608,8 +671,8 @@ __device__ __forceinline__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const
             const uint32_t sN = (uint32_t)wv_shr1((int)outT), mS = (uint32_t)wv_shr1((int)outMS),
                            mL0 = (uint32_t)wv_shr1((int)outL);
             const int iA = t0h[0] + tau - gl, iB = t0h[1] + tau - gl;
-            const uint32_t xsel = xsel_of(xrow);
-            xrow = (X8[min(max(iA + 1, 0), xcl)] & 3u) | (X8[min(max(iB + 1, 0), xcl)] & 0xCu);
+            const Nw16Row xr = nw16_row(xrow);
+            xrow = (X8[min(max(iA + 1, 0), xcl)] & NW16_XM_A) | (X8[min(max(iB + 1, 0), xcl)] & NW16_XM_B);
             // per-half forms of pass 1's `pre` (i < 1: row 0 repeats) and `row1` (i <= 1)
             const uint32_t pm = !MASK ? 0u : (iA < 1 ? 0x0000FFFFu : 0u) | (iB < 1 ? 0xFFFF0000u : 0u);
             const uint32_t r1 = !MASK ? 0u : (iA <= 1 ? 0x0000FFFFu : 0u) | (iB <= 1 ? 0xFFFF0000u : 0u);
@@ -619,11 +682,11 @@ __device__ __forceinline__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const
             for (int s = 0; s < K; ++s) {
                 const uint32_t d0 = (s == 0) ? in1 : own[s - 1];
                 const uint32_t tl = (s == 0) ? sN : cur[s - 1];
-                const uint32_t sc = wv_perm(NW16_TBL_HI, NW16_TBL_LO, xsel ^ yreg[s]);
+                const uint32_t sc = nw16_sc(xr, yreg[s]);
                 const uint32_t up = MASK ? wv_bfi(r1, NBIG, u0[s]) : u0[s];
                 const uint32_t lu = pk_maxu(l0, up);
-                uint32_t v = pk_add(pk_maxu(d0, lu), sc);
-                if (s == OFF) v = leadc0 ? (sc ^ NW16_H) : v;
+                uint32_t v = nw16_add_sc(pk_maxu(d0, lu), sc);
+                if (s == OFF) v = leadc0 ? nw16_sc_biased(sc) : v;
                 cur[s] = MASK ? wv_bfi(pm, own[s], v) : v;
                 const uint32_t P2 = wv_perm(pk_sub(l0, up), pk_sub(d0, lu), 0x0B0A0908u);
                 const uint32_t mU = pk_neg_mask(pk_sub(mcS[s], dI[s]));
@@ -664,7 +727,7 @@ __device__ __forceinline__ void nw16_wave(const NwLaunch &P, uint8_t *wsm, const
                 outT = ld(4 * K + 2); outMS = ld(4 * K + 3); outL = ld(4 * K + 4);
 #pragma unroll
                 for (int s = 0; s < K; ++s) dI[s] = (s ? A[s - 1] : I2) - IGEN;    // (save())
-                xrow = (X8[min(max(t0h[0] - gl, 0), xcl)] & 3u) | (X8[min(max(t0h[1] - gl, 0), xcl)] & 0xCu);
+                xrow = (X8[min(max(t0h[0] - gl, 0), xcl)] & NW16_XM_A) | (X8[min(max(t0h[1] - gl, 0), xcl)] & NW16_XM_B);
             }
             // rows <= 1 need the masked step: while tau <= G - min(t0h) (wave-uniform bound)
             // (every half counts: one that is done still computes, and stays a bounded DP)
