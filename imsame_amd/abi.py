@@ -79,7 +79,7 @@ class Stats(C.Structure):
         ("ms_nw_last", C.c_double), ("launch_k5", C.c_uint64), ("launch_np", C.c_uint64),
         ("launch_k19", C.c_uint64), ("launch_nwp", C.c_uint64), ("nw_fallback", C.c_uint64),
         ("seed_windows", C.c_uint64), ("seed_entries", C.c_uint64), ("seed_ext_chunks", C.c_uint64),
-        ("nw_spec_waste", C.c_uint64),
+        ("nw_spec_waste", C.c_uint64), ("launch_k3", C.c_uint64),
     ]
 
     def as_dict(self):

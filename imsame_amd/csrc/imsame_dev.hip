@@ -1049,9 +1049,9 @@ static int nw16_band_rows() {
 // lane of a call -- whose read lengths differ -- share one layout.
 static void np_strides(uint32_t xcap, uint64_t *tb_dw, uint64_t *ck_dw) {
     const NwShape a = nw16_shape(NW_W / 2, xcap, NW16_K), b = nw16_shape(NW_W / 2, xcap, NW16_K5),
-                  d = nw16_shape(NW16_K19_YLEN, xcap, NW16_K19);
-    *tb_dw = std::max(std::max(nw16_tb_words(a), nw16_tb_words(b)), nw16_tb_words(d));
-    *ck_dw = std::max(std::max(nw16_ck_words(a), nw16_ck_words(b)), nw16_ck_words(d));
+                  d = nw16_shape(NW16_K19_YLEN, xcap, NW16_K19), e = nw16_shape(NW16_K3_YMAX, xcap, NW16_K3);
+    *tb_dw = std::max(std::max(nw16_tb_words(a), nw16_tb_words(b)), std::max(nw16_tb_words(d), nw16_tb_words(e)));
+    *ck_dw = std::max(std::max(nw16_ck_words(a), nw16_ck_words(b)), std::max(nw16_ck_words(d), nw16_ck_words(e)));
 }
 
 // Blocks per CU the XCD partitions of a context's slot bitmap hold: the
@@ -1073,6 +1073,8 @@ static int nw16_np_part_cu(imsame_ctx *c) {
     q((const void *)nw16_kernel<NW16_K5, false, false>); q((const void *)nw16_kernel<NW16_K5, true, false>);
     q((const void *)nw16_kernel<NW16_K19, true, true, NW16_K19_OFF>);
     q((const void *)nw16_kernel<NW16_K19, true, false, NW16_K19_OFF>);
+    q((const void *)nw16_kernel<NW16_K3, false, true>); q((const void *)nw16_kernel<NW16_K3, true, true>);
+    q((const void *)nw16_kernel<NW16_K3, false, false>); q((const void *)nw16_kernel<NW16_K3, true, false>);
     c->np_part_cu = ok ? m : 0;
     return c->np_part_cu;
 }
@@ -1095,9 +1097,18 @@ static int nw16_np_part_cu(imsame_ctx *c) {
 // 1.69 / 1.72 / 1.79 (K = 19) (profiles/r5y/nwsmall_r5y.json); the 1/4 shard's
 // round-2 launches (~2.9k candidates) went 1.1-1.9 -> 0.8-1.4 ms and the
 // shard 29.7 -> 28.8 ms, C2 and the 1/8 shard unchanged (profiles/r5z/).
+// Round 6: the 3-column latency form (NW16_K3) takes a lane's launches of
+// rounds >= 2 below IMSAME_NW_K3_MAX candidates (reads <= NW16_K3_YMAX; the
+// caller checks the range proof for its shape); IMSAME_NW_K=3 forces it.
+static uint32_t nw16_k3_max() {
+    static uint32_t v = [] { const char *e = getenv("IMSAME_NW_K3_MAX"); return e ? (uint32_t)atoi(e) : 3000u; }();
+    return v;
+}
 static int nw16_k(imsame_ctx *c, uint32_t ncand, bool rounds) {
     const char *e = getenv("IMSAME_NW_K"), *fe = getenv("IMSAME_NW_K5_FILL"), *f2 = getenv("IMSAME_NW_K5_FILL2");
     const int force = e ? atoi(e) : 0;
+    if (force == NW16_K3) return NW16_K3;
+    if (rounds && c->cur_round >= 2 && ncand <= nw16_k3_max()) return NW16_K3;
     // a lane's launches of rounds >= 2 (IMSAME_NW_K5_FILL2, 1.5: below ~16k
     // candidates with 3 lanes): C2's round-2 launches of ~15.5k candidates
     // run one or two 19-column waves per SIMD, latency-bound; the 5-column
@@ -1138,6 +1149,13 @@ static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, 
     }
     pl->lp = pl->lng && nwp_enabled() && nwp_fits(p->igap, p->egap, xcap, ymax);
     pl->k = pl->pk ? nw16_k(c, ncand, rounds) : 0;
+    if (pl->k == NW16_K3) {
+        // the latency form: reads <= NW16_K3_YMAX (CK + G <= 64, nw16_fits) whose
+        // values fit its wider column count; LAST when the launch's one read
+        // length is a multiple of 3 (ylen_mult speaks of NW16_K)
+        if (ymax > NW16_K3_YMAX || !nw16_fits(p->igap, p->egap, xcap, ymax, NW16_K3)) pl->k = NW16_K5;
+        else pl->last4 = ylen_uni && ylen_uni == ymax && ylen_uni % NW16_K3 == 0;
+    }
     if (pl->pk && pl->k == NW16_K && nw16_k19_ok(ylen_uni, ymax, xcap, p)) {
         pl->k = NW16_K19;
         pl->last4 = true;                   // 150 = 8 x 19 - OFF: last column in slot K-1
@@ -1152,9 +1170,13 @@ static int plan_nw(imsame_ctx *c, uint32_t ymax, uint32_t xcap, uint32_t ncand, 
     pl->lds = (size_t)wpb * (pl->pk ? nw16_wave_lds(pl->GPW, pl->xstride)
                              : pl->lng ? nwl_wave_lds(pl->xstride) : nw_wave_lds(pl->GPW, pl->xstride));
     int per_cu = 0;
-    const bool k5 = pl->k == NW16_K5, k19 = pl->k == NW16_K19;
+    const bool k5 = pl->k == NW16_K5, k19 = pl->k == NW16_K19, k3 = pl->k == NW16_K3;
     hipError_t oe = pl->lp ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nwp_kernel, wpb * 64, pl->lds)
                   : pl->lng ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nwl_kernel, wpb * 64, pl->lds)
+                  : k3 ? (pl->two ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw16_kernel<NW16_K3, false, true>,
+                                                                             wpb * 64, pl->lds)
+                                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nw16_kernel<NW16_K3, false, false>,
+                                                                             wpb * 64, pl->lds))
                   : k19 ? (pl->two ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
                                          &per_cu, nw16_kernel<NW16_K19, true, true, NW16_K19_OFF>, wpb * 64, pl->lds)
                                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(
@@ -1373,6 +1395,10 @@ static int launch_nw(imsame_ctx *c, NwPlan &pl, const uint32_t *cread, const uin
     else if (pl.lng)                   nwl_kernel<<<pl.blocks, 256, pl.lds, s>>>(P);
     else if (pl.k == NW16_K19 && pl.two) nw16_kernel<NW16_K19, true, true, NW16_K19_OFF><<<pl.blocks, 256, pl.lds, s>>>(P);
     else if (pl.k == NW16_K19)         nw16_kernel<NW16_K19, true, false, NW16_K19_OFF><<<pl.blocks, 256, pl.lds, s>>>(P);
+    else if (pl.k == NW16_K3 && pl.two && pl.last4) nw16_kernel<NW16_K3, true, true><<<pl.blocks, 256, pl.lds, s>>>(P);
+    else if (pl.k == NW16_K3 && pl.two) nw16_kernel<NW16_K3, false, true><<<pl.blocks, 256, pl.lds, s>>>(P);
+    else if (pl.k == NW16_K3 && pl.last4) nw16_kernel<NW16_K3, true, false><<<pl.blocks, 256, pl.lds, s>>>(P);
+    else if (pl.k == NW16_K3)          nw16_kernel<NW16_K3, false, false><<<pl.blocks, 256, pl.lds, s>>>(P);
     else if (pl.two && pl.last4 && k5) nw16_kernel<NW16_K5, true, true><<<pl.blocks, 256, pl.lds, s>>>(P);
     else if (pl.two && k5)             nw16_kernel<NW16_K5, false, true><<<pl.blocks, 256, pl.lds, s>>>(P);
     else if (pl.pk && pl.last4 && k5)  nw16_kernel<NW16_K5, true, false><<<pl.blocks, 256, pl.lds, s>>>(P);
@@ -1657,6 +1683,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
                 st.launch_ms[st.nw_launches] = ms;
                 if (pl.pk) st.launch_pk |= 1ull << st.nw_launches;
                 if (pl.pk && pl.k == NW16_K5) st.launch_k5 |= 1ull << st.nw_launches;
+                if (pl.pk && pl.k == NW16_K3) st.launch_k3 |= 1ull << st.nw_launches;
                 if (pl.np) st.launch_np |= 1ull << st.nw_launches;
                 if (pl.pk && pl.k == NW16_K19) st.launch_k19 |= 1ull << st.nw_launches;
                 if (pl.lp) st.launch_nwp |= 1ull << st.nw_launches;

@@ -75,6 +75,13 @@
 
 #define NW16_K   10               // columns per lane (the full-chip launches)
 #define NW16_K5  5                // columns per lane of the latency-bound launches (nw16_k)
+// The latency form (round 6): 3 columns per lane, one candidate pair per
+// wave (G = 50 at 150 bp).  A lone wave issues its row step serially -- ~16
+// VALU per column plus ~20 per step -- so a launch of a few hundred waves
+// lasts about xlen steps of that chain: 5 columns cost ~100 VALU per step, 3
+// cost ~70.  For the small launches of the last rounds (imsame_dev.hip:nw16_k).
+#define NW16_K3  3
+#define NW16_K3_YMAX 150          // G <= 50: nw16_ck(3) + G <= 64 (the range proof's extra rows)
 #define NW16_BIG 16384
 // Checkpoint interval of the first sweep, per column form (steps; even: the
 // rotation period).  nw16_fits bounds the rows a second sweep runs past the
@@ -83,7 +90,8 @@
 // round 3 wrote 5K+5 every 24 steps (0.46 B/cell at C2), 4K+5 every 48 is
 // ~0.19 B/cell, for ~8 more second-sweep rows per half on average -- only
 // for the halves the first sweep's predicted window does not cover.
-__host__ __device__ constexpr int nw16_ck(int K) { return K <= 5 ? 32 : 48; }
+// (K = 3: G <= 50, so CK 14)
+__host__ __device__ constexpr int nw16_ck(int K) { return K <= 3 ? 14 : K <= 5 ? 32 : 48; }
 // dwords of wave state per lane in a checkpoint (A, B, mcS, u0 per column; I1,
 // I2, outT, outMS, outL); dI is a function of A and I2 there (save())
 __host__ __device__ constexpr int nw16_nst(int K) { return 4 * K + 5; }
@@ -859,6 +867,11 @@ __global__ void xcc_probe_kernel(uint32_t *out) {
 #ifndef NW16_K5_WAVES_PER_EU
 #define NW16_K5_WAVES_PER_EU 5
 #endif
+// (K = 3 needs fewer registers; 5 keeps the context's slot partitions --
+// the largest residency of any packed form, nw16_np_part_cu -- unchanged)
+#ifndef NW16_K3_WAVES_PER_EU
+#define NW16_K3_WAVES_PER_EU 5
+#endif
 // the 19-column form holds 6 x 19 per-column registers: 2 waves per SIMD (256
 // VGPRs), which the first-sweep loop's ILP keeps issuing (a 2-wave SIMD ran
 // the 10-column loop at 4.0 cycles per VALU, profiles/r4b/micro_*)
@@ -867,7 +880,9 @@ __global__ void xcc_probe_kernel(uint32_t *out) {
 #endif
 template <int K, bool LAST, bool TWO, int OFF = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K > 10 ? NW16_K19_WAVES_PER_EU
-                                                                     : K > 8 ? NW16_WAVES_PER_EU : NW16_K5_WAVES_PER_EU)))
+                                                                     : K > 8 ? NW16_WAVES_PER_EU
+                                                                     : K > 3 ? NW16_K5_WAVES_PER_EU
+                                                                             : NW16_K3_WAVES_PER_EU)))
 void nw16_kernel(NwLaunch P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;

@@ -160,6 +160,9 @@ typedef struct imsame_stats {
                                NW calls (alignmentFunctions.c:126-186), which
                                also repeats a rejected record at each of its
                                e-value-passing hits                        */
+    uint64_t launch_k3;     /* bit k: packed NW launch k ran the 3-column
+                               latency form (one pair per wave, 50 lanes at
+                               150 bp: the fewest instructions per row step) */
 } imsame_stats;
 
 typedef struct imsame_ctx imsame_ctx;

@@ -25,6 +25,7 @@ FORMS = {                      # name -> (flags, environment)
     "k19": ("NW16", {}),
     "k10": ("NW16", {"IMSAME_NW_K19": "0"}),
     "k5": ("NW16", {"IMSAME_NW_K": "5"}),
+    "k3": ("NW16", {"IMSAME_NW_K": "3"}),
 }
 
 
@@ -49,7 +50,7 @@ def pairs(n, kind, xlen, ylen, seed):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sizes", default="1,16,128,512,1400,4096")
-    ap.add_argument("--forms", default="int32,k19,k10,k5")
+    ap.add_argument("--forms", default="int32,k19,k10,k5,k3")
     ap.add_argument("--xlen", type=int, default=2000)
     ap.add_argument("--ylen", type=int, default=150)
     ap.add_argument("--reps", type=int, default=5)

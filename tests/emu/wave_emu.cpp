@@ -126,8 +126,9 @@ static uint32_t g_win;
 extern "C" uint32_t emu_win_count(void) { const uint32_t r = g_win; g_win = 0; return r; }
 
 // packed launches that ran the 19-column form (nw16_k19_ok), since the last emu_k19_count()
-static uint32_t g_k19;
+static uint32_t g_k19, g_k3;
 extern "C" uint32_t emu_k19_count(void) { const uint32_t r = g_k19; g_k19 = 0; return r; }
+extern "C" uint32_t emu_k3_count(void) { const uint32_t r = g_k3; g_k3 = 0; return r; }
 // long-read launches that ran the packed kernel (nwp_fits), and its waves that
 // fell back to the int32 path, since the last emu_nwp_count()
 static uint32_t g_nwp, g_fbk;
@@ -171,8 +172,11 @@ static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, cons
     const char *ke = getenv("IMSAME_NW_K");
     uint32_t yuni = n ? (uint32_t)(qs[cread[0] + 1] - qs[cread[0]]) : 0;    // one read length? (nw16_k19_ok)
     for (uint32_t k = 0; k < n; ++k) if (qs[cread[k] + 1] - qs[cread[k]] != yuni) yuni = 0;
-    const int K = (ke && atoi(ke) == NW16_K5) ? NW16_K5
-                : (pk && nw16_k19_ok(yuni, ymax, xmax, p)) ? NW16_K19 : NW16_K;
+    int K = (ke && atoi(ke) == NW16_K5) ? NW16_K5
+          : (pk && nw16_k19_ok(yuni, ymax, xmax, p)) ? NW16_K19 : NW16_K;
+    // IMSAME_NW_K=3: the latency form where it applies (imsame_dev.hip:plan_nw)
+    if (ke && atoi(ke) == NW16_K3)
+        K = (ymax <= NW16_K3_YMAX && nw16_fits(p->igap, p->egap, xmax, ymax, NW16_K3)) ? NW16_K3 : NW16_K5;
     const NwShape sh = pk ? nw16_shape(ymax, xmax, K) : lp ? nwp_shape(ymax, xmax) : lng ? nwl_shape(ymax, xmax)
                      : nw_shape(ymax, xmax);
     // waves of the launch (one arena slot each), as many as it has tasks
@@ -249,6 +253,15 @@ static int run_nw(const uint8_t *db, const uint64_t *dbs, const uint8_t *q, cons
         ++g_k19;
         if (two) run_waves(nwv, [&](int lane, int w) { nw16_wave<NW16_K19, true, true, NW16_K19_OFF>(P, lds.data() + w * lds_slot, lane, (uint32_t)w); });
         else     run_waves(nwv, [&](int lane, int w) { nw16_wave<NW16_K19, true, false, NW16_K19_OFF>(P, lds.data() + w * lds_slot, lane, (uint32_t)w); });
+    }
+    else if (pk && K == NW16_K3) {
+        ++g_k3;
+        bool m3 = true;       // every read length a multiple of 3 (imsame_dev.hip:plan_nw's LAST for K = 3)
+        for (uint32_t k = 0; k < n; ++k) m3 = m3 && (qs[cread[k] + 1] - qs[cread[k]]) == ymax && ymax % NW16_K3 == 0;
+        if (two && m3)        run_waves(nwv, [&](int lane, int w) { nw16_wave<NW16_K3, true, true>(P, lds.data() + w * lds_slot, lane, (uint32_t)w); });
+        else if (two)         run_waves(nwv, [&](int lane, int w) { nw16_wave<NW16_K3, false, true>(P, lds.data() + w * lds_slot, lane, (uint32_t)w); });
+        else if (m3)          run_waves(nwv, [&](int lane, int w) { nw16_wave<NW16_K3, true, false>(P, lds.data() + w * lds_slot, lane, (uint32_t)w); });
+        else                  run_waves(nwv, [&](int lane, int w) { nw16_wave<NW16_K3, false, false>(P, lds.data() + w * lds_slot, lane, (uint32_t)w); });
     }
     else if (pk && K == NW16_K5) {
         if (two && ymult)     run_waves(nwv, [&](int lane, int w) { nw16_wave<NW16_K5, true, true>(P, lds.data() + w * lds_slot, lane, (uint32_t)w); });

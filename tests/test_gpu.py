@@ -33,10 +33,15 @@ def _cmp(r_dev, r_ref, limit=None):
     return bad
 
 
-@pytest.mark.parametrize("flags", [0, FLAG_NW32], ids=["auto", "nw32"])
-def test_nw_pairs_match_reference_golden(dev, oracle, flags):
+@pytest.mark.parametrize("flags,cols", [(0, None), (FLAG_NW32, None), (0, "3"), (0, "5")],
+                         ids=["auto", "nw32", "k3", "k5"])
+def test_nw_pairs_match_reference_golden(dev, oracle, flags, cols, monkeypatch):
     """auto: short reads (one strip) take the packed-pair int16 kernel where
-    the launch fits it; nw32: the int32 kernel for everything."""
+    the launch fits it; nw32: the int32 kernel for everything; k3 / k5: the
+    packed kernel's 3- / 5-column latency forms forced (IMSAME_NW_K) where
+    they apply (3 columns: reads <= 150 bases)."""
+    if cols:
+        monkeypatch.setenv("IMSAME_NW_K", cols)
     rows = G.nw_pairs()
     groups = collections.defaultdict(list)
     for r in rows:
@@ -58,11 +63,14 @@ def test_nw_pairs_match_reference_golden(dev, oracle, flags):
     assert checked_text > 250
 
 
-@pytest.mark.parametrize("seed", [0, 1])
-def test_nw_packed_pairs_random_vs_oracle(dev, oracle, seed):
+@pytest.mark.parametrize("seed,cols", [(0, None), (1, None), (2, "3")])
+def test_nw_packed_pairs_random_vs_oracle(dev, oracle, seed, cols, monkeypatch):
     """Packed-pair kernel on mixed shapes: every launch mixes record lengths
     12..3000 and read lengths 12..160 (unequal halves, idle groups at the
-    tail), similarity 0-100 %, gap parameters up to the int16 range limit."""
+    tail), similarity 0-100 %, gap parameters up to the int16 range limit.
+    cols 3: the 3-column latency form forced, reads <= 150 bases."""
+    if cols:
+        monkeypatch.setenv("IMSAME_NW_K", cols)
     rng = np.random.default_rng(100 + seed)
     acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
     # (-5,-3) leaves the int16 range (int32 kernel); mult5: every read length a
@@ -76,6 +84,8 @@ def test_nw_packed_pairs_random_vs_oracle(dev, oracle, seed):
                 yl = int(rng.choice([20, 100, 150, 160, 10 * int(rng.integers(2, 17))]))
             else:
                 yl = int(rng.choice([12, 31, 100, 149, 150, 151, 155, 160, int(rng.integers(12, 161))]))
+            if cols == "3":
+                yl = min(yl, 150)
             x = acgt[rng.integers(0, 4, xl)]
             if rng.random() < 0.7:                      # read drawn from the record, mutated
                 o = int(rng.integers(0, max(1, xl - yl)))
@@ -926,6 +936,7 @@ def test_nw16_launch_forms_equal(dev, oracle, monkeypatch):
     runs = {}
     for name, env in [("k10_persistent", {"IMSAME_NW_K": "10", "IMSAME_NW_PERSIST": "1"}),
                       ("k5_all", {"IMSAME_NW_K": "5"}),
+                      ("k3_all", {"IMSAME_NW_K": "3"}),
                       ("k10_np", {"IMSAME_NW_K": "10"})]:
         for k, v in env.items():
             monkeypatch.setenv(k, v)
@@ -936,6 +947,8 @@ def test_nw16_launch_forms_equal(dev, oracle, monkeypatch):
     assert st.launch_np == 0 and st.launch_k5 == 0
     st = runs["k5_all"][2]
     assert st.launch_k5 == st.launch_pk and st.launch_pk != 0
+    st = runs["k3_all"][2]                        # the 3-column latency form (150-base reads)
+    assert st.launch_k3 == st.launch_pk and st.launch_pk != 0
     for name, (res, pp, st) in runs.items():
         assert not _cmp(res, base), (name, _cmp(res, base))
         if st.launch_np:                          # round 1b ran in both (its speculation sets n_nw)

@@ -137,7 +137,8 @@ def test_emulated_packed_nw_mixed_shapes(emu, oracle, cols, monkeypatch):
                 assert int(res[k][f]) == int(o[f]), (f, k, ig, eg, len(X[k]), len(Y[k]))
 
 
-@pytest.mark.parametrize("band,cols", [("200", "10"), ("40", "10"), ("0", "10"), ("200", "5"), ("0", "5")])
+@pytest.mark.parametrize("band,cols", [("200", "10"), ("40", "10"), ("0", "10"), ("200", "5"), ("0", "5"),
+                                       ("200", "3"), ("40", "3"), ("0", "3")])
 def test_emulated_two_pass_band(emu, oracle, band, cols, monkeypatch):
     """nw16_kernel.hip's two passes (emulated): the score-only sweep with
     checkpoints, then the traceback band restored per half from its own
@@ -149,7 +150,8 @@ def test_emulated_two_pass_band(emu, oracle, band, cols, monkeypatch):
     X, Y = [], []
     for k in range(9):
         xl = int(rng.integers(250, 700))
-        yl = int(rng.choice([150, 149, 60, int(rng.integers(20, 161))]))
+        # (the 3-column form takes reads of <= 150 bases: NW16_K3_YMAX)
+        yl = int(rng.choice([150, 149, 60, int(rng.integers(20, 151 if cols == "3" else 161))]))
         x = acgt[rng.integers(0, 4, xl)]
         if k % 3 != 2:              # true hits at varied depths (best cells spread over the rows)
             o = int(rng.integers(0, xl - yl))
@@ -171,6 +173,10 @@ def test_emulated_two_pass_band(emu, oracle, band, cols, monkeypatch):
     rc, res2, paths2, fl = emu.nw_pairs(X, Y, p2, paths_cap=4096)
     assert rc == 0 and fl == 0
     n_redo = redo()
+    if cols == "3":                 # the 3-column latency form ran (mixed lengths: no LAST)
+        k3 = emu.lib.emu_k3_count
+        k3.restype = C.c_uint32
+        assert k3() > 0
     p1 = oracle.params(want_paths=1, flags=imsame_amd.FLAG_NW16_ONEPASS)
     rc, res1, paths1, fl = emu.nw_pairs(X, Y, p1, paths_cap=4096)
     assert rc == 0 and fl == 0 and redo() == 0
@@ -221,7 +227,11 @@ def test_emulated_k19_form(emu, oracle, band, monkeypatch):
     k19.restype = C.c_uint32
     k19()
     out = {}
-    for form, env in (("k19", None), ("k10", "10")):
+    k3 = emu.lib.emu_k3_count
+    k3.restype = C.c_uint32
+    k3()
+    # (and the 3-column latency form on the same 150-base reads: its LAST form)
+    for form, env in (("k19", None), ("k10", "10"), ("k3", "3")):
         if env:
             monkeypatch.setenv("IMSAME_NW_K", env)
         for one in (False, True):
@@ -230,6 +240,7 @@ def test_emulated_k19_form(emu, oracle, band, monkeypatch):
             assert rc == 0 and fl == 0
             out[form, one] = (res, paths)
         assert (k19() > 0) == (form == "k19")
+        assert (k3() > 0) == (form == "k3")
     for k in range(len(X)):
         o = oracle.nw(X[k], Y[k], text=False)
         for key, (res, paths) in out.items():
