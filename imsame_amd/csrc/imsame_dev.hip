@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <thread>
 #include <mutex>
+#include <condition_variable>
 #include "../../include/imsame_dev.h"
 
 #include "tables.h"
@@ -70,12 +71,14 @@ __device__ __forceinline__ bool acgt_word_bad(const uint8_t *src, int64_t w, int
     }
     return bad;
 }
+// (the check stops at bad_hi: an upload's 64 zero bytes past its last read
+// are packed, not checked)
 __global__ void pack2_kernel(const uint8_t *src, int64_t lo, int64_t hi, uint32_t *dst, uint64_t w0, uint64_t w1,
-                             unsigned long long *bad = nullptr) {
+                             unsigned long long *bad = nullptr, int64_t bad_hi = INT64_MAX) {
     bool b = false;
     GRID_STRIDE(k, w1 - w0) {
         dst[w0 + k] = pk_word(src, (int64_t)(w0 + k), lo, hi);
-        if (bad) b |= acgt_word_bad(src, (int64_t)(w0 + k), lo, hi);
+        if (bad) b |= acgt_word_bad(src, (int64_t)(w0 + k), lo, min(hi, bad_hi));
     }
     if (b) atomicOr(bad, 8ull);
 }
@@ -210,9 +213,13 @@ __device__ __forceinline__ uint32_t row_bucket(int32_t r, uint32_t nb) {
     const int64_t b = (((int64_t)r + 256) >> 3) + 1;
     return (uint32_t)(b < 1 ? 1 : b > (int64_t)nb - 1 ? (int64_t)nb - 1 : b);
 }
+// (grid-stride over few blocks, ROW_BLOCKS: a launch queued while other
+// lanes' NW waves hold the chip waits for a slot per wave it has, as
+// update_kernel)
+#define ROW_BLOCKS 128u
 __global__ void row_hist_kernel(const int32_t *row, uint32_t n, uint32_t nb, uint32_t *hist) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) atomicAdd(&hist[row_bucket(row[i], nb)], 1u);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        atomicAdd(&hist[row_bucket(row[i], nb)], 1u);
 }
 __global__ __launch_bounds__(1024) void row_scan_kernel(const uint32_t *hist, uint32_t nb, uint32_t *cur) {
     __shared__ uint32_t sm[1024];
@@ -231,8 +238,8 @@ __global__ __launch_bounds__(1024) void row_scan_kernel(const uint32_t *hist, ui
     for (uint32_t k = 0; k < per; ++k) if (a + k < nb) { cur[a + k] = run; run += hist[a + k]; }
 }
 __global__ void row_scatter_kernel(const int32_t *row, uint32_t n, uint32_t nb, uint32_t *cur, uint32_t *perm) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) perm[atomicAdd(&cur[row_bucket(row[i], nb)], 1u)] = i;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        perm[atomicAdd(&cur[row_bucket(row[i], nb)], 1u)] = i;
 }
 
 // ---------------------------------------------------------------------------
@@ -334,7 +341,7 @@ struct imsame_ctx {
     bool q_len_mult = false;         // every read length is a multiple of NW16_K
     uint32_t q_len_uni = 0;          // the one read length of the uploaded range (0: lengths differ)
     // per-read state
-    DBuf res, cur_p, cur_h, memo, nmemo, rstat, act0, act1, act2, cbase, ccnt, perr;
+    DBuf res, cur_p, cur_h, memo, nmemo, rstat, act0, act1, act2, act3, cbase, ccnt, perr;
     // candidates
     DBuf cread, csid, cread2, csid2, cout, cout2;
     DBuf crow, cperm, rhist;          // predicted rows of class-0 candidates, their launch order
@@ -379,11 +386,16 @@ struct imsame_ctx {
     std::vector<uint64_t> lane_paths; // path entries of lanes 1, 2, ... after a split call
     // NW launch intervals (ms since the call's origin event) for the busy time
     hipEvent_t origin = nullptr;
+    hipEvent_t ev_w = nullptr;        // align_one: round 1's unpredicted candidates updated (pipelines)
     std::vector<std::pair<float, float>> nw_iv;
     // IMSAME_DEBUG_TIMELINE: (kind 'S' seed / 'N' NW, round, items, start, end)
     struct TlEv { char kind; int round; uint32_t n; float a, b; };
     std::vector<TlEv> tl;
     int cur_round = 0;
+    // the call's two read pipelines (align_one: pipe_rounds) append launch
+    // intervals and timeline events from two host threads; a launch that is
+    // not non-persistent uses this lane's own arena, one at a time
+    std::mutex iv_mu, persist_mu;
     int nlanes = 1;                   // lanes of the running call (the seed scan's group size
                                       // follows the reads scanned across all of them)
     std::vector<uint32_t> part_paths; // host copy of this lane's paths for an imsame_dev_align_parts callback
@@ -663,12 +675,13 @@ extern "C" void imsame_dev_close(imsame_ctx *c) {
                     &c->act1, &c->cread, &c->csid, &c->cread2, &c->csid2, &c->cout, &c->cout2, &c->ctr,
                     &c->minraw, &c->minlen, &c->minident, &c->tb, &c->bnd, &c->paths, &c->ck, &c->rc_in, &c->rc_out,
                     &c->rc_a, &c->rc_b, &c->rc_c, &c->cbase, &c->ccnt, &c->perr, &c->wcap, &c->wout, &c->wstart,
-                    &c->crow, &c->cperm, &c->rhist, &c->act2, &c->slotbits, &c->np_tb, &c->np_ck, &c->dbw, &c->qw,
+                    &c->crow, &c->cperm, &c->rhist, &c->act2, &c->act3, &c->slotbits, &c->np_tb, &c->np_ck, &c->dbw, &c->qw,
                     &c->cperm_b, &c->rhist_b};
     for (DBuf *b : bufs) b->release();
     (void)hipEventDestroy(c->ev0);
     (void)hipEventDestroy(c->ev1);
     if (c->evb0) (void)hipEventDestroy(c->evb0);
+    if (c->ev_w) (void)hipEventDestroy(c->ev_w);
     if (c->evb1) (void)hipEventDestroy(c->evb1);
     for (auto &q : c->evw)
         for (hipEvent_t e : q) if (e) (void)hipEventDestroy(e);
@@ -1100,23 +1113,47 @@ static int nw16_np_part_cu(imsame_ctx *c) {
 // Round 6: the 3-column latency form (NW16_K3) takes a lane's launches of
 // rounds >= 2 below IMSAME_NW_K3_MAX candidates (reads <= NW16_K3_YMAX; the
 // caller checks the range proof for its shape); IMSAME_NW_K=3 forces it.
+// Alone on the chip, 2000 x 150 launches take (K = 3 vs 5 columns) 0.38-0.42
+// vs 0.50-0.56 ms for one pair, 0.54-0.58 vs 0.62-0.65 ms for 1400 pairs,
+// 0.86 vs 0.75 ms for 4096 (profiles/r6a/nwsmall_r6a.json): the default
+// bound sits between the last two.
 static uint32_t nw16_k3_max() {
-    static uint32_t v = [] { const char *e = getenv("IMSAME_NW_K3_MAX"); return e ? (uint32_t)atoi(e) : 3000u; }();
+    static uint32_t v = [] { const char *e = getenv("IMSAME_NW_K3_MAX"); return e ? (uint32_t)atoi(e) : 2048u; }();
     return v;
+}
+// the round of the launch being planned / timed: per host thread (a lane,
+// or one of a lane's two read pipelines)
+static thread_local int t_round = 0;
+// align_one: reads with round-1 candidates and round 1b's reads run their
+// later rounds as independent pipelines (IMSAME_PIPES=0: joined rounds)
+// ... and round 1's launch cut into unpredicted + predicted candidates
+// (IMSAME_CUT_WEAK=0: one launch)
+static bool cut_weak_on() {
+    const char *e = getenv("IMSAME_CUT_WEAK");
+    return !(e && !atoi(e));
+}
+// Measured (profiles/r6e/): C2 (lanes of 333k reads) 100.7-100.8 ms per step
+// against 101.3 joined; the 1/8 and 1/4 shards (lanes of 42k / 83k reads)
+// 16.2 / 29.0 ms against 15.3 / 27.6 -- there the weak launch and round 1b's
+// queue one behind the other on stream_b and B ends last.  So: lanes of >=
+// 200k reads (the budget rule's bound, round_policy.h); IMSAME_PIPES=1 / 0
+// forces it (read per call: tests compare both forms).
+static bool pipes_on(uint64_t n) {
+    const char *e = getenv("IMSAME_PIPES");
+    return e ? atoi(e) != 0 : n >= 200000;
 }
 static int nw16_k(imsame_ctx *c, uint32_t ncand, bool rounds) {
     const char *e = getenv("IMSAME_NW_K"), *fe = getenv("IMSAME_NW_K5_FILL"), *f2 = getenv("IMSAME_NW_K5_FILL2");
     const int force = e ? atoi(e) : 0;
-    if (force == NW16_K3) return NW16_K3;
-    if (rounds && c->cur_round >= 2 && ncand <= nw16_k3_max()) return NW16_K3;
+    if (force == NW16_K3 || force == NW16_K5 || force == NW16_K) return force;
+    if (rounds && t_round >= 2 && ncand <= nw16_k3_max()) return NW16_K3;
     // a lane's launches of rounds >= 2 (IMSAME_NW_K5_FILL2, 1.5: below ~16k
     // candidates with 3 lanes): C2's round-2 launches of ~15.5k candidates
     // run one or two 19-column waves per SIMD, latency-bound; the 5-column
     // form took C2 from 105.8-105.9 to 105.2-105.3 ms per step, the 1/8 shard
     // and C3 unchanged (profiles/r5zt/; 1.5 for every launch, round 1b's
     // included, slowed the 1/8 shard and C3: r5zs/)
-    const double fill = c->cur_round >= 2 ? (f2 ? atof(f2) : 1.5) : fe ? atof(fe) : 0.3;
-    if (force == NW16_K5 || force == NW16_K) return force;
+    const double fill = t_round >= 2 ? (f2 ? atof(f2) : 1.5) : fe ? atof(fe) : 0.3;
     if (!rounds) return NW16_K;
     const double slots = (double)c->ncu * 4.0 * 4.0 / std::max(1, c->nlanes);
     return (double)ncand / 8.0 < fill * slots ? NW16_K5 : NW16_K;
@@ -1268,8 +1305,9 @@ static int nw_launch_done(imsame_ctx *c, int qi, uint32_t n, double *ms) {
     if (c->origin) {
         float a = 0, b = 0;
         if (hipEventElapsedTime(&a, c->origin, e0) == hipSuccess && hipEventElapsedTime(&b, c->origin, e1) == hipSuccess) {
+            std::lock_guard<std::mutex> g(c->iv_mu);
             c->nw_iv.push_back({a, b});
-            if (timeline_on()) c->tl.push_back({'N', c->cur_round, n, a, b});
+            if (timeline_on()) c->tl.push_back({'N', t_round, n, a, b});
         }
     }
     return 0;
@@ -1309,11 +1347,33 @@ static int np_prepare(imsame_ctx *o, uint32_t xcap) {
     return 0;
 }
 
+// Queue order of a launch's candidates by predicted first row (8-row
+// buckets, unpredicted first: launch_nw's own ordering, done ahead of it) into
+// the cperm buffer of queue qi, and the number of unpredicted candidates --
+// the first *nweak entries -- read back (the stream is synchronized).
+static int row_perm(imsame_ctx *c, const int32_t *crow, uint32_t n, uint32_t xcap_pl, int qi, uint32_t *nweak) {
+    hipStream_t s = qi ? c->stream_b : c->stream;
+    const uint32_t nb = xcap_pl / 8 + 512 / 8 + 2;
+    DBuf &cperm = qi ? c->cperm_b : c->cperm, &rhist = qi ? c->rhist_b : c->rhist;
+    if (cperm.ensure((uint64_t)n * 4) || rhist.ensure((uint64_t)nb * 8)) return IMSAME_E_OOM;
+    uint32_t *hist = rhist.as<uint32_t>(), *cur = hist + nb;
+    HIPCHK(hipMemsetAsync(hist, 0, (size_t)nb * 4, s));
+    row_hist_kernel<<<std::min(nblk(n, 256), ROW_BLOCKS), 256, 0, s>>>(crow, n, nb, hist);
+    row_scan_kernel<<<1, 1024, 0, s>>>(hist, nb, cur);
+    row_scatter_kernel<<<std::min(nblk(n, 256), ROW_BLOCKS), 256, 0, s>>>(crow, n, nb, cur, cperm.as<uint32_t>());
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(nweak, hist, 4, hipMemcpyDeviceToHost, s));
+    LANE_SYNC(c, s);
+    return 0;
+}
+
 static int launch_nw(imsame_ctx *c, NwPlan &pl, const uint32_t *cread, const uint32_t *csid, uint32_t n,
                      imsame_read_result *outp, int64_t ig, int64_t eg, const imsame_params *p, uint32_t ymax,
                      uint32_t xmax, uint32_t *work, const uint8_t *dbp, const uint64_t *dbs, const uint8_t *qp,
                      const uint64_t *qs, uint32_t paths_cap, double *ms, const int32_t *crow = nullptr, int qi = 0,
-                     bool wait = true) {
+                     bool wait = true, const uint32_t *perm_in = nullptr) {
+    // perm_in: the queue order is given (row_perm; the candidates are
+    // perm_in[0 .. n)), crow their predicted rows
     // qi 1: round 1b's stream; wait false: enqueue only (nw_launch_done)
     hipStream_t s = qi ? c->stream_b : c->stream;
     hipEvent_t e0 = qi ? c->evb0 : c->ev0, e1 = qi ? c->evb1 : c->ev1;
@@ -1367,16 +1427,25 @@ static int launch_nw(imsame_ctx *c, NwPlan &pl, const uint32_t *cread, const uin
     P.slot_bits = pl.np ? ao->slotbits.as<uint32_t>() : nullptr; P.slot_words = pl.slot_words;
     HIPCHK(hipMemsetAsync(work, 0, 4, s));
     HIPCHK(hipEventRecord(e0, s));               // the launch's time includes its ordering
-    if (crow && pl.two && n >= 64) {
+    auto win_params = [&] {
+        const char *wu = getenv("IMSAME_NW_WIN_UP"), *wd = getenv("IMSAME_NW_WIN_DOWN");
+        P.win_up = wu ? atoi(wu) : NW16_WIN_UP; P.win_down = wd ? atoi(wd) : NW16_WIN_DOWN;
+        const char *wb = getenv("IMSAME_NW_WIN_BOTTOM");
+        P.win_bottom = wb ? atoi(wb) : NW16_WIN_BOTTOM;
+    };
+    if (perm_in) {
+        P.perm = perm_in;
+        if (crow && pl.two) { P.cand_row = crow; win_params(); }
+    } else if (crow && pl.two && n >= 64) {
         // queue order by predicted row (first-sweep traceback windows)
         const uint32_t nb = ((uint32_t)pl.xcap + 512) / 8 + 2;
         DBuf &cperm = qi ? c->cperm_b : c->cperm, &rhist = qi ? c->rhist_b : c->rhist;
         if (cperm.ensure((uint64_t)n * 4) || rhist.ensure((uint64_t)nb * 8)) return IMSAME_E_OOM;
         uint32_t *hist = rhist.as<uint32_t>(), *cur = hist + nb;
         HIPCHK(hipMemsetAsync(hist, 0, (size_t)nb * 4, s));
-        row_hist_kernel<<<nblk(n, 256), 256, 0, s>>>(crow, n, nb, hist);
+        row_hist_kernel<<<std::min(nblk(n, 256), ROW_BLOCKS), 256, 0, s>>>(crow, n, nb, hist);
         row_scan_kernel<<<1, 1024, 0, s>>>(hist, nb, cur);
-        row_scatter_kernel<<<nblk(n, 256), 256, 0, s>>>(crow, n, nb, cur, cperm.as<uint32_t>());
+        row_scatter_kernel<<<std::min(nblk(n, 256), ROW_BLOCKS), 256, 0, s>>>(crow, n, nb, cur, cperm.as<uint32_t>());
         HIPCHK(hipGetLastError());
         P.perm = cperm.as<uint32_t>(); P.cand_row = crow;
         const char *wu = getenv("IMSAME_NW_WIN_UP"), *wd = getenv("IMSAME_NW_WIN_DOWN");
@@ -1553,6 +1622,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     if (c->res.ensure((uint64_t)n * 64) || c->cur_p.ensure((uint64_t)n * 8) || c->cur_h.ensure((uint64_t)n * 4) ||
         c->memo.ensure((uint64_t)n * 4 * MEMO) || c->nmemo.ensure(n) || c->rstat.ensure(n) ||
         c->act0.ensure((uint64_t)n * 4) || c->act1.ensure((uint64_t)n * 4) || c->act2.ensure((uint64_t)n * 4) ||
+        c->act3.ensure((uint64_t)n * 4) ||
         c->cread.ensure(ccap * 4) || c->csid.ensure(ccap * 4) ||
         c->cout.ensure(ccap * 64) || c->cbase.ensure((uint64_t)n * 4) ||
         c->ccnt.ensure((uint64_t)n * 4) || c->perr.ensure((uint64_t)n * 4) || c->crow.ensure(ccap * 4))
@@ -1563,6 +1633,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         return IMSAME_E_OOM;
     if (poison_on()) {                        // this call's scratch holds nothing it may read
         const DBuf *scr[] = {&c->res, &c->cur_p, &c->cur_h, &c->memo, &c->nmemo, &c->rstat, &c->act0, &c->act1, &c->act2,
+                             &c->act3,
                              &c->cread, &c->csid, &c->cread2, &c->csid2, &c->cout, &c->cout2, &c->cbase, &c->ccnt,
                              &c->perr, &c->crow, &c->cperm, &c->rhist, &c->cperm_b, &c->rhist_b, &c->paths, &c->tb,
                              &c->ck, &c->bnd};
@@ -1598,7 +1669,9 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         if (w1 > w0)
             pack2_kernel<<<gsblk(w1 - w0, 256), 256, 0, s>>>(dev_q(c), (int64_t)c->q_base, (int64_t)c->qb_end,
                                                              (uint32_t *)dev_qw(c), w0, w1,
-                                                             (unsigned long long *)(ctr + C_FLAGS));
+                                                             (unsigned long long *)(ctr + C_FLAGS),
+                                                             (int64_t)c->qb_end - 64);      // the zero padding
+                                                                                            // (set_query_range_async)
         HIPCHK(hipGetLastError());
     }
     InitLaunch I = {qsd, read_from, n, c->res.as<imsame_read_result>(), c->cur_p.as<uint64_t>(),
@@ -1617,7 +1690,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     uint32_t *act = c->act0.as<uint32_t>(), *nxt = c->act1.as<uint32_t>();
     while (nact) {
         st.rounds++;
-        c->cur_round = (int)st.rounds;
+        c->cur_round = t_round = (int)st.rounds;
         HIPCHK(hipMemsetAsync(ctr + C_NCAND, 0, 7 * 8, s));     // NCAND, NCAND2, NNEXT, (1b) NCANDB, NCAND2B, NNEXT2, WORKB
         SeedLaunch S;
         S.db = c->db.as<uint8_t>(); S.db_start = c->db_start.as<uint64_t>(); S.n_db = c->n_db; S.db_len = c->db_len;
@@ -1650,8 +1723,9 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         S.wstart = c->use_wstart ? c->wstart.as<uint64_t>() : nullptr;
         S.minlen = c->minlen.as<uint32_t>(); S.n_minlen = ymax + 1;
         S.minident = c->minident.as<uint32_t>(); S.n_minident = xcap + ymax + 2;
-        auto seed_launch = [&](const SeedLaunch &SL, uint32_t na, hipStream_t ss, hipEvent_t e0, hipEvent_t e1) -> int {
-            const int L = RP.pick_L(rnd, na);
+        auto seed_launch = [&](const SeedLaunch &SL, uint32_t na, hipStream_t ss, hipEvent_t e0, hipEvent_t e1,
+                               uint32_t rr = 0) -> int {
+            const int L = RP.pick_L(rr ? rr : rnd, na);
             const size_t slds = 256 * SEED_LDS_PER_LANE;
             // (IMSAME_SEED_BLOCKS: at most this many blocks, the kernels stride)
             auto sb = [&](uint64_t lanes) { return std::min<unsigned>(nblk(lanes, 256), seed_blocks()); };
@@ -1666,39 +1740,41 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
             HIPCHK(hipGetLastError());
             return 0;
         };
-        auto seed_time = [&](hipEvent_t e0, hipEvent_t e1, uint32_t na) -> int {
+        auto seed_time = [&](imsame_stats &sx, hipEvent_t e0, hipEvent_t e1, uint32_t na) -> int {
             float fs = 0;
             HIPCHK(hipEventElapsedTime(&fs, e0, e1));
-            st.ms_seed += fs;
+            sx.ms_seed += fs;
             if (c->origin && timeline_on()) {
                 float a = 0;
-                if (hipEventElapsedTime(&a, c->origin, e0) == hipSuccess)
-                    c->tl.push_back({'S', (int)st.rounds, na, a, a + fs});
+                if (hipEventElapsedTime(&a, c->origin, e0) == hipSuccess) {
+                    std::lock_guard<std::mutex> g(c->iv_mu);
+                    c->tl.push_back({'S', t_round, na, a, a + fs});
+                }
             }
             return 0;
         };
-        auto rec_launch = [&](const NwPlan &pl, uint32_t nc, double ms) {
-            if (st.nw_launches < IMSAME_LAUNCH_STATS) {
-                st.launch_cand[st.nw_launches] = nc;
-                st.launch_ms[st.nw_launches] = ms;
-                if (pl.pk) st.launch_pk |= 1ull << st.nw_launches;
-                if (pl.pk && pl.k == NW16_K5) st.launch_k5 |= 1ull << st.nw_launches;
-                if (pl.pk && pl.k == NW16_K3) st.launch_k3 |= 1ull << st.nw_launches;
-                if (pl.np) st.launch_np |= 1ull << st.nw_launches;
-                if (pl.pk && pl.k == NW16_K19) st.launch_k19 |= 1ull << st.nw_launches;
-                if (pl.lp) st.launch_nwp |= 1ull << st.nw_launches;
+        auto rec_launch = [&](imsame_stats &sx, const NwPlan &pl, uint32_t nc, double ms) {
+            if (sx.nw_launches < IMSAME_LAUNCH_STATS) {
+                sx.launch_cand[sx.nw_launches] = nc;
+                sx.launch_ms[sx.nw_launches] = ms;
+                if (pl.pk) sx.launch_pk |= 1ull << sx.nw_launches;
+                if (pl.pk && pl.k == NW16_K5) sx.launch_k5 |= 1ull << sx.nw_launches;
+                if (pl.pk && pl.k == NW16_K3) sx.launch_k3 |= 1ull << sx.nw_launches;
+                if (pl.np) sx.launch_np |= 1ull << sx.nw_launches;
+                if (pl.pk && pl.k == NW16_K19) sx.launch_k19 |= 1ull << sx.nw_launches;
+                if (pl.lp) sx.launch_nwp |= 1ull << sx.nw_launches;
             }
-            st.ms_nw += ms; st.nw_launches++; st.n_nw += nc;
+            sx.ms_nw += ms; sx.nw_launches++; sx.n_nw += nc;
         };
         auto upd_launch = [&](const uint32_t *cr, const uint32_t *cs, uint32_t nc, const imsame_read_result *o,
-                              uint32_t *next, int nnext_slot, hipStream_t ss) -> int {
+                              uint32_t *next, int nnext_slot, hipStream_t ss, const uint32_t *uperm = nullptr) -> int {
             UpdLaunch U = {cr, cs, nc, o, read_from, c->res.as<imsame_read_result>(),
                            c->rstat.as<uint8_t>(), c->memo.as<uint32_t>(), c->nmemo.as<uint8_t>(),
                            c->cbase.as<uint32_t>(), c->ccnt.as<uint32_t>(), c->perr.as<uint32_t>(),
                            c->cur_p.as<uint64_t>(), next,
                            (uint32_t *)(ctr + nnext_slot), (unsigned long long *)(ctr + C_CELLS),
                            (unsigned long long *)(ctr + C_NACC), (unsigned long long *)(ctr + C_ERR),
-                           c->db_start.as<uint64_t>(), ctr + C_FLAGS, (unsigned long long *)(ctr + C_WASTE)};
+                           c->db_start.as<uint64_t>(), ctr + C_FLAGS, (unsigned long long *)(ctr + C_WASTE), uperm};
             update_kernel<<<std::min<unsigned>(nblk(nc, 256), upd_blocks()), 256, 0, ss>>>(U);
             POISON_SYNC(ss, "update_kernel", c);
             HIPCHK(hipGetLastError());
@@ -1750,7 +1826,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
             uint64_t ha[2], hb[2];
             HIPCHK(hipMemcpyAsync(ha, ctr + C_NCAND, 16, hipMemcpyDeviceToHost, s));
             LANE_SYNC(c, s);
-            if ((rc = seed_time(c->ev0, c->ev1, nA))) return rc;
+            if ((rc = seed_time(st, c->ev0, c->ev1, nA))) return rc;
             if (ha[1]) return IMSAME_E_STATE;                         // short reads only: cannot happen
             const uint32_t na1 = (uint32_t)ha[0];
             NwPlan pla = {}, plb = {};
@@ -1766,7 +1842,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
             }
             HIPCHK(hipMemcpyAsync(hb, ctr + C_NCANDB, 16, hipMemcpyDeviceToHost, sb));
             LANE_SYNC(c, sb);
-            if ((rc = seed_time(c->evb0, c->evb1, nB))) return rc;
+            if ((rc = seed_time(st, c->evb0, c->evb1, nB))) return rc;
             if (hb[1]) return IMSAME_E_STATE;
             const uint32_t nb1 = (uint32_t)hb[0];
             bool a_done = na1 == 0;
@@ -1778,7 +1854,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
                                   plb.ck_dw == pla.ck_dw && plb.bnd_dw == pla.bnd_dw && plb.max_blocks == pla.max_blocks;
                 if (!same && !a_done) {
                     if ((rc = nw_launch_done(c, 0, na1, &msa))) return rc;
-                    rec_launch(pla, na1, msa);
+                    rec_launch(st, pla, na1, msa);
                     a_done = true;
                 }
                 rc = launch_nw(c, plb, Sb.cread, Sb.csid, nb1, c->cout.as<imsame_read_result>() + offB, p->igap, p->egap,
@@ -1790,11 +1866,11 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
             }
             if (!a_done) {
                 if ((rc = nw_launch_done(c, 0, na1, &msa))) return rc;
-                rec_launch(pla, na1, msa);
+                rec_launch(st, pla, na1, msa);
             }
             if (nb1) {
                 if ((rc = nw_launch_done(c, 1, nb1, &msb))) return rc;
-                rec_launch(plb, nb1, msb);
+                rec_launch(st, plb, nb1, msb);
             }
             LANE_SYNC(c, sb);
             uint64_t nn = 0;
@@ -1812,7 +1888,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         uint64_t hc[3];
         HIPCHK(hipMemcpyAsync(hc, ctr + C_NCAND, 24, hipMemcpyDeviceToHost, s));
         LANE_SYNC(c, s);
-        if ((rc = seed_time(c->ev0, c->ev1, nact))) return rc;
+        if ((rc = seed_time(st, c->ev0, c->ev1, nact))) return rc;
         const uint32_t n1 = (uint32_t)hc[0], n2 = (uint32_t)hc[1];
         if (n1 + n2 + hc[2] == 0) break;                          // no candidates, nobody paused
         // Round 1b.  Reads that paused in round 1 without a candidate (budget
@@ -1830,6 +1906,225 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         bool r1b = RP.r1b(rnd, n1, n2, hc[2]);
         if (r1b && n1 && (rc = plan_nw(c, short_y, xcap, n1, p, c->q_len_mult, &pla, true, c->q_len_uni))) return rc;
         if (r1b && n1 && !pla.np) r1b = false;
+        // Independent pipelines (round 6).  The reads with round-1 candidates
+        // (A) and the reads round 1 paused without one (B, round 1b's scan) are
+        // disjoint and never need each other's NW results, so from round 1 on
+        // each runs its own rounds to the end on its own stream -- A on the
+        // lane's stream, B on stream_b from a host thread of its own -- with its
+        // own active lists (A: act0 / act3, B: act1 / act2), counters (C_NCAND..
+        // / C_NCANDB..) and part of the candidate lists (A: [0, n1), B: [n1,
+        // ccap)).  Joined, both waited for the LATER of the two round-1 launches
+        // before round 2: at C2 B's launch ends 20-30 ms before A's, and its
+        // round-2 reads (most of round 2: random reads whose weak candidates
+        // were rejected) sat behind A's (profiles/r6b/ timeline).  Same scans,
+        // budgets and visiting order per read, so the same results (tests).
+        // IMSAME_PIPES=0: the joined rounds below.
+        if (r1b && pipes_on(n)) {
+            if (!c->stream_b) {
+                HIPCHK(hipStreamCreateWithFlags(&c->stream_b, hipStreamNonBlocking));
+                HIPCHK(hipEventCreate(&c->evb0));
+                HIPCHK(hipEventCreate(&c->evb1));
+                for (int k = 0; k < 2; ++k)
+                    HIPCHK(hipEventCreateWithFlags(&c->evw[1][k], hipEventBlockingSync | hipEventDisableTiming));
+            }
+            hipStream_t sb = c->stream_b;
+            const uint32_t npz = (uint32_t)hc[2];
+            uint32_t *cr0 = c->cread.as<uint32_t>(), *cs0 = c->csid.as<uint32_t>();
+            imsame_read_result *co0 = c->cout.as<imsame_read_result>();
+            // B's round 1b scan, as the joined form's
+            SeedLaunch Sb = S;
+            Sb.active = nxt; Sb.n_active = npz;
+            Sb.spec = 1;
+            Sb.spec_weak = RP.r1b_spec_weak(n1, npz);
+            Sb.budget = RP.r1b_budget();
+            Sb.next = c->act2.as<uint32_t>(); Sb.nnext = (uint32_t *)(ctr + C_NNEXT2);
+            Sb.cread = cr0 + n1; Sb.csid = cs0 + n1;
+            Sb.ncand = (uint32_t *)(ctr + C_NCANDB); Sb.crow = crow && RP.r1b_rows ? crow + n1 : nullptr;
+            Sb.ncand2 = (uint32_t *)(ctr + C_NCAND2B);
+            Sb.dbg = nullptr;
+            if ((rc = seed_launch(Sb, npz, sb, c->evb0, c->evb1))) return rc;
+            // a pipeline's state: stream (qi 0 / 1) and its events, lists,
+            // candidate region [off, off + room), counter slots (cn: ncand,
+            // ncand2, nnext; cw: its NW launch's work counter), round
+            struct Pipe { hipStream_t s; int qi; hipEvent_t e0, e1; uint32_t *act, *nxt; uint32_t nact;
+                          uint64_t off, room; int cn, cw; uint32_t rnd; };
+            // one NW launch of a pipeline's candidates + its update (next list:
+            // P.nxt, or `next` / counter slot `nslot`; perm: the candidates are
+            // perm[0 .. nc) of the pipeline's part, whole reads' sets)
+            auto pipe_nw = [&](Pipe &P, imsame_stats &sx, NwPlan &pl, uint32_t nc, const int32_t *cw_row,
+                               const uint32_t *perm = nullptr, uint32_t *next = nullptr, int nslot = -1) -> int {
+                // a launch that is not non-persistent uses this lane's own arena:
+                // one at a time (launch_nw waits for it: wait = true)
+                std::unique_lock<std::mutex> lk(c->persist_mu, std::defer_lock);
+                if (!pl.np) lk.lock();
+                double ms = 0;
+                int r = launch_nw(c, pl, cr0 + P.off, cs0 + P.off, nc, co0 + P.off, p->igap, p->egap, p, ymax, xcap,
+                                  (uint32_t *)(ctr + P.cw), c->db.as<uint8_t>(), c->db_start.as<uint64_t>(), qd, qsd,
+                                  pcap, &ms, cw_row, P.qi, true, perm);
+                if (r) return r;
+                if (lk.owns_lock()) lk.unlock();
+                rec_launch(sx, pl, nc, ms);
+                return upd_launch(cr0 + P.off, cs0 + P.off, nc, co0 + P.off, next ? next : P.nxt,
+                                  nslot >= 0 ? nslot : P.cn + 2, P.s, perm);
+            };
+            // rounds >= 2 of a pipeline, to its end
+            auto pipe_rounds = [&](Pipe &P, imsame_stats &sx) -> int {
+                while (P.nact) {
+                    ++P.rnd;
+                    t_round = (int)P.rnd;
+                    HIPCHK(hipMemsetAsync(ctr + P.cn, 0, 3 * 8, P.s));       // ncand, ncand2, nnext
+                    SeedLaunch Sp = S;
+                    Sp.active = P.act; Sp.n_active = P.nact;
+                    // speculation within this pipeline's part of the lists
+                    const uint64_t room = std::max<uint64_t>(1, P.room / P.nact);
+                    const uint64_t w = (!RP.spec_set && RP.pick_L(P.rnd, P.nact) >= 64) ? SPEC_BIG : RP.spec_later;
+                    Sp.spec = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(w, room));
+                    Sp.spec_weak = (uint32_t)std::min<uint64_t>(RP.spec_weak, room);
+                    Sp.budget = RP.budget(P.rnd);
+                    Sp.next = P.nxt; Sp.nnext = (uint32_t *)(ctr + P.cn + 2);
+                    Sp.cread = cr0 + P.off; Sp.csid = cs0 + P.off;
+                    Sp.ncand = (uint32_t *)(ctr + P.cn); Sp.ncand2 = (uint32_t *)(ctr + P.cn + 1);
+                    Sp.crow = crow ? crow + P.off : nullptr;
+                    Sp.dbg = nullptr;
+                    if (int r = seed_launch(Sp, P.nact, P.s, P.e0, P.e1, P.rnd)) return r;
+                    uint64_t hp[3];
+                    HIPCHK(hipMemcpyAsync(hp, ctr + P.cn, 24, hipMemcpyDeviceToHost, P.s));
+                    LANE_SYNC(c, P.s);
+                    if (int r = seed_time(sx, P.e0, P.e1, P.nact)) return r;
+                    if (hp[1]) return IMSAME_E_STATE;                   // short reads only: cannot happen
+                    const uint32_t nc = (uint32_t)hp[0];
+                    if (nc + hp[2] == 0) break;
+                    if (nc) {
+                        NwPlan pl;
+                        if (int r = plan_nw(c, short_y, xcap, nc, p, c->q_len_mult, &pl, true, c->q_len_uni)) return r;
+                        if (int r = pipe_nw(P, sx, pl, nc, crow ? crow + P.off : nullptr)) return r;
+                    }
+                    uint64_t nn = 0;
+                    HIPCHK(hipMemcpyAsync(&nn, ctr + P.cn + 2, 8, hipMemcpyDeviceToHost, P.s));
+                    LANE_SYNC(c, P.s);
+                    if (getenv("IMSAME_DEBUG_ROUNDS"))
+                        fprintf(stderr, "[round %u pipe %c] active=%u spec=%u budget=%u cand=%u next=%llu\n", P.rnd,
+                                P.qi ? 'B' : 'A', P.nact, Sp.spec, Sp.budget, nc, (unsigned long long)nn);
+                    P.nact = (uint32_t)nn;
+                    std::swap(P.act, P.nxt);
+                }
+                return 0;
+            };
+            // B, on its own host thread: round 1's unpredicted candidates' and
+            // round 1b's NW launches + updates, then its rounds
+            imsame_stats stB;
+            memset(&stB, 0, sizeof stB);
+            // Round 1's launch is cut in two by the row order (row_perm): the
+            // UNPREDICTED candidates (weak first hits: random reads, whose
+            // candidates are all unpredicted; the front of the order) run on
+            // B's stream after the 1b scan and their update appends the rejected
+            // reads to B's list; the PREDICTED ones (true reads, one candidate
+            // each) run on A's stream at once, A's list.  Most later-round reads
+            // are the weak ones (C2: ~6.4k of a lane's ~6.5k round-2 reads,
+            // profiles/r6c/), so round 2 now scans on beside the true reads'
+            // launch instead of after it.  (Run first on A's stream, the weak
+            // launch and its update delayed the true reads' launch by 5-17 ms
+            // at C2: profiles/r6d/.)  A hands B the cut through wstate: 1 with
+            // nw / pm set (ev_w after the perm on A's stream), -1 if A failed.
+            std::mutex wmu;
+            std::condition_variable wcv;
+            int wstate = 0;
+            uint32_t nw = 0;
+            const uint32_t *pm = nullptr;
+            auto w_done = [&](int v) { { std::lock_guard<std::mutex> g(wmu); wstate = v; } wcv.notify_all(); };
+            if (!c->ev_w) HIPCHK(hipEventCreateWithFlags(&c->ev_w, hipEventDisableTiming));
+            // (B.act: round 1b's active list, act1; its update appends to B.nxt,
+            // act2, where the 1b scan put the reads it paused -- round 2's list)
+            Pipe B = {sb, 1, c->evb0, c->evb1, nxt, c->act2.as<uint32_t>(), 0, n1, ccap - n1, C_NCANDB, C_WORKB, 1};
+            int rcB = 0;
+            std::thread thB([&] {
+                rcB = [&]() -> int {
+                    HIPCHK(hipSetDevice(c->device));
+                    t_round = 1;
+                    uint64_t hb[2];
+                    HIPCHK(hipMemcpyAsync(hb, ctr + C_NCANDB, 16, hipMemcpyDeviceToHost, sb));
+                    LANE_SYNC(c, sb);                    // the 1b scan (its events: before a launch reuses them)
+                    if (int r = seed_time(stB, c->evb0, c->evb1, npz)) return r;
+                    {
+                        std::unique_lock<std::mutex> g(wmu);
+                        wcv.wait(g, [&] { return wstate != 0; });
+                        if (wstate < 0) return IMSAME_E_STATE;   // A failed before it: A reports it
+                    }
+                    if (nw) {                            // the unpredicted candidates (A's part of the lists)
+                        HIPCHK(hipStreamWaitEvent(sb, c->ev_w, 0));
+                        Pipe W = B;
+                        W.off = 0; W.room = n1;
+                        NwPlan plw;
+                        if (int r = plan_nw(c, short_y, xcap, nw, p, c->q_len_mult, &plw, true, c->q_len_uni)) return r;
+                        if (int r = pipe_nw(W, stB, plw, nw, crow, pm, c->act2.as<uint32_t>(), C_NNEXT2)) return r;
+                    }
+                    if (hb[1]) return IMSAME_E_STATE;
+                    const uint32_t nb = (uint32_t)hb[0];
+                    if (nb) {
+                        NwPlan plb;
+                        if (int r = plan_nw(c, short_y, xcap, nb, p, c->q_len_mult, &plb, true, c->q_len_uni)) return r;
+                        if (int r = pipe_nw(B, stB, plb, nb, Sb.crow)) return r;
+                    }
+                    uint64_t nn = 0;
+                    HIPCHK(hipMemcpyAsync(&nn, ctr + C_NNEXT2, 8, hipMemcpyDeviceToHost, sb));
+                    LANE_SYNC(c, sb);
+                    B.nact = (uint32_t)nn;
+                    std::swap(B.act, B.nxt);             // round 2 scans act2; act1 is free
+                    return pipe_rounds(B, stB);
+                }();
+            });
+            // A, on this thread: the cut, round 1's predicted candidates' launch
+            // + update (its next list: act3; C_NNEXT held round 1's paused
+            // count), then its rounds
+            Pipe A = {s, 0, c->ev0, c->ev1, c->act3.as<uint32_t>(), act, 0, 0, n1, C_NCAND, C_WORK, 1};
+            const int rcA = [&]() -> int {
+                HIPCHK(hipMemsetAsync(ctr + C_NNEXT, 0, 8, s));
+                if (n1 && crow && pla.two && cut_weak_on()) {
+                    uint32_t k = 0;
+                    if (int r = row_perm(c, crow, n1, (uint32_t)pla.xcap, 0, &k)) return r;
+                    nw = k; pm = c->cperm.as<uint32_t>();
+                    HIPCHK(hipEventRecord(c->ev_w, s));
+                }
+                w_done(1);
+                if (getenv("IMSAME_DEBUG_ROUNDS"))
+                    fprintf(stderr, "[round 1 pipes] cand=%u unpredicted=%u paused=%u\n", n1, nw, npz);
+                if (n1 > nw) {                           // the predicted ones
+                    NwPlan pls = pla;
+                    if (nw && (rc = plan_nw(c, short_y, xcap, n1 - nw, p, c->q_len_mult, &pls, true, c->q_len_uni)))
+                        return rc;
+                    std::swap(A.act, A.nxt);             // the update writes A.nxt = act3
+                    const int r = pipe_nw(A, st, pls, n1 - nw, crow, pm ? pm + nw : nullptr);
+                    std::swap(A.act, A.nxt);
+                    if (r) return r;
+                }
+                uint64_t nn = 0;
+                HIPCHK(hipMemcpyAsync(&nn, ctr + C_NNEXT, 8, hipMemcpyDeviceToHost, s));
+                LANE_SYNC(c, s);
+                A.nact = (uint32_t)nn;
+                return pipe_rounds(A, st);
+            }();
+            if (!wstate) w_done(-1);                     // (A failed before its first launch)
+            thB.join();
+            if (rcA) return rcA;
+            if (rcB) return rcB;
+            // one stats record: B's launches after A's
+            st.rounds = std::max(A.rnd, B.rnd);
+            st.ms_seed += stB.ms_seed;
+            for (uint64_t j = 0; j < std::min<uint64_t>(stB.nw_launches, IMSAME_LAUNCH_STATS); ++j) {
+                const uint64_t d = st.nw_launches + j;
+                if (d >= IMSAME_LAUNCH_STATS) break;
+                st.launch_cand[d] = stB.launch_cand[j]; st.launch_ms[d] = stB.launch_ms[j];
+                const uint64_t bit = 1ull << j, to = 1ull << d;
+                if (stB.launch_pk & bit) st.launch_pk |= to;
+                if (stB.launch_k5 & bit) st.launch_k5 |= to;
+                if (stB.launch_k3 & bit) st.launch_k3 |= to;
+                if (stB.launch_np & bit) st.launch_np |= to;
+                if (stB.launch_k19 & bit) st.launch_k19 |= to;
+                if (stB.launch_nwp & bit) st.launch_nwp |= to;
+            }
+            st.ms_nw += stB.ms_nw; st.nw_launches += stB.nw_launches; st.n_nw += stB.n_nw;
+            break;
+        }
         if (r1b) {
             if (!c->stream_b) {
                 HIPCHK(hipStreamCreateWithFlags(&c->stream_b, hipStreamNonBlocking));
@@ -1864,7 +2159,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
             uint64_t hb[2];
             HIPCHK(hipMemcpyAsync(hb, ctr + C_NCANDB, 16, hipMemcpyDeviceToHost, sb));
             LANE_SYNC(c, sb);                         // the 1b scan only: N1a runs on
-            if ((rc = seed_time(c->evb0, c->evb1, npz))) return rc;
+            if ((rc = seed_time(st, c->evb0, c->evb1, npz))) return rc;
             const uint32_t nb = (uint32_t)hb[0];
             if (hb[1]) return IMSAME_E_STATE;                         // short reads only: cannot happen
             NwPlan plb = {};
@@ -1878,7 +2173,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
                                   plb.ck_dw == pla.ck_dw && plb.bnd_dw == pla.bnd_dw && plb.max_blocks == pla.max_blocks;
                 if (!same && !a_done) {                               // not N1a's arena layout: after it
                     if ((rc = nw_launch_done(c, 0, n1, &msa))) return rc;
-                    rec_launch(pla, n1, msa);
+                    rec_launch(st, pla, n1, msa);
                     a_done = true;
                 }
                 rc = launch_nw(c, plb, c->cread.as<uint32_t>() + n1, c->csid.as<uint32_t>() + n1, nb,
@@ -1891,11 +2186,11 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
             }
             if (!a_done) {
                 if ((rc = nw_launch_done(c, 0, n1, &msa))) return rc;
-                rec_launch(pla, n1, msa);
+                rec_launch(st, pla, n1, msa);
             }
             if (nb) {
                 if ((rc = nw_launch_done(c, 1, nb, &msb))) return rc;
-                rec_launch(plb, nb, msb);
+                rec_launch(st, plb, nb, msb);
             }
             LANE_SYNC(c, sb);
             uint64_t nn = 0;
@@ -1924,7 +2219,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
                            (uint32_t *)(ctr + cls[k].work), c->db.as<uint8_t>(), c->db_start.as<uint64_t>(), qd, qsd,
                            pcap, &ms, k == 0 ? crow : nullptr);
             if (rc) return rc;
-            rec_launch(pl, cls[k].n, ms);
+            rec_launch(st, pl, cls[k].n, ms);
             if ((rc = upd_launch(cls[k].cr, cls[k].cs, cls[k].n, cls[k].o, nxt, C_NNEXT, s))) return rc;
         }
         uint64_t nn = 0;
@@ -2209,6 +2504,7 @@ static int align_impl(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint6
     std::vector<std::pair<float, float>> iv = c->nw_iv;
     for (int k = 1; k < nl; ++k) iv.insert(iv.end(), L[k]->nw_iv.begin(), L[k]->nw_iv.end());
     st.nw_launches = 0; st.launch_pk = 0; st.launch_k5 = 0; st.launch_np = 0; st.launch_k19 = 0; st.launch_nwp = 0;
+    st.launch_k3 = 0;
     for (int k = 0; k < np; ++k) {
         const imsame_stats &x = S[k];
         if (k) {
@@ -2229,6 +2525,7 @@ static int align_impl(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint6
             if ((x.launch_np >> j) & 1) st.launch_np |= 1ull << (st.nw_launches + j);
             if ((x.launch_k19 >> j) & 1) st.launch_k19 |= 1ull << (st.nw_launches + j);
             if ((x.launch_nwp >> j) & 1) st.launch_nwp |= 1ull << (st.nw_launches + j);
+            if ((x.launch_k3 >> j) & 1) st.launch_k3 |= 1ull << (st.nw_launches + j);
         }
         st.nw_launches += x.nw_launches;
     }

@@ -867,10 +867,11 @@ __global__ void xcc_probe_kernel(uint32_t *out) {
 #ifndef NW16_K5_WAVES_PER_EU
 #define NW16_K5_WAVES_PER_EU 5
 #endif
-// (K = 3 needs fewer registers; 5 keeps the context's slot partitions --
-// the largest residency of any packed form, nw16_np_part_cu -- unchanged)
+// (K = 3: 4 waves per SIMD, 128 VGPRs -- at 5 its second-sweep loops spill;
+// its launches are latency-bound, a few waves per SIMD.  The context's slot
+// partitions hold the largest residency of any packed form, nw16_np_part_cu)
 #ifndef NW16_K3_WAVES_PER_EU
-#define NW16_K3_WAVES_PER_EU 5
+#define NW16_K3_WAVES_PER_EU 4
 #endif
 // the 19-column form holds 6 x 19 per-column registers: 2 waves per SIMD (256
 // VGPRs), which the first-sweep loop's ILP keeps issuing (a 2-wave SIMD ran

@@ -641,6 +641,8 @@ struct UpdLaunch {
     const uint64_t *db_start;
     const uint64_t *flags = nullptr;       // NW launch flags (C_FLAGS): bit 2 = a wave ran no task
     unsigned long long *waste = nullptr;   // candidates computed past a read's accepted one (speculation)
+    const uint32_t *perm = nullptr;        // the candidates are perm[0 .. n) (NULL: 0 .. n); whole reads'
+                                           // sets (imsame_dev.hip: the round-1 launch cut in two)
 };
 
 // Per read (run by its first candidate): the first accepted candidate in
@@ -764,7 +766,7 @@ __global__ void update_kernel(UpdLaunch U) {
     // rows unwritten: consume none of them (the host fails the call)
     if (U.flags && (__hip_atomic_load(U.flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 4u)) return;
     for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < U.n; c += gridDim.x * blockDim.x)
-        update_one(U, c, cells, acc, waste);
+        update_one(U, U.perm ? U.perm[c] : c, cells, acc, waste);
     if (cells) atomicAdd(U.cells, (unsigned long long)cells);
     if (waste && U.waste) atomicAdd(U.waste, (unsigned long long)waste);
     if (acc) atomicAdd(U.nacc, (unsigned long long)acc);

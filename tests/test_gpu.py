@@ -436,6 +436,9 @@ def test_split_rounds_equal(dev, oracle, monkeypatch, capfd):
     q, qs = synth.make_reads_arr(ref, 150_000, 150, seed=82, frac_true=0.67)
     dev.index(ref, rst)
     dev.set_query(q, qs)
+    # (split rounds belong to the joined rounds: with independent pipelines
+    # each pipeline's rounds stay whole)
+    monkeypatch.setenv("IMSAME_PIPES", "0")
     monkeypatch.setenv("IMSAME_SPLIT_ROUNDS", "0")
     base, pb, sb = dev.align(n_threads=16, want_paths=True)
     monkeypatch.delenv("IMSAME_SPLIT_ROUNDS")
@@ -947,8 +950,8 @@ def test_nw16_launch_forms_equal(dev, oracle, monkeypatch):
     assert st.launch_np == 0 and st.launch_k5 == 0
     st = runs["k5_all"][2]
     assert st.launch_k5 == st.launch_pk and st.launch_pk != 0
-    st = runs["k3_all"][2]                        # the 3-column latency form (150-base reads)
-    assert st.launch_k3 == st.launch_pk and st.launch_pk != 0
+    st = runs["k3_all"][2]        # the 3-column latency form (reads <= 150 bases; longer: 5 columns)
+    assert st.launch_k3 != 0 and (st.launch_k3 | st.launch_k5) == st.launch_pk, (hex(st.launch_k3), hex(st.launch_pk))
     for name, (res, pp, st) in runs.items():
         assert not _cmp(res, base), (name, _cmp(res, base))
         if st.launch_np:                          # round 1b ran in both (its speculation sets n_nw)
@@ -1170,3 +1173,77 @@ def test_k19_form_equals_k10_and_oracle(dev, oracle, monkeypatch):
     assert rc == 0
     for (a, b), e in zip(wins, exp):
         assert not _cmp(r19[a:b], e), ((a, b), _cmp(r19[a:b], e))
+
+
+def test_non_acgt_bytes_refused(dev):
+    """include/imsame_dev.h: the database and the reads hold only 'A', 'C',
+    'G', 'T' -- what IMSAME's loaders keep (IMSAME.c:216-221, :340-345) and
+    what the 2-bit codes can tell apart.  An 'N' in the database fails the
+    index build, a lowercase base in a read fails the call (the check runs in
+    the query's packing kernel; the upload's zero padding is not checked),
+    both with IMSAME_E_ARG, and the same inputs with ACGT only align."""
+    from imsame_amd import ImsameError
+    ref, rst = synth.make_reference_arr(400_000, 2_000, seed=5)
+    q, qs = synth.make_reads_arr(ref, 3_000, 150, seed=6)
+    bad = ref.copy()
+    bad[123_457] = ord("N")
+    with pytest.raises(ImsameError) as e:
+        dev.index(bad, rst)
+    assert e.value.code == abi.IMSAME_E_ARG
+    dev.index(ref, rst)
+    qb = q.copy()
+    qb[int(qs[1_777]) + 5] = ord("a")
+    dev.set_query(qb, qs)
+    with pytest.raises(ImsameError) as e:
+        dev.align(n_threads=16)
+    assert e.value.code == abi.IMSAME_E_ARG
+    dev.set_query(q, qs)
+    res, _, st = dev.align(n_threads=16)
+    assert (res["status"] == 1).sum() > 2_000
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("shape", ["shard", "c2_lane"])
+def test_independent_pipelines_equal_joined_rounds(dev, oracle, shape, monkeypatch):
+    """imsame_dev.hip:align_one's independent pipelines: after round 1 the
+    reads with round-1 candidates (A, the lane's stream) and round 1b's reads
+    (B, stream_b, a host thread of its own) run their later rounds apart, each
+    in its own part of the candidate lists.  Every per-read field, every
+    accepted path's text and the NW count equal the joined rounds'
+    (IMSAME_PIPES=0), with round 1's launch cut into its unpredicted and
+    predicted candidates (default) or not (IMSAME_CUT_WEAK=0); the default run
+    equals the oracle on three windows; a third of the reads are random (many
+    later rounds on both pipelines), and IMSAME_SPEC=2 / IMSAME_SPEC_WEAK=8
+    squeeze the pipelines' list parts."""
+    n = 125_000 if shape == "shard" else 400_000
+    ref, rst = synth.make_reference_arr(8_000_000, 2_000, seed=91)
+    q, qs = synth.make_reads_arr(ref, n, 150, seed=92, frac_true=0.67, ins=0.002, dele=0.002)
+    dev.index(ref, rst)
+    dev.set_query(q, qs)
+    monkeypatch.setenv("IMSAME_PIPES", "0")
+    base, pb, sb = dev.align(n_threads=16, want_paths=True)
+    monkeypatch.setenv("IMSAME_PIPES", "1")           # (by default only lanes of >= 200k reads)
+    monkeypatch.setenv("IMSAME_DEBUG_ROUNDS", "1")
+    res = None
+    for env in [{}, {"IMSAME_CUT_WEAK": "0"}, {"IMSAME_SPEC": "2", "IMSAME_SPEC_WEAK": "8"}]:
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        r, pp, st = dev.align(n_threads=16, want_paths=True)
+        for k in env:
+            monkeypatch.delenv(k)
+        assert not _cmp(r, base), (env, _cmp(r, base))
+        if not env:
+            assert st.n_nw == sb.n_nw, (st.n_nw, sb.n_nw)
+            res = r
+        for k in np.flatnonzero(base["status"] == 1)[::173]:
+            s_ = int(base[k]["db_seq"])
+            X = ref[int(rst[s_]):int(rst[s_]) + 2_000].tobytes()
+            Y = q[int(qs[k]):int(qs[k]) + int(base[k]["ylen"])].tobytes()
+            t1, _ = render(X, Y, r[k], pp[r[k]["path_off"]:r[k]["path_off"] + r[k]["path_len"]])
+            t0, _ = render(X, Y, base[k], pb[base[k]["path_off"]:base[k]["path_off"] + base[k]["path_len"]])
+            assert t1 == t0, (env, k)
+    wins = _windows(len(qs))
+    rc, exp, _ = oracle.align_windows(ref, rst, q, qs, wins, None, 16)
+    assert rc == 0
+    for (a, b), e in zip(wins, exp):
+        assert not _cmp(res[a:b], e), ((a, b), _cmp(res[a:b], e))
