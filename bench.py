@@ -36,11 +36,6 @@ import numpy as np
 # does in a multi-rank run); results do not depend on it.
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
     os.environ["GPU_MAX_HW_QUEUES"] = "8"
-# small host<->device copies on a DMA engine instead of a blit kernel: the
-# library zeroes and reads its round counters with them, and a kernel would
-# wait for a wave slot behind the other lanes' NW waves (imsame_dev.hip:
-# zero_async, scripts/micro/small_ops.hip)
-os.environ.setdefault("GPU_FORCE_BLIT_COPY_SIZE", "0")
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)

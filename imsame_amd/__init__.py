@@ -34,10 +34,6 @@ from .abi import Params, Stats, RESULT_DTYPE, PARITY_FIELDS  # noqa: F401
 # queues allow), see INTEGRATION.md.
 if not os.environ.get("GPU_MAX_HW_QUEUES") and not os.environ.get("IMSAME_NO_HWQ_DEFAULT"):
     os.environ["GPU_MAX_HW_QUEUES"] = "8"
-# ... and small copies on a DMA engine (the round counters: imsame_dev.hip:
-# zero_async), same opt-out
-if not os.environ.get("GPU_FORCE_BLIT_COPY_SIZE") and not os.environ.get("IMSAME_NO_HWQ_DEFAULT"):
-    os.environ["GPU_FORCE_BLIT_COPY_SIZE"] = "0"
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DEV = os.environ.get("IMSAME_LIB_DEV") or os.path.join(HERE, "lib", "libimsame_dev.so")

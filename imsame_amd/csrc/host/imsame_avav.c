@@ -179,7 +179,6 @@ static void load_rc(mgen *m, imsame_ctx *ctx) {
 
 int main(int argc, char **argv) {
     setenv("GPU_MAX_HW_QUEUES", "8", 0);     /* one hardware queue per lane (see imsame_cli.c) */
-    setenv("GPU_FORCE_BLIT_COPY_SIZE", "0", 0);   /* small copies on a DMA engine (imsame_dev.hip:zero_async) */
     /* positional arguments exactly as the script; options after them */
     int npos = 0, dry = 0;
     const char *pos[6] = {0}, *devspec = NULL;

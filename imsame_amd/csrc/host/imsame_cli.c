@@ -102,7 +102,6 @@ int main(int argc, char **argv) {
      * runs at most one lane per queue and never sets this itself); a value in
      * the environment is kept.  Before the first HIP call. */
     setenv("GPU_MAX_HW_QUEUES", "8", 0);
-    setenv("GPU_FORCE_BLIT_COPY_SIZE", "0", 0);   /* small copies on a DMA engine (imsame_dev.hip:zero_async) */
     const char *qpath = NULL, *dpath = NULL, *opath = NULL, *devspec = NULL;
     imsame_params prm;
     imsame_params_default(&prm);

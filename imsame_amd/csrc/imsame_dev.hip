@@ -432,27 +432,6 @@ enum { C_NCAND = 0, C_NCAND2, C_NNEXT, C_NCANDB, C_NCAND2B, C_NNEXT2, C_WORKB,  
        C_PROF, C_WIN = C_PROF + 12, C_FBK, C_SWORK, C_DBG = C_SWORK + 3, C_WASTE = C_DBG + 8,
        C_NSLOTS };
 
-// Zero `bytes` at device address p on stream s with a copy from page-locked
-// zeros.  Small copies run on a DMA engine when the process sets
-// GPU_FORCE_BLIT_COPY_SIZE=0 (bench.py, the CLIs and the Python package do,
-// before HIP starts), so they never wait for a wave slot; hipMemsetAsync
-// launches a fill kernel, which waits behind other lanes' NW waves like any
-// kernel: 17 ms against 8 us for a small copy on a chip held by 20-ms waves
-// (scripts/micro/small_ops.hip, profiles/r6m/small_ops_r6l.txt).  Used for the
-// counters of the rounds; larger buffers keep hipMemsetAsync.
-#define ZERO_BYTES 65536
-static int zero_async(void *p, size_t bytes, hipStream_t s) {
-    static std::once_flag f;
-    static void *z = nullptr;
-    std::call_once(f, [] {
-        if (hipHostMalloc(&z, ZERO_BYTES, hipHostMallocDefault) == hipSuccess) memset(z, 0, ZERO_BYTES);
-        else z = nullptr;
-    });
-    if (!z || bytes > ZERO_BYTES) return hipMemsetAsync(p, 0, bytes, s) == hipSuccess ? 0 : IMSAME_E_HIP;
-    return hipMemcpyAsync(p, z, bytes, hipMemcpyHostToDevice, s) == hipSuccess ? 0 : IMSAME_E_HIP;
-}
-#define ZERO(p, bytes, s) do { if (int zrc_ = zero_async((p), (bytes), (s))) return zrc_; } while (0)
-
 static double now_ms() {
     struct timespec ts; clock_gettime(CLOCK_MONOTONIC, &ts);
     return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
@@ -954,7 +933,7 @@ extern "C" int imsame_dev_set_query_range_async(imsame_ctx *c, const uint8_t *q_
     // on the upload stream: every lane (this context's stream included) waits
     // only for the parts that hold its reads
     HIPCHK(hipMemcpyAsync(c->q_start.p, c->h_q_start, ns * 8, hipMemcpyHostToDevice, c->ustream));
-    ZERO((uint8_t *)c->q.p + nb, 64, c->ustream);
+    HIPCHK(hipMemsetAsync((uint8_t *)c->q.p + nb, 0, 64, c->ustream));
     // (the packed copy the seed scan reads, qw, is made by each lane over its
     // own reads once their parts are in HBM: align_one)
     c->qw_end = qw_end; c->qb_end = c->q_base + nb + 64;
@@ -1378,7 +1357,7 @@ static int row_perm(imsame_ctx *c, const int32_t *crow, uint32_t n, uint32_t xca
     DBuf &cperm = qi ? c->cperm_b : c->cperm, &rhist = qi ? c->rhist_b : c->rhist;
     if (cperm.ensure((uint64_t)n * 4) || rhist.ensure((uint64_t)nb * 8)) return IMSAME_E_OOM;
     uint32_t *hist = rhist.as<uint32_t>(), *cur = hist + nb;
-    ZERO(hist, (size_t)nb * 4, s);
+    HIPCHK(hipMemsetAsync(hist, 0, (size_t)nb * 4, s));
     row_hist_kernel<<<std::min(nblk(n, 256), ROW_BLOCKS), 256, 0, s>>>(crow, n, nb, hist);
     row_scan_kernel<<<1, 1024, 0, s>>>(hist, nb, cur);
     row_scatter_kernel<<<std::min(nblk(n, 256), ROW_BLOCKS), 256, 0, s>>>(crow, n, nb, cur, cperm.as<uint32_t>());
@@ -1446,7 +1425,7 @@ static int launch_nw(imsame_ctx *c, NwPlan &pl, const uint32_t *cread, const uin
     P.band_w = pl.band_w; P.redo = (uint32_t *)(ctr + C_REDO); P.win = (uint32_t *)(ctr + C_WIN);
     P.prof = getenv("IMSAME_NW_PROF") ? (unsigned long long *)(ctr + C_PROF) : nullptr;
     P.slot_bits = pl.np ? ao->slotbits.as<uint32_t>() : nullptr; P.slot_words = pl.slot_words;
-    ZERO(work, 4, s);
+    HIPCHK(hipMemsetAsync(work, 0, 4, s));
     HIPCHK(hipEventRecord(e0, s));               // the launch's time includes its ordering
     auto win_params = [&] {
         const char *wu = getenv("IMSAME_NW_WIN_UP"), *wd = getenv("IMSAME_NW_WIN_DOWN");
@@ -1463,7 +1442,7 @@ static int launch_nw(imsame_ctx *c, NwPlan &pl, const uint32_t *cread, const uin
         DBuf &cperm = qi ? c->cperm_b : c->cperm, &rhist = qi ? c->rhist_b : c->rhist;
         if (cperm.ensure((uint64_t)n * 4) || rhist.ensure((uint64_t)nb * 8)) return IMSAME_E_OOM;
         uint32_t *hist = rhist.as<uint32_t>(), *cur = hist + nb;
-        ZERO(hist, (size_t)nb * 4, s);
+        HIPCHK(hipMemsetAsync(hist, 0, (size_t)nb * 4, s));
         row_hist_kernel<<<std::min(nblk(n, 256), ROW_BLOCKS), 256, 0, s>>>(crow, n, nb, hist);
         row_scan_kernel<<<1, 1024, 0, s>>>(hist, nb, cur);
         row_scatter_kernel<<<std::min(nblk(n, 256), ROW_BLOCKS), 256, 0, s>>>(crow, n, nb, cur, cperm.as<uint32_t>());
@@ -1666,7 +1645,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     const uint8_t *qd = dev_q(c);
     const uint64_t *qsd = dev_qs(c);
     uint64_t *ctr = c->ctr.as<uint64_t>();
-    ZERO(ctr, C_NSLOTS * 8, s);
+    HIPCHK(hipMemsetAsync(ctr, 0, C_NSLOTS * 8, s));
     const unsigned long long errinit = ~0ull;
     HIPCHK(hipMemcpyAsync(ctr + C_ERR, &errinit, 8, hipMemcpyHostToDevice, s));
     // This lane's packed query words (seed_kernel.hip:pk_word; queued after
@@ -1712,7 +1691,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     while (nact) {
         st.rounds++;
         c->cur_round = t_round = (int)st.rounds;
-        ZERO(ctr + C_NCAND, 7 * 8, s);     // NCAND, NCAND2, NNEXT, (1b) NCANDB, NCAND2B, NNEXT2, WORKB
+        HIPCHK(hipMemsetAsync(ctr + C_NCAND, 0, 7 * 8, s));     // NCAND, NCAND2, NNEXT, (1b) NCANDB, NCAND2B, NNEXT2, WORKB
         SeedLaunch S;
         S.db = c->db.as<uint8_t>(); S.db_start = c->db_start.as<uint64_t>(); S.n_db = c->n_db; S.db_len = c->db_len;
         S.dbw = c->dbw.as<uint32_t>(); S.qw = dev_qw(c);
@@ -1739,7 +1718,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         S.err = (unsigned long long *)(ctr + C_ERR); S.nhits = (unsigned long long *)(ctr + C_HITS);
         S.nwork = (unsigned long long *)(ctr + C_SWORK);
         S.dbg = getenv("IMSAME_DEBUG_ROUNDS") ? (unsigned long long *)(ctr + C_DBG) : nullptr;
-        if (S.dbg) ZERO(S.dbg, 8 * 8, s);
+        if (S.dbg) HIPCHK(hipMemsetAsync(S.dbg, 0, 8 * 8, s));
         S.wcap = c->use_wcap ? c->wcap.as<uint64_t>() : nullptr;
         S.wstart = c->use_wstart ? c->wstart.as<uint64_t>() : nullptr;
         S.minlen = c->minlen.as<uint32_t>(); S.n_minlen = ymax + 1;
@@ -1993,7 +1972,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
                 while (P.nact) {
                     ++P.rnd;
                     t_round = (int)P.rnd;
-                    ZERO(ctr + P.cn, 3 * 8, P.s);       // ncand, ncand2, nnext
+                    HIPCHK(hipMemsetAsync(ctr + P.cn, 0, 3 * 8, P.s));       // ncand, ncand2, nnext
                     SeedLaunch Sp = S;
                     Sp.active = P.act; Sp.n_active = P.nact;
                     // speculation within this pipeline's part of the lists
@@ -2099,7 +2078,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
             // count), then its rounds
             Pipe A = {s, 0, c->ev0, c->ev1, c->act3.as<uint32_t>(), act, 0, 0, n1, C_NCAND, C_WORK, 1};
             const int rcA = [&]() -> int {
-                ZERO(ctr + C_NNEXT, 8, s);
+                HIPCHK(hipMemsetAsync(ctr + C_NNEXT, 0, 8, s));
                 if (n1 && crow && pla.two && cut_weak_on()) {
                     uint32_t k = 0;
                     if (int r = row_perm(c, crow, n1, (uint32_t)pla.xcap, 0, &k)) return r;
