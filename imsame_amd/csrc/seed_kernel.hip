@@ -444,6 +444,9 @@ __device__ __forceinline__ bool emit_has(const uint32_t (&em)[SM], uint32_t ne, 
     return f;
 }
 
+#ifndef SEED_PREFETCH
+#define SEED_PREFETCH 1
+#endif
 // SM: the most candidates a read may emit (its list in LDS, emit[] in registers)
 template <int L, int SM = SPEC_MAX>
 __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane, uint2 *lst, SeedTally &tl) {
@@ -475,16 +478,31 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
     uint32_t e0p = 0, e0r = 0;             // first candidate's window (read-relative) and bucket rank
     bool done = !gvalid || p >= up_to || read_irrelevant(S, ylen), paused = false,
          exhausted = gvalid && p >= up_to;
+    // The CSR bounds of a lane's window are loaded one window ahead (SEED_PREFETCH):
+    // the bucket offsets of the window the lane scans next (p + L + wl, if the
+    // group advances) are in flight while the current window's entries and
+    // extensions are walked, one dependent load fewer per window on the chain
+    // offsets -> entries -> record bounds -> bases.
+    uint64_t pf_lo = 0, pf_hi = 0;
+    auto bounds = [&](const uint64_t w) {
+        const uint32_t code = kmer_code_pk(S.qw, w);
+        pf_lo = S.off[code]; pf_hi = S.off[code + 1];
+    };
+    if (SEED_PREFETCH && !done && p + (uint64_t)wl < up_to) bounds(p + (uint64_t)wl);
     while (wv_any(!done)) {
         // ---- every lane scans its window (no wave ops in here)
         const uint64_t pw = p + (uint64_t)wl;
         uint32_t nl = 0, last_rel = 0, ev = 0;
         bool full = false;
+        uint64_t wbase = pf_lo, hi = pf_hi;
+        if (SEED_PREFETCH && !done && pw + (uint64_t)L < up_to) bounds(pw + (uint64_t)L);
         if (!done && pw < up_to) {
             // (a read that may still start speculating lists for it already)
             const uint32_t need = (ne == 0 && nm == 0 && S.spec_weak > spec ? S.spec_weak : spec) - ne;
-            const uint32_t code = kmer_code_pk(S.qw, pw);
-            const uint64_t wbase = S.off[code], hi = S.off[code + 1];
+            if (!SEED_PREFETCH) {
+                const uint32_t code = kmer_code_pk(S.qw, pw);
+                wbase = S.off[code]; hi = S.off[code + 1];
+            }
             ++tl.wins;
             for (uint64_t e = wbase + (wl == 0 ? h : 0u); e < hi; ++e) {
                 const uint2 ent = S.ent[e];
