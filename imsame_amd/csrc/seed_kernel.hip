@@ -444,8 +444,11 @@ __device__ __forceinline__ bool emit_has(const uint32_t (&em)[SM], uint32_t ne, 
     return f;
 }
 
+// (measured and dropped, round 6: C2 101.05-101.07 vs 101.10-101.17 ms, the 1/8
+// shard 15.39 vs 15.37, C3 377.3 vs 376.5 -- the scan's bound is not the
+// offsets' load, profiles/r6o/; off by default)
 #ifndef SEED_PREFETCH
-#define SEED_PREFETCH 1
+#define SEED_PREFETCH 0
 #endif
 // SM: the most candidates a read may emit (its list in LDS, emit[] in registers)
 template <int L, int SM = SPEC_MAX>
