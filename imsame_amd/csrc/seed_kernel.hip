@@ -152,17 +152,82 @@ __device__ __forceinline__ uint32_t kmer_code_pk(const uint32_t *__restrict__ w,
     return (((r >> 1) & 0x55555555u) | ((r & 0x55555555u) << 1)) >> (32 - 2 * IMSAME_FIXED_K);
 }
 
+// Eight steps of the ungapped walk at once.  Each step of the reference's
+// walk (alignmentFromQuickHits :321-337 right, :344-360 left) adds +-POINT to
+// the score, counts an identity on a match, moves the best end when
+// best <= score, and the walk stops after the step that takes the score to
+// <= 0.  Over 8 steps whose match bits are m (bit j = step j) from a score of
+// POINT*t, all of that is a function of (t, m) for t = 1..8 (t >= 9 cannot
+// stop within 8 steps, so one row serves them all; row 0 = already stopped):
+//   bits 0-3   js: the step the walk stops at, 8 = none
+//   bits 4-8   mx + 8: the highest score (in POINTs, relative to the start)
+//              of the steps before js (-8 if none)
+//   bits 9-11  am: the LAST step reaching mx (ties move the end, :334)
+//   bits 12-15 pc: identities up to js (all 8 steps when js = 8)
+// The walk takes a table row per 8 bases instead of ~13 instructions and an
+// exec-mask branch per base (the scan ran ~654 extensions per read at C3).
+static_assert(IMSAME_POINT == 4, "ung_half scales t by POINT = 4");
+struct UngTab { uint16_t v[10 * 256]; };
+constexpr UngTab make_ung_tab() {
+    UngTab T{};
+    for (int t = 0; t < 10; ++t)
+        for (int m = 0; m < 256; ++m) {
+            int js = t ? 8 : 0, mx = -8, am = 0, pc = 0, s = 0;
+            for (int j = 0; j < 8 && t; ++j) {
+                const int eq = (m >> j) & 1;
+                s += eq ? 1 : -1;
+                pc += eq;
+                if (t < 9 && t + s <= 0) { js = j; break; }
+                if (mx <= s) { mx = s; am = j; }
+            }
+            T.v[t * 256 + m] = (uint16_t)(js | (mx + 8) << 4 | am << 9 | pc << 12);
+        }
+    return T;
+}
+__device__ constexpr UngTab g_ung_tab = make_ung_tab();
+#define UNG_TAB_WORDS (10 * 256 / 2)
+// a block's copy of the table in LDS (every thread of the block calls it)
+__device__ __forceinline__ void ung_tab_load(uint16_t *lds) {
+#ifndef IMSAME_WAVE_EMU
+    const uint32_t *g = (const uint32_t *)g_ung_tab.v;
+    for (uint32_t i = threadIdx.x; i < UNG_TAB_WORDS; i += blockDim.x) ((uint32_t *)lds)[i] = g[i];
+    __syncthreads();
+#endif
+}
+// one 8-step row: m8 = match bits, xr = the first step's position relative to
+// the walk's origin, dir = +1 (right walk) / -1 (left walk)
+__device__ __forceinline__ void ung_half(const uint16_t *__restrict__ tab, uint32_t m8, int &sc, int &best,
+                                         int &endrel, uint32_t &idents, int xr, int dir) {
+    const int t = min(max(sc, 0) >> 2, 9);
+    const uint32_t e = tab[t * 256 + (int)m8];
+    const int cand = sc + IMSAME_POINT * ((int)((e >> 4) & 31u) - 8);
+    if (best <= cand) { best = cand; endrel = xr + dir * (int)((e >> 9) & 7u); }
+    const uint32_t pc = e >> 12;
+    idents += pc;
+    sc = (e & 15u) < 8u ? 0 : sc + IMSAME_POINT * (2 * (int)pc - 8);
+}
+// 16 steps' match bits from pk_diff's mismatch bits (step k at bit 2k),
+// steps >= n treated as mismatches: steps 0-7 in bits 0-7, 8-15 in bits 16-23
+__device__ __forceinline__ uint32_t ung_match16(uint32_t mism, int64_t n) {
+    uint32_t x = ~mism & (n >= 16 ? 0x55555555u : ((1u << (2 * (uint32_t)n)) - 1u) & 0x55555555u);
+    x = (x | (x >> 1)) & 0x33333333u;
+    x = (x | (x >> 2)) & 0x0F0F0F0Fu;
+    return (x | (x >> 4)) & 0x00FF00FFu;
+}
+
 // alignmentFromQuickHits (alignmentFunctions.c:276-387): the raw score in the
 // reference's u64 wrap arithmetic (:373).  Loop bounds fold the reference's
 // per-step tests (:321-322, :344-345) into one limit per direction.  The
 // base-serial walk of the reference runs over 16-base chunks of the packed
 // buffers (one dword load per chunk and side, the mismatches of 16 bases from
-// one xor); the first chunk of each direction is fetched before either walk
-// starts.
+// one xor, two table rows per chunk: ung_half); the first chunk of each
+// direction is fetched before either walk starts.  tab: g_ung_tab (its LDS
+// copy in the scan kernels).
 // (*nch, when given, counts the 16-base chunk pairs loaded)
-__device__ __forceinline__ uint64_t ungapped_raw(const uint32_t *__restrict__ db, const uint32_t *__restrict__ q,
-                                                 int64_t pd0, int64_t pq0, int64_t xs, int64_t xe, int64_t ys,
-                                                 int64_t ye, int64_t dbl, int64_t ql, uint32_t *nch = nullptr) {
+__device__ __forceinline__ uint64_t ungapped_raw(const uint16_t *__restrict__ tab, const uint32_t *__restrict__ db,
+                                                 const uint32_t *__restrict__ q, int64_t pd0, int64_t pq0, int64_t xs,
+                                                 int64_t xe, int64_t ys, int64_t ye, int64_t dbl, int64_t ql,
+                                                 uint32_t *nch = nullptr) {
     int64_t end_x = pd0 - 1, beg_x = end_x - IMSAME_FIXED_K + 1;
     int sc = IMSAME_FIXED_K * IMSAME_POINT, best_r = sc, best_l = sc;
     uint32_t idents = IMSAME_FIXED_K;
@@ -184,40 +249,36 @@ __device__ __forceinline__ uint64_t ungapped_raw(const uint32_t *__restrict__ db
     }
     uint32_t nc = lwin ? 2 : 1;
     const int64_t fx = min(min(dbl - 1, xe), pd0 + (min(ql - 1, ye) - pq0));
+    // (steps past n are mismatches to the table: they come after the last
+    // real step, so they cannot move the best end, and the walk ends there)
+    int er = -1;                        // end_x - pd0
     for (int64_t x = pd0; sc > 0 && x <= fx;) {
         const int64_t n = min((int64_t)16, fx - x + 1);
-        const uint32_t ne = pk_diff(wv_alignbit(d1, d0, dsh), wv_alignbit(q1, q0, qsh));
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            if (k < n && sc > 0) {
-                const bool eq = !((ne >> (2 * k)) & 1u);
-                sc += eq ? IMSAME_POINT : -IMSAME_POINT;
-                idents += eq;
-                if (best_r <= sc) { best_r = sc; end_x = x + k; }
-            }
-        }
+        const uint32_t m = ung_match16(pk_diff(wv_alignbit(d1, d0, dsh), wv_alignbit(q1, q0, qsh)), n);
+        const int xr = (int)(x - pd0);
+        ung_half(tab, m & 0xFFu, sc, best_r, er, idents, xr, 1);
+        ung_half(tab, m >> 16, sc, best_r, er, idents, xr + 8, 1);
         x += n;                             // n < 16 only for the last chunk (x > fx after it)
         if (sc > 0 && x <= fx) { d0 = d1; d1 = db[(x >> 4) + 1]; q0 = q1; q1 = q[((x + dq) >> 4) + 1]; ++nc; }
     }
+    end_x = pd0 + er;
     sc = best_r;                        // left pass restarts from the right max, best_l stays 48 (:339)
     const int64_t lx = max(max((int64_t)0, xs), bx0 - (by0 - max((int64_t)0, ys)));
     int64_t x = bx0, y = by0;
     if (lwin) {
+        // a chunk's slot 15 - k is step k: bit-reversed, step k's mismatch bit lands at 2k
+        int bl = 1;                     // beg_x - bx0
         while (sc > 0 && x >= lx && x >= 15 && y >= 15) {
             const int64_t n = min((int64_t)16, x - lx + 1);
-            const uint32_t ne = pk_diff(wv_alignbit(l1, l0, lsh), wv_alignbit(m1, m0, lqsh));
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                if (k < n && sc > 0) {
-                    const bool eq = !((ne >> (2 * (15 - k))) & 1u);
-                    sc += eq ? IMSAME_POINT : -IMSAME_POINT;
-                    idents += eq;
-                    if (best_l <= sc) { best_l = sc; beg_x = x - k; }
-                }
-            }
+            const uint32_t mism = wv_bitrev(pk_diff(wv_alignbit(l1, l0, lsh), wv_alignbit(m1, m0, lqsh))) >> 1;
+            const uint32_t m = ung_match16(mism, n);
+            const int xr = (int)(x - bx0);
+            ung_half(tab, m & 0xFFu, sc, best_l, bl, idents, xr, -1);
+            ung_half(tab, m >> 16, sc, best_l, bl, idents, xr - 8, -1);
             x -= n; y -= n;                 // n < 16 only when x passes lx (the loop ends)
             if (sc > 0 && x >= lx && x >= 15 && y >= 15) { l1 = l0; l0 = db[(x - 15) >> 4]; m1 = m0; m0 = q[(y - 15) >> 4]; ++nc; }
         }
+        beg_x = bx0 + bl;
     }
     for (; sc > 0 && x >= lx; --x, --y) {                 // the first 15 bases of a buffer
         if (pk_base(db, x) == pk_base(q, y)) { sc += IMSAME_POINT; ++idents; } else sc -= IMSAME_POINT;
@@ -294,7 +355,7 @@ __device__ __forceinline__ uint32_t spec_after_first(const SeedLaunch &S, uint32
     return (nm == 0 && S.spec_weak > spec && weak_hit(raw, ylen)) ? S.spec_weak : spec;
 }
 
-__device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, SeedTally &tl) {
+__device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, SeedTally &tl, const uint16_t *tab) {
     const uint64_t r = S.active[idx], k = r - S.read_from;
     const uint64_t rs = S.q_start[r], re = S.q_start[r + 1];
     const uint64_t ylen = re - rs;
@@ -362,7 +423,7 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, Seed
             const int64_t xs = (int64_t)S.db_start[sid];
             const int64_t xe = (sid == S.n_db - 1) ? (int64_t)S.db_len : (int64_t)S.db_start[sid + 1] - 1;
             ++tl.hits;
-            const uint64_t raw = ungapped_raw(S.dbw, S.qw, xs + ent.x, (int64_t)p + 1, xs, xe, ys, ye,
+            const uint64_t raw = ungapped_raw(tab, S.dbw, S.qw, xs + ent.x, (int64_t)p + 1, xs, xe, ys, ye,
                                               (int64_t)S.db_len, (int64_t)S.q_len, &tl.chunks);
             if (mraw != ~0ull && raw >= mraw) {                      // e < min_e (:139)
                 const uint64_t xlen = S.db_start[sid + 1] - S.db_start[sid];
@@ -452,7 +513,8 @@ __device__ __forceinline__ bool emit_has(const uint32_t (&em)[SM], uint32_t ne, 
 #endif
 // SM: the most candidates a read may emit (its list in LDS, emit[] in registers)
 template <int L, int SM = SPEC_MAX>
-__device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane, uint2 *lst, SeedTally &tl) {
+__device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane, uint2 *lst, SeedTally &tl,
+                           const uint16_t *tab) {
     const bool gvalid = gidx < S.n_active;
     const int gbase = lane - wl;                                  // first lane of the group
     uint64_t r = 0, k = 0, rs = 0, re = 0, ylen = 0, up_to = 0, p = 0;
@@ -519,7 +581,7 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
                 ++ev;
                 const int64_t xs = (int64_t)S.db_start[sid];
                 const int64_t xe = (sid == S.n_db - 1) ? (int64_t)S.db_len : (int64_t)S.db_start[sid + 1] - 1;
-                const uint64_t raw = ungapped_raw(S.dbw, S.qw, xs + ent.x, (int64_t)pw + 1, xs, xe, ys, ye,
+                const uint64_t raw = ungapped_raw(tab, S.dbw, S.qw, xs + ent.x, (int64_t)pw + 1, xs, xe, ys, ye,
                                                   (int64_t)S.db_len, (int64_t)S.q_len, &tl.chunks);
                 if (mraw != ~0ull && raw >= mraw) {                      // e < min_e (:139)
                     const uint64_t xlen = S.db_start[sid + 1] - S.db_start[sid];
@@ -607,7 +669,7 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
         const uint2 ent = S.ent[S.off[kmer_code_pk(S.qw, rs + e0p)] + e0r];
         const int64_t xs = (int64_t)S.db_start[ent.y];
         const int64_t xe = (ent.y == S.n_db - 1) ? (int64_t)S.db_len : (int64_t)S.db_start[ent.y + 1] - 1;
-        const uint64_t raw = ungapped_raw(S.dbw, S.qw, xs + ent.x, (int64_t)(rs + e0p) + 1, xs, xe, ys, ye,
+        const uint64_t raw = ungapped_raw(tab, S.dbw, S.qw, xs + ent.x, (int64_t)(rs + e0p) + 1, xs, xe, ys, ye,
                                           (int64_t)S.db_len, (int64_t)S.q_len);
         S.crow[o] = predicted_row(raw, ylen, ent.x, (int64_t)e0p + 1, S.weak_rows);
         for (uint32_t m = 1; m < ne; ++m) S.crow[o + m] = INT32_MIN;
@@ -640,7 +702,7 @@ __device__ __forceinline__ void accept_window_one(const SeedLaunch &S, const ims
         for (uint64_t e = S.off[code]; e < S.off[code + 1]; ++e) {
             const uint2 ent = S.ent[e];
             if (ent.y != sid) continue;
-            const uint64_t raw = ungapped_raw(S.dbw, S.qw, xs + ent.x, (int64_t)p + 1, xs, xe, ys, ye,
+            const uint64_t raw = ungapped_raw(g_ung_tab.v, S.dbw, S.qw, xs + ent.x, (int64_t)p + 1, xs, xe, ys, ye,
                                               (int64_t)S.db_len, (int64_t)S.q_len);
             if (mraw != ~0ull && raw >= mraw) { w = p; break; }
         }
@@ -760,18 +822,22 @@ void seed_group_kernel(SeedLaunch S) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x & 63, wl = lane % L;
     uint2 *lst = (uint2 *)smem + threadIdx.x * SM;
+    __shared__ uint16_t tab[10 * 256];
+    ung_tab_load(tab);
     constexpr uint32_t GPW = 64 / L;                       // groups per wave
     const uint32_t nwv = gridDim.x * (blockDim.x >> 6);
     SeedTally tl;
     for (uint32_t wv = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); (uint64_t)wv * GPW < S.n_active; wv += nwv)
-        seed_group<L, SM>(S, wv * GPW + (uint32_t)lane / L, wl, lane, lst, tl);
+        seed_group<L, SM>(S, wv * GPW + (uint32_t)lane / L, wl, lane, lst, tl, tab);
     seed_tally_flush(S, tl);
 }
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEED_WAVES_PER_EU))) void seed_kernel(SeedLaunch S) {
+    __shared__ uint16_t tab[10 * 256];
+    ung_tab_load(tab);
     SeedTally tl;
     for (uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x; idx < S.n_active; idx += gridDim.x * blockDim.x)
-        seed_one(S, idx, tl);
+        seed_one(S, idx, tl, tab);
     seed_tally_flush(S, tl);
 }
 

@@ -438,7 +438,7 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
             if (L <= 1) {
                 for (uint32_t i = 0; i < na; ++i) {
                     SeedTally tl;
-                    seed_one(SL, i, tl);
+                    seed_one(SL, i, tl, g_ung_tab.v);
                     nhits += tl.hits; swin += tl.wins; sent += tl.ents; sch += tl.chunks;
                 }
             } else {                   // seed_group_kernel: 64-lane waves, several host threads
@@ -455,10 +455,10 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
                         run_wave([&](int lane) {
                             SeedTally h;
                             const uint32_t gidx = (uint32_t)((w0 + lane) / L);
-                            if (L == 64) seed_group<64, SPEC_BIG>(SL, gidx, lane, lane, ld + lane * SPEC_BIG, h);
-                            else if (L >= 16) seed_group<16>(SL, gidx, lane % 16, lane, ld + lane * SPEC_MAX, h);
-                            else if (L >= 4) seed_group<4>(SL, gidx, lane % 4, lane, ld + lane * SPEC_MAX, h);
-                            else         seed_group<2>(SL, gidx, lane % 2, lane, ld + lane * SPEC_MAX, h);
+                            if (L == 64) seed_group<64, SPEC_BIG>(SL, gidx, lane, lane, ld + lane * SPEC_BIG, h, g_ung_tab.v);
+                            else if (L >= 16) seed_group<16>(SL, gidx, lane % 16, lane, ld + lane * SPEC_MAX, h, g_ung_tab.v);
+                            else if (L >= 4) seed_group<4>(SL, gidx, lane % 4, lane, ld + lane * SPEC_MAX, h, g_ung_tab.v);
+                            else         seed_group<2>(SL, gidx, lane % 2, lane, ld + lane * SPEC_MAX, h, g_ung_tab.v);
                             wh += h.hits; ww += h.wins; we += h.ents; wc += h.chunks;
                         });
                     }
@@ -540,7 +540,7 @@ extern "C" uint64_t emu_ungapped(const uint8_t *db, uint64_t db_len, const uint6
     const int64_t xe = (sid == n_db - 1) ? (int64_t)db_len : (int64_t)db_start[sid + 1] - 1;
     const int64_t ys = (int64_t)q_start[read];
     const int64_t ye = (read == n_q - 1) ? (int64_t)q_len : (int64_t)q_start[read + 1] - 1;
-    return ungapped_raw(dbw.data(), qw.data(), (int64_t)pd0, (int64_t)pq0,
+    return ungapped_raw(g_ung_tab.v, dbw.data(), qw.data(), (int64_t)pd0, (int64_t)pq0,
                         xs, xe, ys, ye, (int64_t)db_len, (int64_t)q_len);
 }
 

@@ -560,6 +560,29 @@ def test_emulated_ungapped_matches_reference_golden(emu, oracle):
     for off in (12, 13, 40, 200, 399, 400):
         exp = oracle.ungapped(ref, rst, q2, qs2, 1000 + off, off, 0, sid).raw
         assert _emu_ungapped(emu, ref, rst, q2, qs2, 1000 + off, off, 0, sid) == exp
+    # true diagonals with sparse mismatches (walks of many chunks that stop
+    # anywhere in an 8-step table row, or run into a read's or a record's end
+    # inside a chunk), every seed position of reads of ragged lengths
+    base = 20_000
+    src = ref[base:base + 1200].copy()
+    for rate in (0.03, 0.12, 0.3):
+        q3 = src.copy()
+        mm = rng.random(len(q3)) < rate
+        q3[mm] = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, int(mm.sum()))]
+        cuts = np.sort(rng.choice(np.arange(20, len(q3) - 20), 9, replace=False))
+        qs3 = np.concatenate([[0], cuts]).astype(np.uint64)
+        for rd in range(len(qs3)):
+            ys = int(qs3[rd])
+            ye = int(qs3[rd + 1]) if rd + 1 < len(qs3) else len(q3)
+            for pq0 in range(ys + 12, ye + 1, 3):
+                pd0 = base + pq0
+                sid = int(np.searchsorted(rst, pd0 - 12, side="right") - 1)
+                if int(rst[sid]) > pd0 - 12 or (sid + 1 < len(rst) and int(rst[sid + 1]) < pd0):
+                    continue                # seeds lie inside one record
+                exp = oracle.ungapped(ref, rst, q3, qs3, pd0, pq0, rd, sid).raw
+                assert _emu_ungapped(emu, ref, rst, q3, qs3, pd0, pq0, rd, sid) == exp, (rate, rd, pq0)
+                n += 1
+    assert n > 2600
 
 
 @pytest.mark.parametrize("flags", [0, imsame_amd.FLAG_NW32], ids=["auto", "nw32"])
