@@ -103,19 +103,26 @@ __global__ void kmer_code_kernel(const uint8_t *seq, uint64_t L, const uint32_t 
     }
 }
 
-// Entry = {pos - start[record], record}: 8 bytes whatever the database size
-// (positions past 2^32 need no wider entry; records stay < 2^32 bases).
-// The reference's pos (last base + 1, IMSAME.c:247) is start[record] + x.
+// Entry = {x, record}: 8 bytes whatever the database size.  The reference's
+// pos (last base + 1, IMSAME.c:247) is x itself below 2^32 bases (abs: the
+// scan loads a hit's bases without waiting for its record's start,
+// seed_kernel.hip:ent_pos), else start[record] + x (records stay < 2^32 bases).
 __global__ void kmer_scatter(const uint32_t *codes, uint64_t L, const uint64_t *off, uint32_t *fill,
-                             const uint64_t *st, uint64_t n_db, uint2 *ent) {
+                             const uint64_t *st, uint64_t n_db, uint2 *ent, bool abs) {
     GRID_STRIDE(p, L) {
         const uint32_t c = codes[p];
         if (c == 0xFFFFFFFFu) continue;
         uint64_t lo = 0, hi = n_db;             // last record with start <= p
         while (hi - lo > 1) { uint64_t m = (lo + hi) >> 1; if (st[m] <= p) lo = m; else hi = m; }
         const uint64_t slot = off[c] + atomicAdd(&fill[c], 1u);
-        ent[slot] = make_uint2((uint32_t)(p + 1 - st[lo]), (uint32_t)lo);
+        ent[slot] = make_uint2((uint32_t)(p + 1 - (abs ? 0 : st[lo])), (uint32_t)lo);
     }
+}
+// the absolute entry form where positions fit (IMSAME_ENT_REL=1: the relative
+// form everywhere, tests)
+static bool ent_abs_for(uint64_t db_len) {
+    const char *e = getenv("IMSAME_ENT_REL");
+    return !(e && atoi(e)) && db_len < 0xFFFFFFFFull;
 }
 
 // records are contiguous and ascending, so descending pos = descending (record, x)
@@ -315,6 +322,7 @@ struct imsame_ctx {
     // database + index; dbw: the bases 2-bit packed (seed_kernel.hip:pk_word)
     DBuf db, db_start, off, ent, brk, codes, fill, big, dbw;
     uint64_t n_db = 0, db_len = 0, n_ent = 0;
+    bool ent_abs = false;             // index entries in the absolute form (kmer_scatter)
     uint32_t max_rec = 0;
     std::vector<uint64_t> h_db_start;
     bool have_index = false;
@@ -705,7 +713,7 @@ static int lane_sub(imsame_ctx *c, int k, imsame_ctx **out) {
     imsame_ctx *l = c->subs[k - 1];
     l->db = c->db; l->db_start = c->db_start; l->off = c->off; l->ent = c->ent; l->q = c->q; l->q_start = c->q_start;
     l->dbw = c->dbw; l->qw = c->qw; l->qw_base = c->qw_base; l->qw_end = c->qw_end; l->qb_end = c->qb_end;
-    l->n_db = c->n_db; l->db_len = c->db_len; l->n_ent = c->n_ent; l->max_rec = c->max_rec;
+    l->n_db = c->n_db; l->db_len = c->db_len; l->n_ent = c->n_ent; l->max_rec = c->max_rec; l->ent_abs = c->ent_abs;
     l->have_index = c->have_index;
     l->n_q = c->n_q; l->q_len = c->q_len; l->q_lo = c->q_lo; l->q_hi = c->q_hi; l->q_base = c->q_base;
     l->q_lo_first = c->q_lo_first; l->hq = c->hq; l->hqb = c->hqb; l->have_query = c->have_query;
@@ -795,11 +803,12 @@ extern "C" int imsame_dev_index(imsame_ctx *c, const uint8_t *db_seq, uint64_t d
         if (hbad) return IMSAME_E_ARG;                 // not an ACGT-filtered database (the header)
     }
     c->n_ent = total;
+    c->ent_abs = ent_abs_for(db_len);
     if (c->ent.ensure((total + 1) * 8)) return IMSAME_E_OOM;
     HIPCHK(hipMemsetAsync(c->fill.p, 0, (uint64_t)NBUCKETS * 4, s));
     if (db_len) kmer_scatter<<<gsblk(db_len, 256), 256, 0, s>>>(c->codes.as<uint32_t>(), db_len, c->off.as<uint64_t>(),
                                                               c->fill.as<uint32_t>(), c->db_start.as<uint64_t>(), n_db,
-                                                              c->ent.as<uint2>());
+                                                              c->ent.as<uint2>(), c->ent_abs);
     POISON_SYNC(s, "kmer_scatter", c);
     uint32_t *nbig = c->fill.as<uint32_t>();       // fill is free again: reuse as a counter
     HIPCHK(hipMemsetAsync(nbig, 0, 4, s));
@@ -1697,7 +1706,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         S.dbw = c->dbw.as<uint32_t>(); S.qw = dev_qw(c);
         S.q = qd; S.q_start = qsd; S.n_q = c->n_q; S.q_len = c->q_len;
         S.qs_lo = c->q_lo; S.qs_lo_first = c->q_lo_first;
-        S.off = c->off.as<uint64_t>(); S.ent = c->ent.as<uint2>();
+        S.off = c->off.as<uint64_t>(); S.ent = c->ent.as<uint2>(); S.ent_abs = c->ent_abs;
         S.active = act; S.n_active = nact;
         S.read_from = read_from;
         S.T = n_threads_semantic ? n_threads_semantic : 1;
@@ -1730,11 +1739,19 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
             // (IMSAME_SEED_BLOCKS: at most this many blocks, the kernels stride)
             auto sb = [&](uint64_t lanes) { return std::min<unsigned>(nblk(lanes, 256), seed_blocks()); };
             HIPCHK(hipEventRecord(e0, ss));
-            if (L >= 64)      seed_group_kernel<64, SPEC_BIG><<<sb((uint64_t)na * 64), 256, 256 * SPEC_BIG * 8, ss>>>(SL);
-            else if (L >= 16) seed_group_kernel<16><<<sb((uint64_t)na * 16), 256, slds, ss>>>(SL);
-            else if (L >= 4) seed_group_kernel<4><<<sb((uint64_t)na * 4), 256, slds, ss>>>(SL);
-            else if (L >= 2) seed_group_kernel<2><<<sb((uint64_t)na * 2), 256, slds, ss>>>(SL);
-            else             seed_kernel<<<sb(na), 256, 0, ss>>>(SL);
+            if (SL.ent_abs) {
+                if (L >= 64)      seed_group_kernel<64, SPEC_BIG, true><<<sb((uint64_t)na * 64), 256, 256 * SPEC_BIG * 8, ss>>>(SL);
+                else if (L >= 16) seed_group_kernel<16, SPEC_MAX, true><<<sb((uint64_t)na * 16), 256, slds, ss>>>(SL);
+                else if (L >= 4)  seed_group_kernel<4, SPEC_MAX, true><<<sb((uint64_t)na * 4), 256, slds, ss>>>(SL);
+                else if (L >= 2)  seed_group_kernel<2, SPEC_MAX, true><<<sb((uint64_t)na * 2), 256, slds, ss>>>(SL);
+                else              seed_kernel<true><<<sb(na), 256, 0, ss>>>(SL);
+            } else {
+                if (L >= 64)      seed_group_kernel<64, SPEC_BIG, false><<<sb((uint64_t)na * 64), 256, 256 * SPEC_BIG * 8, ss>>>(SL);
+                else if (L >= 16) seed_group_kernel<16, SPEC_MAX, false><<<sb((uint64_t)na * 16), 256, slds, ss>>>(SL);
+                else if (L >= 4)  seed_group_kernel<4, SPEC_MAX, false><<<sb((uint64_t)na * 4), 256, slds, ss>>>(SL);
+                else if (L >= 2)  seed_group_kernel<2, SPEC_MAX, false><<<sb((uint64_t)na * 2), 256, slds, ss>>>(SL);
+                else              seed_kernel<false><<<sb(na), 256, 0, ss>>>(SL);
+            }
             POISON_SYNC(ss, "seed kernel", c);
             HIPCHK(hipEventRecord(e1, ss));
             HIPCHK(hipGetLastError());
@@ -2629,7 +2646,7 @@ extern "C" int imsame_dev_align_windows(imsame_ctx *c, uint64_t read_from, uint6
         S.dbw = c->dbw.as<uint32_t>(); S.qw = dev_qw(c);
         S.q = dev_q(c); S.q_start = dev_qs(c); S.n_q = c->n_q; S.q_len = c->q_len;
         S.qs_lo = c->q_lo; S.qs_lo_first = c->q_lo_first;
-        S.off = c->off.as<uint64_t>(); S.ent = c->ent.as<uint2>();
+        S.off = c->off.as<uint64_t>(); S.ent = c->ent.as<uint2>(); S.ent_abs = c->ent_abs;
         S.read_from = read_from;
         S.T = n_threads_semantic ? n_threads_semantic : 1;
         S.rpt = (uint64_t)floorl((long double)c->n_q / (long double)S.T);     // IMSAME.c:414

@@ -26,6 +26,7 @@ struct SeedLaunch {
     const uint32_t *dbw, *qw;              // the same bases 2-bit packed (pk_base: word p >> 4 holds base p;
                                            // qw biased like q)
     const uint64_t *off; const uint2 *ent;        // CSR {pos - record start, record}, buckets in descending pos
+    bool ent_abs = false;                  // ... {pos, record}: the absolute form (ent_pos)
     const uint32_t *active; uint32_t n_active;
     uint64_t read_from, rpt, T;
     uint64_t qs_lo, qs_lo_first;          // q_start holds reads >= qs_lo (a shard upload); reads
@@ -60,6 +61,23 @@ struct SeedLaunch {
     unsigned long long *dbg;               // diagnostics (IMSAME_DEBUG_ROUNDS): reads per scan outcome
                                            // (seed_outcome), NULL: off
 };
+// An index entry's database position (the reference's pos, one past the
+// k-mer's last base, IMSAME.c:247) and its offset in the record.  The
+// absolute form (databases below 2^32 bases, imsame_dev.hip:kmer_scatter)
+// gives the position without the record's start, so a hit's first database
+// words load while its record bounds are still in flight.
+__device__ __forceinline__ int64_t ent_pos(const SeedLaunch &S, uint2 ent, int64_t xs) {
+    return S.ent_abs ? (int64_t)ent.x : xs + (int64_t)ent.x;
+}
+__device__ __forceinline__ int64_t ent_rel(const SeedLaunch &S, uint2 ent, int64_t xs) {
+    return S.ent_abs ? (int64_t)ent.x - xs : (int64_t)ent.x;
+}
+// ... the form fixed at compile time (the scan kernels: a select on the
+// launch's flag would make the position wait for the record's start anyway)
+template <bool ABS>
+__device__ __forceinline__ int64_t ent_pos_t(uint2 ent, int64_t xs) { return ABS ? (int64_t)ent.x : xs + (int64_t)ent.x; }
+template <bool ABS>
+__device__ __forceinline__ int64_t ent_rel_t(uint2 ent, int64_t xs) { return ABS ? (int64_t)ent.x - xs : (int64_t)ent.x; }
 // scan outcome classes of a read (diagnostics): no candidate + size error /
 // paused / done; candidates + size error / paused / exhausted / spec full
 #ifndef IMSAME_WAVE_EMU
@@ -215,38 +233,52 @@ __device__ __forceinline__ uint32_t ung_match16(uint32_t mism, int64_t n) {
     return (x | (x >> 4)) & 0x00FF00FFu;
 }
 
+// The first chunk of each direction of a hit's extension (ungapped_raw):
+// issued as soon as the hit's database position is known, before the
+// record's bounds arrive (index entries in the absolute form, SeedLaunch::ent_abs)
+struct UngFirst { uint32_t d0, d1, q0, q1, l0, l1, m0, m1; };
+__device__ __forceinline__ UngFirst ung_first(const uint32_t *__restrict__ db, const uint32_t *__restrict__ q,
+                                              int64_t pd0, int64_t pq0) {
+    UngFirst f;
+    f.d0 = db[pd0 >> 4]; f.d1 = db[(pd0 >> 4) + 1]; f.q0 = q[pq0 >> 4]; f.q1 = q[(pq0 >> 4) + 1];
+    // left walk: chunk = bases x-15 .. x (x = bx0 = pd0 - 13 first); it needs
+    // 15 bases below the start
+    const int64_t bx0 = pd0 - IMSAME_FIXED_K - 1, by0 = pq0 - IMSAME_FIXED_K - 1;
+    f.l0 = f.l1 = f.m0 = f.m1 = 0;
+    if (bx0 >= 15 && by0 >= 15) {
+        f.l0 = db[(bx0 - 15) >> 4]; f.l1 = db[((bx0 - 15) >> 4) + 1];
+        f.m0 = q[(by0 - 15) >> 4]; f.m1 = q[((by0 - 15) >> 4) + 1];
+    }
+    return f;
+}
+
 // alignmentFromQuickHits (alignmentFunctions.c:276-387): the raw score in the
 // reference's u64 wrap arithmetic (:373).  Loop bounds fold the reference's
 // per-step tests (:321-322, :344-345) into one limit per direction.  The
 // base-serial walk of the reference runs over 16-base chunks of the packed
 // buffers (one dword load per chunk and side, the mismatches of 16 bases from
 // one xor, two table rows per chunk: ung_half); the first chunk of each
-// direction is fetched before either walk starts.  tab: g_ung_tab (its LDS
-// copy in the scan kernels).
+// direction is fetched before either walk starts (f = ung_first(db, q, pd0,
+// pq0)).  tab: g_ung_tab (its LDS copy in the scan kernels).
 // (*nch, when given, counts the 16-base chunk pairs loaded)
-__device__ __forceinline__ uint64_t ungapped_raw(const uint16_t *__restrict__ tab, const uint32_t *__restrict__ db,
-                                                 const uint32_t *__restrict__ q, int64_t pd0, int64_t pq0, int64_t xs,
-                                                 int64_t xe, int64_t ys, int64_t ye, int64_t dbl, int64_t ql,
-                                                 uint32_t *nch = nullptr) {
+__device__ __forceinline__ uint64_t ungapped_walk(const uint16_t *__restrict__ tab, const uint32_t *__restrict__ db,
+                                                  const uint32_t *__restrict__ q, const UngFirst &f, int64_t pd0,
+                                                  int64_t pq0, int64_t xs, int64_t xe, int64_t ys, int64_t ye,
+                                                  int64_t dbl, int64_t ql, uint32_t *nch = nullptr) {
     int64_t end_x = pd0 - 1, beg_x = end_x - IMSAME_FIXED_K + 1;
     int sc = IMSAME_FIXED_K * IMSAME_POINT, best_r = sc, best_l = sc;
     uint32_t idents = IMSAME_FIXED_K;
     const int64_t bx0 = pd0 - IMSAME_FIXED_K - 1, by0 = pq0 - IMSAME_FIXED_K - 1;
-    const bool lwin = bx0 >= 15 && by0 >= 15;            // left chunks need 15 bases below the start
+    const bool lwin = bx0 >= 15 && by0 >= 15;
     // right walk: chunk = bases x .. x+15, words [x >> 4, (x >> 4) + 1];
     // word indices are recomputed from the positions (fewer live registers:
     // the scan kernels stay at 4 waves per SIMD, seed_group_kernel)
     const int64_t dq = pq0 - pd0;                        // y - x on the right walk
     const uint32_t dsh = 2u * (uint32_t)(pd0 & 15), qsh = 2u * (uint32_t)(pq0 & 15);
-    uint32_t d0 = db[pd0 >> 4], d1 = db[(pd0 >> 4) + 1], q0 = q[pq0 >> 4], q1 = q[(pq0 >> 4) + 1];
-    // left walk: chunk = bases x-15 .. x (x = bx0 = pd0 - 13 first), walked
-    // downwards (slot 15 first); its shifts are the right walk's + 8 bases
-    uint32_t l0 = 0, l1 = 0, m0 = 0, m1 = 0;
+    uint32_t d0 = f.d0, d1 = f.d1, q0 = f.q0, q1 = f.q1;
+    // left walk, downwards (slot 15 first); its shifts are the right walk's + 8 bases
+    uint32_t l0 = f.l0, l1 = f.l1, m0 = f.m0, m1 = f.m1;
     const uint32_t lsh = (dsh + 8u) & 31u, lqsh = (qsh + 8u) & 31u;
-    if (lwin) {
-        l0 = db[(bx0 - 15) >> 4]; l1 = db[((bx0 - 15) >> 4) + 1];
-        m0 = q[(by0 - 15) >> 4]; m1 = q[((by0 - 15) >> 4) + 1];
-    }
     uint32_t nc = lwin ? 2 : 1;
     const int64_t fx = min(min(dbl - 1, xe), pd0 + (min(ql - 1, ye) - pq0));
     // (steps past n are mismatches to the table: they come after the last
@@ -287,6 +319,12 @@ __device__ __forceinline__ uint64_t ungapped_raw(const uint16_t *__restrict__ ta
     if (nch) *nch += nc;
     const uint64_t t_len = (uint64_t)(end_x - beg_x);
     return (uint64_t)idents * IMSAME_POINT - (t_len - idents) * IMSAME_POINT;
+}
+__device__ __forceinline__ uint64_t ungapped_raw(const uint16_t *__restrict__ tab, const uint32_t *__restrict__ db,
+                                                 const uint32_t *__restrict__ q, int64_t pd0, int64_t pq0, int64_t xs,
+                                                 int64_t xe, int64_t ys, int64_t ye, int64_t dbl, int64_t ql,
+                                                 uint32_t *nch = nullptr) {
+    return ungapped_walk(tab, db, q, ung_first(db, q, pd0, pq0), pd0, pq0, xs, xe, ys, ye, dbl, ql, nch);
 }
 
 // a thread's scan work: hits extended, and for the seed roofline windows
@@ -355,6 +393,7 @@ __device__ __forceinline__ uint32_t spec_after_first(const SeedLaunch &S, uint32
     return (nm == 0 && S.spec_weak > spec && weak_hit(raw, ylen)) ? S.spec_weak : spec;
 }
 
+template <bool ABS>
 __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, SeedTally &tl, const uint16_t *tab) {
     const uint64_t r = S.active[idx], k = r - S.read_from;
     const uint64_t rs = S.q_start[r], re = S.q_start[r + 1];
@@ -423,7 +462,7 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, Seed
             const int64_t xs = (int64_t)S.db_start[sid];
             const int64_t xe = (sid == S.n_db - 1) ? (int64_t)S.db_len : (int64_t)S.db_start[sid + 1] - 1;
             ++tl.hits;
-            const uint64_t raw = ungapped_raw(tab, S.dbw, S.qw, xs + ent.x, (int64_t)p + 1, xs, xe, ys, ye,
+            const uint64_t raw = ungapped_raw(tab, S.dbw, S.qw, ent_pos_t<ABS>(ent, xs), (int64_t)p + 1, xs, xe, ys, ye,
                                               (int64_t)S.db_len, (int64_t)S.q_len, &tl.chunks);
             if (mraw != ~0ull && raw >= mraw) {                      // e < min_e (:139)
                 const uint64_t xlen = S.db_start[sid + 1] - S.db_start[sid];
@@ -434,7 +473,7 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, Seed
                 }
                 if (nw_cannot_accept(S, xlen, ylen)) continue;       // NW would reject it
                 if (ne == 0) {
-                    row0 = predicted_row(raw, ylen, ent.x, (int64_t)(p + 1 - rs), S.weak_rows);
+                    row0 = predicted_row(raw, ylen, ent_rel_t<ABS>(ent, xs), (int64_t)(p + 1 - rs), S.weak_rows);
                     spec = spec_after_first(S, spec, nm, raw, ylen);
                 }
                 emit[ne++] = sid;
@@ -512,7 +551,7 @@ __device__ __forceinline__ bool emit_has(const uint32_t (&em)[SM], uint32_t ne, 
 #define SEED_PREFETCH 0
 #endif
 // SM: the most candidates a read may emit (its list in LDS, emit[] in registers)
-template <int L, int SM = SPEC_MAX>
+template <int L, int SM = SPEC_MAX, bool ABS = true>
 __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane, uint2 *lst, SeedTally &tl,
                            const uint16_t *tab) {
     const bool gvalid = gidx < S.n_active;
@@ -577,12 +616,14 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
                 for (uint32_t m = 0; m < nm; ++m) skip |= S.memo[k * MEMO + m] == sid;
                 for (uint32_t m = 0; m < nl; ++m) skip |= lst[m].x == sid;
                 if (skip) continue;                       // NW(sid, r) rejected, pending or listed (Q18)
-                if (hit_irrelevant(S, S.db_start[sid + 1] - S.db_start[sid], ylen)) continue;
+                const int64_t xs = (int64_t)S.db_start[sid], xn = (int64_t)S.db_start[sid + 1];
+                const int64_t pd0 = ent_pos_t<ABS>(ent, xs);
+                const UngFirst f = ung_first(S.dbw, S.qw, pd0, (int64_t)pw + 1);
+                if (hit_irrelevant(S, (uint64_t)(xn - xs), ylen)) continue;
                 ++ev;
-                const int64_t xs = (int64_t)S.db_start[sid];
-                const int64_t xe = (sid == S.n_db - 1) ? (int64_t)S.db_len : (int64_t)S.db_start[sid + 1] - 1;
-                const uint64_t raw = ungapped_raw(tab, S.dbw, S.qw, xs + ent.x, (int64_t)pw + 1, xs, xe, ys, ye,
-                                                  (int64_t)S.db_len, (int64_t)S.q_len, &tl.chunks);
+                const int64_t xe = (sid == S.n_db - 1) ? (int64_t)S.db_len : xn - 1;
+                const uint64_t raw = ungapped_walk(tab, S.dbw, S.qw, f, pd0, (int64_t)pw + 1, xs, xe, ys, ye,
+                                                   (int64_t)S.db_len, (int64_t)S.q_len, &tl.chunks);
                 if (mraw != ~0ull && raw >= mraw) {                      // e < min_e (:139)
                     const uint64_t xlen = S.db_start[sid + 1] - S.db_start[sid];
                     const bool bad = xlen > S.max_rs || ylen > S.max_rs;   // terror (:155) if reached
@@ -669,9 +710,9 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
         const uint2 ent = S.ent[S.off[kmer_code_pk(S.qw, rs + e0p)] + e0r];
         const int64_t xs = (int64_t)S.db_start[ent.y];
         const int64_t xe = (ent.y == S.n_db - 1) ? (int64_t)S.db_len : (int64_t)S.db_start[ent.y + 1] - 1;
-        const uint64_t raw = ungapped_raw(tab, S.dbw, S.qw, xs + ent.x, (int64_t)(rs + e0p) + 1, xs, xe, ys, ye,
-                                          (int64_t)S.db_len, (int64_t)S.q_len);
-        S.crow[o] = predicted_row(raw, ylen, ent.x, (int64_t)e0p + 1, S.weak_rows);
+        const uint64_t raw = ungapped_raw(tab, S.dbw, S.qw, ent_pos_t<ABS>(ent, xs), (int64_t)(rs + e0p) + 1, xs, xe, ys,
+                                          ye, (int64_t)S.db_len, (int64_t)S.q_len);
+        S.crow[o] = predicted_row(raw, ylen, ent_rel_t<ABS>(ent, xs), (int64_t)e0p + 1, S.weak_rows);
         for (uint32_t m = 1; m < ne; ++m) S.crow[o + m] = INT32_MIN;
     }
     S.cbase[k] = o; S.ccnt[k] = ne;
@@ -702,7 +743,7 @@ __device__ __forceinline__ void accept_window_one(const SeedLaunch &S, const ims
         for (uint64_t e = S.off[code]; e < S.off[code + 1]; ++e) {
             const uint2 ent = S.ent[e];
             if (ent.y != sid) continue;
-            const uint64_t raw = ungapped_raw(g_ung_tab.v, S.dbw, S.qw, xs + ent.x, (int64_t)p + 1, xs, xe, ys, ye,
+            const uint64_t raw = ungapped_raw(g_ung_tab.v, S.dbw, S.qw, ent_pos(S, ent, xs), (int64_t)p + 1, xs, xe, ys, ye,
                                               (int64_t)S.db_len, (int64_t)S.q_len);
             if (mraw != ~0ull && raw >= mraw) { w = p; break; }
         }
@@ -816,7 +857,7 @@ __global__ void accept_window_kernel(const SeedLaunch S, const imsame_read_resul
 // Wave-stride over the groups (a launch may hold fewer waves than groups,
 // imsame_dev.hip:seed_blocks; a wave's groups are consecutive, so the loop's
 // exit is wave-uniform)
-template <int L, int SM = SPEC_MAX>
+template <int L, int SM = SPEC_MAX, bool ABS = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SM > SPEC_MAX ? 1 : SEED_WAVES_PER_EU)))
 void seed_group_kernel(SeedLaunch S) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -828,16 +869,17 @@ void seed_group_kernel(SeedLaunch S) {
     const uint32_t nwv = gridDim.x * (blockDim.x >> 6);
     SeedTally tl;
     for (uint32_t wv = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); (uint64_t)wv * GPW < S.n_active; wv += nwv)
-        seed_group<L, SM>(S, wv * GPW + (uint32_t)lane / L, wl, lane, lst, tl, tab);
+        seed_group<L, SM, ABS>(S, wv * GPW + (uint32_t)lane / L, wl, lane, lst, tl, tab);
     seed_tally_flush(S, tl);
 }
 
+template <bool ABS = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEED_WAVES_PER_EU))) void seed_kernel(SeedLaunch S) {
     __shared__ uint16_t tab[10 * 256];
     ung_tab_load(tab);
     SeedTally tl;
     for (uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x; idx < S.n_active; idx += gridDim.x * blockDim.x)
-        seed_one(S, idx, tl, tab);
+        seed_one<ABS>(S, idx, tl, tab);
     seed_tally_flush(S, tl);
 }
 

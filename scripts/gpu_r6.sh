@@ -67,9 +67,12 @@ run_step() {   # $1 = step, $2 = output suffix
             -- python3 bench.py --config c5w --steps 1 --warmup 0 --cpu-sample 0 > $O/bench_profc5w_${TAG}$X.json \
             2> $O/bench_profc5w_${TAG}$X.err; ok_or_stop $? profc5w$X ;;
     # PMC passes, one counter group per run, the program directly after `--`
-    pmc*) CFG=${s#pmc}; CFG=${CFG:-c2}; i=0
-         for grp in "SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_BUSY_CYCLES" \
-                    "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE"; do
+    # (sqpmc<cfg>: the SQ group only)
+    pmc*|sqpmc*) CFG=${s#sqpmc}; CFG=${CFG#pmc}; CFG=${CFG:-c2}; i=0
+         GRPS=("SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_BUSY_CYCLES" \
+               "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE")
+         [[ $s == sqpmc* ]] && GRPS=("${GRPS[0]}" "SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAIT_ANY")
+         for grp in "${GRPS[@]}"; do
            i=$((i+1))
            timeout -s KILL 400 rocprofv3 --pmc $grp --kernel-include-regex 'nw16_kernel|nw_kernel|nwl_kernel|nwp_kernel|seed_' -T \
              -d $O/pmc_${CFG}_${TAG}${X}_p$i -o pmc --output-format csv \

@@ -305,7 +305,7 @@ extern "C" int emu_nw_pairs(const uint8_t *xs, const uint64_t *x_start, const ui
 // host CSR with the device index's semantics (imsame_dev.hip: kmer_code_kernel,
 // kmer_scatter, segsort): buckets in descending pos
 static void build_csr(const uint8_t *db, uint64_t L, const uint64_t *dbs, uint64_t n_db, const uint8_t *brk_in,
-                      std::vector<uint64_t> &off, std::vector<uint2> &ent) {
+                      std::vector<uint64_t> &off, std::vector<uint2> &ent, bool abs) {
     std::vector<uint32_t> brk(L / 32 + 2, 0);
     if (brk_in) for (uint64_t b = 0; b < (L + 7) / 8; ++b) brk[b / 4] |= (uint32_t)brk_in[b] << (8 * (b % 4));
     for (uint64_t s = 0; s < n_db; ++s) if (dbs[s] < L) brk[dbs[s] >> 5] |= 1u << (dbs[s] & 31);
@@ -327,7 +327,7 @@ static void build_csr(const uint8_t *db, uint64_t L, const uint64_t *dbs, uint64
         if (code[p] == 0xFFFFFFFFu) continue;
         uint64_t lo = 0, hi = n_db;
         while (hi - lo > 1) { uint64_t m = (lo + hi) / 2; if (dbs[m] <= p) lo = m; else hi = m; }
-        ent[fill[code[p]]++] = uint2{(uint32_t)(p + 1 - dbs[lo]), (uint32_t)lo};
+        ent[fill[code[p]]++] = uint2{(uint32_t)(p + 1 - (abs ? 0 : dbs[lo])), (uint32_t)lo};
     }
 }
 
@@ -370,8 +370,12 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
     k2.insert(k2.end(), (const uint8_t *)dbs.data(), (const uint8_t *)(dbs.data() + dbs.size()));
     if (db_brk) k2.insert(k2.end(), db_brk, db_brk + (db_len + 7) / 8);
     k2.push_back(db_brk ? 1 : 0);
+    // the device's entry form (imsame_dev.hip:ent_abs_for)
+    const char *er = getenv("IMSAME_ENT_REL");
+    const bool ent_abs = !(er && atoi(er)) && db_len < 0xFFFFFFFFull;
+    k2.push_back(ent_abs ? 1 : 0);
     if (k2 != key || off.empty()) {
-        build_csr(db, db_len, dbs.data(), n_db, db_brk, off, ent);
+        build_csr(db, db_len, dbs.data(), n_db, db_brk, off, ent, ent_abs);
         key.swap(k2);
     }
     uint32_t max_rec = 0, ymax = 0;
@@ -414,7 +418,7 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
         S.q = q; S.q_start = qsv.data(); S.n_q = n_q; S.q_len = q_len;
         S.dbw = dbw.data(); S.qw = qw.data();
         S.qs_lo = read_from; S.qs_lo_first = qlo_first;
-        S.off = off.data(); S.ent = ent.data(); S.wcap = nullptr; S.wstart = nullptr;
+        S.off = off.data(); S.ent = ent.data(); S.ent_abs = ent_abs; S.wcap = nullptr; S.wstart = nullptr;
         S.active = act.data(); S.n_active = nact;
         S.read_from = read_from; S.T = T ? T : 1;
         S.rpt = (uint64_t)floorl((long double)n_q / (long double)S.T);
@@ -438,7 +442,7 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
             if (L <= 1) {
                 for (uint32_t i = 0; i < na; ++i) {
                     SeedTally tl;
-                    seed_one(SL, i, tl, g_ung_tab.v);
+                    if (SL.ent_abs) seed_one<true>(SL, i, tl, g_ung_tab.v); else seed_one<false>(SL, i, tl, g_ung_tab.v);
                     nhits += tl.hits; swin += tl.wins; sent += tl.ents; sch += tl.chunks;
                 }
             } else {                   // seed_group_kernel: 64-lane waves, several host threads
@@ -455,10 +459,14 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
                         run_wave([&](int lane) {
                             SeedTally h;
                             const uint32_t gidx = (uint32_t)((w0 + lane) / L);
-                            if (L == 64) seed_group<64, SPEC_BIG>(SL, gidx, lane, lane, ld + lane * SPEC_BIG, h, g_ung_tab.v);
-                            else if (L >= 16) seed_group<16>(SL, gidx, lane % 16, lane, ld + lane * SPEC_MAX, h, g_ung_tab.v);
-                            else if (L >= 4) seed_group<4>(SL, gidx, lane % 4, lane, ld + lane * SPEC_MAX, h, g_ung_tab.v);
-                            else         seed_group<2>(SL, gidx, lane % 2, lane, ld + lane * SPEC_MAX, h, g_ung_tab.v);
+                            if (L == 64) SL.ent_abs ? seed_group<64, SPEC_BIG, true>(SL, gidx, lane, lane, ld + lane * SPEC_BIG, h, g_ung_tab.v)
+                                         : seed_group<64, SPEC_BIG, false>(SL, gidx, lane, lane, ld + lane * SPEC_BIG, h, g_ung_tab.v);
+                            else if (L >= 16) SL.ent_abs ? seed_group<16, SPEC_MAX, true>(SL, gidx, lane % 16, lane, ld + lane * SPEC_MAX, h, g_ung_tab.v)
+                                         : seed_group<16, SPEC_MAX, false>(SL, gidx, lane % 16, lane, ld + lane * SPEC_MAX, h, g_ung_tab.v);
+                            else if (L >= 4) SL.ent_abs ? seed_group<4, SPEC_MAX, true>(SL, gidx, lane % 4, lane, ld + lane * SPEC_MAX, h, g_ung_tab.v)
+                                         : seed_group<4, SPEC_MAX, false>(SL, gidx, lane % 4, lane, ld + lane * SPEC_MAX, h, g_ung_tab.v);
+                            else         SL.ent_abs ? seed_group<2, SPEC_MAX, true>(SL, gidx, lane % 2, lane, ld + lane * SPEC_MAX, h, g_ung_tab.v)
+                                         : seed_group<2, SPEC_MAX, false>(SL, gidx, lane % 2, lane, ld + lane * SPEC_MAX, h, g_ung_tab.v);
                             wh += h.hits; ww += h.wins; we += h.ents; wc += h.chunks;
                         });
                     }

@@ -193,6 +193,21 @@ def test_synthetic_c2_shape_vs_oracle_all_T(dev, oracle):
     assert not _cmp(res32, res), _cmp(res32, res)
     res16, _, _ = dev.align(n_threads=16, params=dev.params(flags=FLAG_NW16))
     assert not _cmp(res16, res), _cmp(res16, res)
+    # the index's relative entry form (databases past 2^32 bases take it,
+    # seed_kernel.hip:ent_pos), with one lane per read and with groups
+    os.environ["IMSAME_ENT_REL"] = "1"
+    try:
+        dev.index(ref, rst)
+        for lanes in ("1", "4"):
+            os.environ["IMSAME_SEED_L"] = lanes
+            try:
+                resr, _, _ = dev.align(n_threads=16)
+            finally:
+                del os.environ["IMSAME_SEED_L"]
+            assert not _cmp(resr, res), (lanes, _cmp(resr, res))
+    finally:
+        del os.environ["IMSAME_ENT_REL"]
+        dev.index(ref, rst)
     # shards with the global chunk-head semantics equal the full run
     full, _, _ = dev.align(n_threads=8)
     parts = [dev.align(a, b, n_threads=8)[0] for a, b in ((0, 3001), (3001, 7777), (7777, 12_000))]

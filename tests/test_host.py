@@ -610,17 +610,20 @@ def test_emulated_pipeline_matches_oracle(emu, oracle, name, flags, monkeypatch)
             assert st.err_read == er
 
 
-@pytest.mark.parametrize("budget,lanes,spec,weak", [("1", "1", "8", "4"), ("3", "1", "1", "1"), ("0", "4", "8", "8"),
-                                                    ("3", "4", "2", "4"), ("1", "16", "8", "2"), ("0", "16", "1", "8"),
-                                                    ("0", "1", "1", "8"), ("1", "64", "8", "4"), ("3", "64", "2", "1")])
-def test_emulated_pipeline_seed_budget(emu, oracle, budget, lanes, spec, weak, monkeypatch):
+@pytest.mark.parametrize("budget,lanes,spec,weak,rel", [
+    ("1", "1", "8", "4", "0"), ("3", "1", "1", "1", "0"), ("0", "4", "8", "8", "0"), ("3", "4", "2", "4", "0"),
+    ("1", "16", "8", "2", "0"), ("0", "16", "1", "8", "0"), ("0", "1", "1", "8", "0"), ("1", "64", "8", "4", "0"),
+    ("3", "64", "2", "1", "0"), ("1", "1", "8", "4", "1"), ("3", "4", "2", "4", "1"), ("1", "64", "8", "4", "1")])
+def test_emulated_pipeline_seed_budget(emu, oracle, budget, lanes, spec, weak, rel, monkeypatch):
     """Reads that pause on the per-round hit budget resume at the same hit,
     the grouped scan (L lanes per read, seed_kernel.hip:seed_group) merges
     its windows in visiting order, and speculative candidates after a
     rejection (up to `spec` per read and round) or from a weak first
     candidate on (up to `weak`, seed_kernel.hip:spec_after_first) keep the
     first accepted one in visiting order: results equal the oracle's for
-    every budget (0 = none), group size and speculation width."""
+    every budget (0 = none), group size and speculation width, with the
+    index entries in either form (rel: IMSAME_ENT_REL, seed_kernel.hip:ent_pos)."""
+    monkeypatch.setenv("IMSAME_ENT_REL", rel)
     monkeypatch.setenv("IMSAME_SEED_BUDGET", budget)
     monkeypatch.setenv("IMSAME_SEED_L", lanes)
     monkeypatch.setenv("IMSAME_SPEC", spec)
