@@ -1735,21 +1735,20 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
         auto seed_launch = [&](const SeedLaunch &SL, uint32_t na, hipStream_t ss, hipEvent_t e0, hipEvent_t e1,
                                uint32_t rr = 0) -> int {
             const int L = RP.pick_L(rr ? rr : rnd, na);
-            const size_t slds = 256 * SEED_LDS_PER_LANE;
             // (IMSAME_SEED_BLOCKS: at most this many blocks, the kernels stride)
             auto sb = [&](uint64_t lanes) { return std::min<unsigned>(nblk(lanes, 256), seed_blocks()); };
             HIPCHK(hipEventRecord(e0, ss));
             if (SL.ent_abs) {
-                if (L >= 64)      seed_group_kernel<64, SPEC_BIG, true><<<sb((uint64_t)na * 64), 256, 256 * SPEC_BIG * 8, ss>>>(SL);
-                else if (L >= 16) seed_group_kernel<16, SPEC_MAX, true><<<sb((uint64_t)na * 16), 256, slds, ss>>>(SL);
-                else if (L >= 4)  seed_group_kernel<4, SPEC_MAX, true><<<sb((uint64_t)na * 4), 256, slds, ss>>>(SL);
-                else if (L >= 2)  seed_group_kernel<2, SPEC_MAX, true><<<sb((uint64_t)na * 2), 256, slds, ss>>>(SL);
+                if (L >= 64)      seed_group_kernel<64, SPEC_BIG, true><<<sb((uint64_t)na * 64), 256, SEED_LDS_BLOCK(64, SPEC_BIG), ss>>>(SL);
+                else if (L >= 16) seed_group_kernel<16, SPEC_MAX, true><<<sb((uint64_t)na * 16), 256, SEED_LDS_BLOCK(16, SPEC_MAX), ss>>>(SL);
+                else if (L >= 4)  seed_group_kernel<4, SPEC_MAX, true><<<sb((uint64_t)na * 4), 256, SEED_LDS_BLOCK(4, SPEC_MAX), ss>>>(SL);
+                else if (L >= 2)  seed_group_kernel<2, SPEC_MAX, true><<<sb((uint64_t)na * 2), 256, SEED_LDS_BLOCK(2, SPEC_MAX), ss>>>(SL);
                 else              seed_kernel<true><<<sb(na), 256, 0, ss>>>(SL);
             } else {
-                if (L >= 64)      seed_group_kernel<64, SPEC_BIG, false><<<sb((uint64_t)na * 64), 256, 256 * SPEC_BIG * 8, ss>>>(SL);
-                else if (L >= 16) seed_group_kernel<16, SPEC_MAX, false><<<sb((uint64_t)na * 16), 256, slds, ss>>>(SL);
-                else if (L >= 4)  seed_group_kernel<4, SPEC_MAX, false><<<sb((uint64_t)na * 4), 256, slds, ss>>>(SL);
-                else if (L >= 2)  seed_group_kernel<2, SPEC_MAX, false><<<sb((uint64_t)na * 2), 256, slds, ss>>>(SL);
+                if (L >= 64)      seed_group_kernel<64, SPEC_BIG, false><<<sb((uint64_t)na * 64), 256, SEED_LDS_BLOCK(64, SPEC_BIG), ss>>>(SL);
+                else if (L >= 16) seed_group_kernel<16, SPEC_MAX, false><<<sb((uint64_t)na * 16), 256, SEED_LDS_BLOCK(16, SPEC_MAX), ss>>>(SL);
+                else if (L >= 4)  seed_group_kernel<4, SPEC_MAX, false><<<sb((uint64_t)na * 4), 256, SEED_LDS_BLOCK(4, SPEC_MAX), ss>>>(SL);
+                else if (L >= 2)  seed_group_kernel<2, SPEC_MAX, false><<<sb((uint64_t)na * 2), 256, SEED_LDS_BLOCK(2, SPEC_MAX), ss>>>(SL);
                 else              seed_kernel<false><<<sb(na), 256, 0, ss>>>(SL);
             }
             POISON_SYNC(ss, "seed kernel", c);

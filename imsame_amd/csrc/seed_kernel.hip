@@ -525,6 +525,10 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, Seed
 // `budget` extensions; like seed_one's pauses they only reshape the work.
 // LDS: SEED_LDS_PER_LANE bytes per lane (the lane's list).
 #define SEED_LDS_PER_LANE (SPEC_MAX * 8)
+// ... and MEMO words per group after the lists (the read's memo, seed_group):
+// a launch of L lanes per read and SM list entries per lane takes
+// 256 * SM * 8 + (256 / L) * MEMO * 4 bytes of dynamic LDS per block
+#define SEED_LDS_BLOCK(L, SM) (256 * (SM) * 8 + (256 / (L)) * MEMO * 4)
 // list entry: {record, rank in the bucket | bit 31 size error | bit 30 weak hit}
 #define LST_RANK 0x3FFFFFFFu
 // lanes per read: enough lanes in flight to hide the probe latency
@@ -550,10 +554,12 @@ __device__ __forceinline__ bool emit_has(const uint32_t (&em)[SM], uint32_t ne, 
 #ifndef SEED_PREFETCH
 #define SEED_PREFETCH 0
 #endif
+// a record's bit in a read's memo filter (seed_group)
+__device__ __forceinline__ uint32_t memo_bit(uint32_t sid) { return 1u << ((sid * 0x9E3779B1u) >> 27); }
 // SM: the most candidates a read may emit (its list in LDS, emit[] in registers)
 template <int L, int SM = SPEC_MAX, bool ABS = true>
 __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane, uint2 *lst, SeedTally &tl,
-                           const uint16_t *tab) {
+                           const uint16_t *tab, uint32_t *gm) {
     const bool gvalid = gidx < S.n_active;
     const int gbase = lane - wl;                                  // first lane of the group
     uint64_t r = 0, k = 0, rs = 0, re = 0, ylen = 0, up_to = 0, p = 0;
@@ -578,6 +584,15 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
     uint32_t emit[SM];
 #pragma unroll
     for (int m = 0; m < SM; ++m) emit[m] = 0xFFFFFFFFu;
+    // The read's rejected records (memo): copied once into the group's LDS
+    // (gm, MEMO words) with a one-word filter of them, so an entry tests one
+    // register bit, and the LDS copy only where the bit is set, instead of
+    // nm dependent global loads per entry
+    if (gvalid)
+        for (uint32_t m = (uint32_t)wl; m < nm; m += L) gm[m] = S.memo[k * MEMO + m];
+    wv_lds_sync();
+    uint32_t mbloom = 0;
+    for (uint32_t m = 0; m < nm; ++m) mbloom |= memo_bit(gm[m]);
     uint32_t ne = 0, perr = 0, used = 0;
     uint32_t e0p = 0, e0r = 0;             // first candidate's window (read-relative) and bucket rank
     bool done = !gvalid || p >= up_to || read_irrelevant(S, ylen), paused = false,
@@ -613,7 +628,8 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
                 ++tl.ents;
                 const uint32_t sid = ent.y;
                 bool skip = emit_has(emit, ne, sid);
-                for (uint32_t m = 0; m < nm; ++m) skip |= S.memo[k * MEMO + m] == sid;
+                if (mbloom & memo_bit(sid))
+                    for (uint32_t m = 0; m < nm; ++m) skip |= gm[m] == sid;
                 for (uint32_t m = 0; m < nl; ++m) skip |= lst[m].x == sid;
                 if (skip) continue;                       // NW(sid, r) rejected, pending or listed (Q18)
                 const int64_t xs = (int64_t)S.db_start[sid], xn = (int64_t)S.db_start[sid + 1];
@@ -863,13 +879,14 @@ void seed_group_kernel(SeedLaunch S) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x & 63, wl = lane % L;
     uint2 *lst = (uint2 *)smem + threadIdx.x * SM;
+    uint32_t *gm = (uint32_t *)(smem + 256 * SM * 8) + (threadIdx.x / L) * MEMO;   // SEED_LDS_GROUP
     __shared__ uint16_t tab[10 * 256];
     ung_tab_load(tab);
     constexpr uint32_t GPW = 64 / L;                       // groups per wave
     const uint32_t nwv = gridDim.x * (blockDim.x >> 6);
     SeedTally tl;
     for (uint32_t wv = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); (uint64_t)wv * GPW < S.n_active; wv += nwv)
-        seed_group<L, SM, ABS>(S, wv * GPW + (uint32_t)lane / L, wl, lane, lst, tl, tab);
+        seed_group<L, SM, ABS>(S, wv * GPW + (uint32_t)lane / L, wl, lane, lst, tl, tab, gm);
     seed_tally_flush(S, tl);
 }
 

@@ -449,6 +449,7 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
                 const uint64_t nwaves = ((uint64_t)na * L + 63) / 64;
                 const int nt = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)emu_threads(), nwaves));
                 std::vector<uint2> lds((size_t)nt * 64 * SPEC_BIG);
+                std::vector<uint32_t> gms((size_t)nt * 64 * MEMO);
                 std::atomic<unsigned long long> wh{0}, ww{0}, we{0}, wc{0};
                 std::atomic<uint64_t> next_wave{0};
                 std::vector<std::thread> th;
@@ -456,17 +457,18 @@ extern "C" int emu_align(const uint8_t *db, uint64_t db_len, const uint64_t *db_
                     for (uint64_t wv; (wv = next_wave++) < nwaves;) {
                         const uint64_t w0 = wv * 64;
                         uint2 *ld = lds.data() + (size_t)t * 64 * SPEC_BIG;
+                        uint32_t *gmw = gms.data() + (size_t)t * 64 * MEMO;
                         run_wave([&](int lane) {
                             SeedTally h;
                             const uint32_t gidx = (uint32_t)((w0 + lane) / L);
-                            if (L == 64) SL.ent_abs ? seed_group<64, SPEC_BIG, true>(SL, gidx, lane, lane, ld + lane * SPEC_BIG, h, g_ung_tab.v)
-                                         : seed_group<64, SPEC_BIG, false>(SL, gidx, lane, lane, ld + lane * SPEC_BIG, h, g_ung_tab.v);
-                            else if (L >= 16) SL.ent_abs ? seed_group<16, SPEC_MAX, true>(SL, gidx, lane % 16, lane, ld + lane * SPEC_MAX, h, g_ung_tab.v)
-                                         : seed_group<16, SPEC_MAX, false>(SL, gidx, lane % 16, lane, ld + lane * SPEC_MAX, h, g_ung_tab.v);
-                            else if (L >= 4) SL.ent_abs ? seed_group<4, SPEC_MAX, true>(SL, gidx, lane % 4, lane, ld + lane * SPEC_MAX, h, g_ung_tab.v)
-                                         : seed_group<4, SPEC_MAX, false>(SL, gidx, lane % 4, lane, ld + lane * SPEC_MAX, h, g_ung_tab.v);
-                            else         SL.ent_abs ? seed_group<2, SPEC_MAX, true>(SL, gidx, lane % 2, lane, ld + lane * SPEC_MAX, h, g_ung_tab.v)
-                                         : seed_group<2, SPEC_MAX, false>(SL, gidx, lane % 2, lane, ld + lane * SPEC_MAX, h, g_ung_tab.v);
+                            if (L == 64) SL.ent_abs ? seed_group<64, SPEC_BIG, true>(SL, gidx, lane, lane, ld + lane * SPEC_BIG, h, g_ung_tab.v, gmw + (lane / L) * MEMO)
+                                         : seed_group<64, SPEC_BIG, false>(SL, gidx, lane, lane, ld + lane * SPEC_BIG, h, g_ung_tab.v, gmw + (lane / L) * MEMO);
+                            else if (L >= 16) SL.ent_abs ? seed_group<16, SPEC_MAX, true>(SL, gidx, lane % 16, lane, ld + lane * SPEC_MAX, h, g_ung_tab.v, gmw + (lane / L) * MEMO)
+                                         : seed_group<16, SPEC_MAX, false>(SL, gidx, lane % 16, lane, ld + lane * SPEC_MAX, h, g_ung_tab.v, gmw + (lane / L) * MEMO);
+                            else if (L >= 4) SL.ent_abs ? seed_group<4, SPEC_MAX, true>(SL, gidx, lane % 4, lane, ld + lane * SPEC_MAX, h, g_ung_tab.v, gmw + (lane / L) * MEMO)
+                                         : seed_group<4, SPEC_MAX, false>(SL, gidx, lane % 4, lane, ld + lane * SPEC_MAX, h, g_ung_tab.v, gmw + (lane / L) * MEMO);
+                            else         SL.ent_abs ? seed_group<2, SPEC_MAX, true>(SL, gidx, lane % 2, lane, ld + lane * SPEC_MAX, h, g_ung_tab.v, gmw + (lane / L) * MEMO)
+                                         : seed_group<2, SPEC_MAX, false>(SL, gidx, lane % 2, lane, ld + lane * SPEC_MAX, h, g_ung_tab.v, gmw + (lane / L) * MEMO);
                             wh += h.hits; ww += h.wins; we += h.ents; wc += h.chunks;
                         });
                     }
