@@ -349,27 +349,33 @@ __device__ __forceinline__ bool is_chunk_head(const SeedLaunch &S, uint64_t r, u
 // min(xlen, ylen) (build_alignment counts equal X/Y characters, each X and Y
 // base at most once, :254-258).  Such a hit is rejected without running NW --
 // the reference runs it and rejects it (C5: 10 kbp reads vs 2 kbp records).
-__device__ __forceinline__ bool nw_cannot_accept(const SeedLaunch &S, uint64_t xlen, uint64_t ylen) {
-    if (!S.minlen || ylen >= S.n_minlen) return false;
+// The test per read: NW(record, read) cannot be accepted iff
+// accept_floor(S, ylen) > min(xlen, ylen) (the scans compute the floor once
+// per read: two dependent table loads fewer per hit)
+__device__ __forceinline__ uint64_t accept_floor(const SeedLaunch &S, uint64_t ylen) {
+    if (!S.minlen || ylen >= S.n_minlen) return 0;
     uint32_t l0 = S.minlen[ylen];
-    if (l0 == 0xFFFFFFFFu) return true;
+    if (l0 == 0xFFFFFFFFu) return ~0ull;
     l0 = l0 ? l0 : 1u;                                    // minident[0] never passes
-    if (l0 >= S.n_minident) return true;                  // longer than any path
+    if (l0 >= S.n_minident) return ~0ull;                 // longer than any path
     const uint32_t mi = S.minident[l0];
-    return mi == 0xFFFFFFFFu || (uint64_t)mi > (xlen < ylen ? xlen : ylen);
+    return mi == 0xFFFFFFFFu ? ~0ull : (uint64_t)mi;
+}
+__device__ __forceinline__ bool nw_cannot_accept(uint64_t floor, uint64_t xlen, uint64_t ylen) {
+    return floor > (xlen < ylen ? xlen : ylen);
 }
 
 // A hit whose record cannot be accepted for this read AND cannot trip the
 // size abort (both lengths within max_read_size) has no observable effect
 // whatever its e-value: the reference would extend it and either fail the
 // e-value test or run an NW it then rejects.  Skipped before the extension.
-__device__ __forceinline__ bool hit_irrelevant(const SeedLaunch &S, uint64_t xlen, uint64_t ylen) {
-    return xlen <= S.max_rs && ylen <= S.max_rs && nw_cannot_accept(S, xlen, ylen);
+__device__ __forceinline__ bool hit_irrelevant(const SeedLaunch &S, uint64_t floor, uint64_t xlen, uint64_t ylen) {
+    return xlen <= S.max_rs && ylen <= S.max_rs && nw_cannot_accept(floor, xlen, ylen);
 }
 // ... and when even the longest record cannot accept the read, nothing the
 // read's scan meets can: its outcome is "not found" without a scan.
-__device__ __forceinline__ bool read_irrelevant(const SeedLaunch &S, uint64_t ylen) {
-    return S.max_rec <= S.max_rs && hit_irrelevant(S, S.max_rec, ylen);
+__device__ __forceinline__ bool read_irrelevant(const SeedLaunch &S, uint64_t floor, uint64_t ylen) {
+    return S.max_rec <= S.max_rs && hit_irrelevant(S, floor, S.max_rec, ylen);
 }
 
 // The first candidate of a read predicts its NW path (nw16_kernel.hip's
@@ -415,7 +421,8 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, Seed
     for (int m = 0; m < MEMO; ++m) memo[m] = (m < (int)nm) ? S.memo[k * MEMO + m] : 0xFFFFFFFFu;
     const uint64_t mraw = ylen < S.n_minraw ? S.minraw[ylen] : ~0ull;
     const int64_t ys = (int64_t)rs, ye = (r == S.n_q - 1) ? (int64_t)S.q_len : (int64_t)re - 1;
-    if (read_irrelevant(S, ylen)) { S.rstat[k] = RS_DONE; return; }      // nothing can be accepted
+    const uint64_t afl = accept_floor(S, ylen);
+    if (read_irrelevant(S, afl, ylen)) { S.rstat[k] = RS_DONE; return; }      // nothing can be accepted
     // Up to `spec` e-value-passing hits of distinct, not-yet-rejected records,
     // in visiting order.  NW(record, read) is pure (Q18): whichever of them is
     // accepted first in this order is exactly the reference's accepted hit,
@@ -452,7 +459,7 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, Seed
             for (int m = 0; m < MEMO; ++m) skip |= memo[m] == sid;
             for (uint32_t m = 0; m < ne; ++m) skip |= emit[m] == sid;
             if (skip) continue;                 // NW(sid, r) already rejected or pending (Q18)
-            if (hit_irrelevant(S, S.db_start[sid + 1] - S.db_start[sid], ylen)) continue;
+            if (hit_irrelevant(S, afl, S.db_start[sid + 1] - S.db_start[sid], ylen)) continue;
             if (budget == 0) {
                 S.cur_p[k] = p; S.cur_h[k] = h;                      // resume at this hit
                 paused = stop = true;
@@ -471,7 +478,7 @@ __device__ __forceinline__ void seed_one(const SeedLaunch &S, uint32_t idx, Seed
                     stop = true;
                     break;
                 }
-                if (nw_cannot_accept(S, xlen, ylen)) continue;       // NW would reject it
+                if (nw_cannot_accept(afl, xlen, ylen)) continue;     // NW would reject it
                 if (ne == 0) {
                     row0 = predicted_row(raw, ylen, ent_rel_t<ABS>(ent, xs), (int64_t)(p + 1 - rs), S.weak_rows);
                     spec = spec_after_first(S, spec, nm, raw, ylen);
@@ -564,7 +571,7 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
     const int gbase = lane - wl;                                  // first lane of the group
     uint64_t r = 0, k = 0, rs = 0, re = 0, ylen = 0, up_to = 0, p = 0;
     uint32_t h = 0, nm = 0, spec = 1, budget = 0xFFFFFFFFu;
-    uint64_t mraw = ~0ull;
+    uint64_t mraw = ~0ull, afl = 0;
     int64_t ys = 0, ye = 0;
     if (gvalid) {
         r = S.active[gidx]; k = r - S.read_from;
@@ -579,6 +586,7 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
         spec = nm ? S.spec : 1u;
         budget = S.budget ? S.budget : 0xFFFFFFFFu;
         mraw = ylen < S.n_minraw ? S.minraw[ylen] : ~0ull;
+        afl = accept_floor(S, ylen);
         ys = (int64_t)rs; ye = (r == S.n_q - 1) ? (int64_t)S.q_len : (int64_t)re - 1;
     }
     uint32_t emit[SM];
@@ -595,7 +603,7 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
     for (uint32_t m = 0; m < nm; ++m) mbloom |= memo_bit(gm[m]);
     uint32_t ne = 0, perr = 0, used = 0;
     uint32_t e0p = 0, e0r = 0;             // first candidate's window (read-relative) and bucket rank
-    bool done = !gvalid || p >= up_to || read_irrelevant(S, ylen), paused = false,
+    bool done = !gvalid || p >= up_to || read_irrelevant(S, afl, ylen), paused = false,
          exhausted = gvalid && p >= up_to;
     // The CSR bounds of a lane's window are loaded one window ahead (SEED_PREFETCH):
     // the bucket offsets of the window the lane scans next (p + L + wl, if the
@@ -623,8 +631,12 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
                 wbase = S.off[code]; hi = S.off[code + 1];
             }
             ++tl.wins;
-            for (uint64_t e = wbase + (wl == 0 ? h : 0u); e < hi; ++e) {
-                const uint2 ent = S.ent[e];
+            // (the next entry is loaded while this one's extension runs)
+            uint64_t e = wbase + (wl == 0 ? h : 0u);
+            uint2 ent_nx = e < hi ? S.ent[e] : make_uint2(0u, 0u);
+            for (; e < hi; ++e) {
+                const uint2 ent = ent_nx;
+                if (e + 1 < hi) ent_nx = S.ent[e + 1];
                 ++tl.ents;
                 const uint32_t sid = ent.y;
                 bool skip = emit_has(emit, ne, sid);
@@ -635,7 +647,7 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
                 const int64_t xs = (int64_t)S.db_start[sid], xn = (int64_t)S.db_start[sid + 1];
                 const int64_t pd0 = ent_pos_t<ABS>(ent, xs);
                 const UngFirst f = ung_first(S.dbw, S.qw, pd0, (int64_t)pw + 1);
-                if (hit_irrelevant(S, (uint64_t)(xn - xs), ylen)) continue;
+                if (hit_irrelevant(S, afl, (uint64_t)(xn - xs), ylen)) continue;
                 ++ev;
                 const int64_t xe = (sid == S.n_db - 1) ? (int64_t)S.db_len : xn - 1;
                 const uint64_t raw = ungapped_walk(tab, S.dbw, S.qw, f, pd0, (int64_t)pw + 1, xs, xe, ys, ye,
@@ -643,7 +655,7 @@ __device__ void seed_group(const SeedLaunch &S, uint32_t gidx, int wl, int lane,
                 if (mraw != ~0ull && raw >= mraw) {                      // e < min_e (:139)
                     const uint64_t xlen = S.db_start[sid + 1] - S.db_start[sid];
                     const bool bad = xlen > S.max_rs || ylen > S.max_rs;   // terror (:155) if reached
-                    if (!bad && nw_cannot_accept(S, xlen, ylen)) continue; // NW would reject it
+                    if (!bad && nw_cannot_accept(afl, xlen, ylen)) continue; // NW would reject it
                     lst[nl++] = make_uint2(sid, (uint32_t)(e - wbase) | (bad ? 0x80000000u : 0u) |
                                                     (weak_hit(raw, ylen) ? 0x40000000u : 0u));
                     last_rel = (uint32_t)(e - wbase);
