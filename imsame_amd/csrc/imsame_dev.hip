@@ -315,6 +315,11 @@ struct imsame_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     // round 1b (align_one): a second stream and event pair, created on first use
     hipStream_t stream_b = nullptr;
+    // ... the same at the device's highest stream priority, for calls whose
+    // second pipeline (weak reads' rounds) carried more NW than the first in
+    // this lane's previous call (b_prio; align_one swaps it in as stream_b)
+    hipStream_t stream_bh = nullptr;
+    bool b_prio = false;
     hipEvent_t evb0 = nullptr, evb1 = nullptr;
     // wait events (IMSAME_WAIT block / yield, lane_sync): [0] a stream's
     // queued work, [1] the end of an NW launch; per queue (stream, stream_b)
@@ -647,9 +652,12 @@ extern "C" int imsame_dev_open(int device, imsame_ctx **out) {
     // share the hardware queues the runtime has left (created here, not in a
     // call: creating one while other lanes run stalled a CLI call for 4.8 s,
     // profiles/r3r_*)
+    int prio_lo = 0, prio_hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) rc = IMSAME_E_HIP;
     for (size_t k = 0; k <= c->subs.size() && !rc; ++k) {
         imsame_ctx *l = k ? c->subs[k - 1] : c;
         if (hipStreamCreateWithFlags(&l->stream_b, hipStreamNonBlocking) != hipSuccess ||
+            hipStreamCreateWithPriority(&l->stream_bh, hipStreamNonBlocking, prio_hi) != hipSuccess ||
             hipEventCreate(&l->evb0) != hipSuccess || hipEventCreate(&l->evb1) != hipSuccess ||
             hipEventCreateWithFlags(&l->evw[1][0], hipEventBlockingSync | hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&l->evw[1][1], hipEventBlockingSync | hipEventDisableTiming) != hipSuccess)
@@ -694,6 +702,7 @@ extern "C" void imsame_dev_close(imsame_ctx *c) {
     for (auto &q : c->evw)
         for (hipEvent_t e : q) if (e) (void)hipEventDestroy(e);
     if (c->stream_b) (void)hipStreamDestroy(c->stream_b);
+    if (c->stream_bh) (void)hipStreamDestroy(c->stream_bh);
     if (c->origin && !c->is_sub) (void)hipEventDestroy(c->origin);     // a lane borrows its parent's
     if (!c->is_sub)
         for (hipEvent_t e : c->q_part_ev) (void)hipEventDestroy(e);
@@ -1151,6 +1160,18 @@ static bool pipes_on(uint64_t n) {
     const char *e = getenv("IMSAME_PIPES");
     return e ? atoi(e) != 0 : n >= 200000;
 }
+// The second pipeline at high priority (stream_bh): IMSAME_PRIO_B=0 never,
+// 1 always, unset: where this lane's previous pipelined call ran more NW
+// candidates in the second pipeline than in the first (c->b_prio).  Then
+// the weak reads' chain of rounds is the call's critical path and takes the
+// wave slots its launches free first, while the first pipeline's big round-1
+// launch fills the rest (C3: 350.5 -> 341.5-343.8 ms; at C2 the first
+// pipeline's launch is the long one, and priority for the second made it
+// 97.0 -> 98.2 ms, profiles/r6p2/).
+static bool prio_b(const imsame_ctx *c) {
+    const char *e = getenv("IMSAME_PRIO_B");
+    return c->stream_bh && (e ? atoi(e) != 0 : c->b_prio);
+}
 static int nw16_k(imsame_ctx *c, uint32_t ncand, bool rounds) {
     const char *e = getenv("IMSAME_NW_K"), *fe = getenv("IMSAME_NW_K5_FILL"), *f2 = getenv("IMSAME_NW_K5_FILL2");
     const int force = e ? atoi(e) : 0;
@@ -1598,6 +1619,12 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     const uint32_t n = (uint32_t)(read_to - read_from);
+    // the second pipeline's stream for this call (prio_b), back at return
+    struct StreamSwap {
+        imsame_ctx *c; bool on;
+        ~StreamSwap() { if (on) std::swap(c->stream_b, c->stream_bh); }
+    } swap_b{c, pipes_on(n) && prio_b(c)};
+    if (swap_b.on) std::swap(c->stream_b, c->stream_bh);
     // this lane's bases (and the 16-byte chunk loads' reach past its last read)
     if (int rq = query_wait(c, s, hqs(c, read_to) + 64)) return rq;
     imsame_stats st;
@@ -2123,6 +2150,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
             thB.join();
             if (rcA) return rcA;
             if (rcB) return rcB;
+            c->b_prio = stB.n_nw > st.n_nw;             // for the next call (prio_b)
             // one stats record: B's launches after A's
             st.rounds = std::max(A.rnd, B.rnd);
             st.ms_seed += stB.ms_seed;
