@@ -400,6 +400,7 @@ struct imsame_ctx {
     // NW launch intervals (ms since the call's origin event) for the busy time
     hipEvent_t origin = nullptr;
     hipEvent_t ev_w = nullptr;        // align_one: round 1's unpredicted candidates updated (pipelines)
+    hipEvent_t ev_wd = nullptr;       // align_one: the weak launch and its update ended (pipelines)
     std::vector<std::pair<float, float>> nw_iv;
     // IMSAME_DEBUG_TIMELINE: (kind 'S' seed / 'N' NW, round, items, start, end)
     struct TlEv { char kind; int round; uint32_t n; float a, b; };
@@ -654,10 +655,12 @@ extern "C" int imsame_dev_open(int device, imsame_ctx **out) {
     // profiles/r3r_*)
     int prio_lo = 0, prio_hi = 0;
     if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) rc = IMSAME_E_HIP;
+    const char *pbe = getenv("IMSAME_PRIO_B");
+    const bool no_bh = pbe && !atoi(pbe);         // (prio_b off: no high-priority streams at all)
     for (size_t k = 0; k <= c->subs.size() && !rc; ++k) {
         imsame_ctx *l = k ? c->subs[k - 1] : c;
         if (hipStreamCreateWithFlags(&l->stream_b, hipStreamNonBlocking) != hipSuccess ||
-            hipStreamCreateWithPriority(&l->stream_bh, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+            (!no_bh && hipStreamCreateWithPriority(&l->stream_bh, hipStreamNonBlocking, prio_hi) != hipSuccess) ||
             hipEventCreate(&l->evb0) != hipSuccess || hipEventCreate(&l->evb1) != hipSuccess ||
             hipEventCreateWithFlags(&l->evw[1][0], hipEventBlockingSync | hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&l->evw[1][1], hipEventBlockingSync | hipEventDisableTiming) != hipSuccess)
@@ -698,6 +701,7 @@ extern "C" void imsame_dev_close(imsame_ctx *c) {
     (void)hipEventDestroy(c->ev1);
     if (c->evb0) (void)hipEventDestroy(c->evb0);
     if (c->ev_w) (void)hipEventDestroy(c->ev_w);
+    if (c->ev_wd) (void)hipEventDestroy(c->ev_wd);
     if (c->evb1) (void)hipEventDestroy(c->evb1);
     for (auto &q : c->evw)
         for (hipEvent_t e : q) if (e) (void)hipEventDestroy(e);
@@ -2075,7 +2079,14 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
             uint32_t nw = 0;
             const uint32_t *pm = nullptr;
             auto w_done = [&](int v) { { std::lock_guard<std::mutex> g(wmu); wstate = v; } wcv.notify_all(); };
+            // ... and B hands A the end of the weak launch back through wdstate
+            // (1: ev_wd recorded after its update, -1: B failed): the weak launch
+            // and its update read the cut (pm = A's cperm), which A's next
+            // launches rewrite with their own row order
+            int wdstate = 0;
+            auto wd_done = [&](int v) { { std::lock_guard<std::mutex> g(wmu); wdstate = v; } wcv.notify_all(); };
             if (!c->ev_w) HIPCHK(hipEventCreateWithFlags(&c->ev_w, hipEventDisableTiming));
+            if (!c->ev_wd) HIPCHK(hipEventCreateWithFlags(&c->ev_wd, hipEventDisableTiming));
             // (B.act: round 1b's active list, act1; its update appends to B.nxt,
             // act2, where the 1b scan put the reads it paused -- round 2's list)
             Pipe B = {sb, 1, c->evb0, c->evb1, nxt, c->act2.as<uint32_t>(), 0, n1, ccap - n1, C_NCANDB, C_WORKB, 1};
@@ -2100,7 +2111,9 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
                         NwPlan plw;
                         if (int r = plan_nw(c, short_y, xcap, nw, p, c->q_len_mult, &plw, true, c->q_len_uni)) return r;
                         if (int r = pipe_nw(W, stB, plw, nw, crow, pm, c->act2.as<uint32_t>(), C_NNEXT2)) return r;
+                        HIPCHK(hipEventRecord(c->ev_wd, sb));
                     }
+                    wd_done(1);
                     if (hb[1]) return IMSAME_E_STATE;
                     const uint32_t nb = (uint32_t)hb[0];
                     if (nb) {
@@ -2115,6 +2128,7 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
                     std::swap(B.act, B.nxt);             // round 2 scans act2; act1 is free
                     return pipe_rounds(B, stB);
                 }();
+                if (!wdstate) wd_done(-1);               // (B failed before the weak launch ended)
             });
             // A, on this thread: the cut, round 1's predicted candidates' launch
             // + update (its next list: act3; C_NNEXT held round 1's paused
@@ -2144,6 +2158,12 @@ static int align_one(imsame_ctx *c, uint64_t read_from, uint64_t read_to, uint64
                 HIPCHK(hipMemcpyAsync(&nn, ctr + C_NNEXT, 8, hipMemcpyDeviceToHost, s));
                 LANE_SYNC(c, s);
                 A.nact = (uint32_t)nn;
+                if (nw && A.nact) {                      // A's next launches rewrite cperm
+                    std::unique_lock<std::mutex> g(wmu);
+                    wcv.wait(g, [&] { return wdstate != 0; });
+                    if (wdstate < 0) return IMSAME_E_STATE;   // B failed: B reports it
+                    HIPCHK(hipStreamWaitEvent(s, c->ev_wd, 0));
+                }
                 return pipe_rounds(A, st);
             }();
             if (!wstate) w_done(-1);                     // (A failed before its first launch)
